@@ -1,0 +1,73 @@
+"""Shared test helpers: build oracle states from golden/synthetic problems."""
+from collections import OrderedDict
+
+import numpy as np
+
+from oracle import msckf_oracle as O
+
+
+def oracle_state_from_arrays(d, sigma2=0.035 ** 2, Qc=None):
+    """``d`` holds the keys written by tools/gen_golden.py:problem_arrays (or
+    an UpdateProblem converted with ``problem_to_dict``)."""
+    imu = O.ImuState(q=d["imu_q"].copy(), p=d["imu_p"].copy(), v=d["imu_v"].copy(),
+                     bg=d["imu_bg"].copy(), ba=d["imu_ba"].copy(), q_null=d["imu_q_null"].copy(),
+                     R_imu_cam0=d["imu_R_imu_cam0"].copy(), t_cam0_imu=d["imu_t_cam0_imu"].copy())
+    cams = OrderedDict()
+    for i in range(int(d["N"])):
+        cams[i] = O.CamState(i, float(i), d["cam_q"][i].copy(), d["cam_p"][i].copy(),
+                             d["cam_q_null"][i].copy())
+    if Qc is None:
+        Qc = np.diag([0.005 ** 2] * 3 + [0.001 ** 2] * 3 + [0.05 ** 2] * 3 + [0.01 ** 2] * 3)
+    return O.FilterState(imu, cams, d["P"].copy(), d["gravity"].copy(), d["R_cam0_cam1"],
+                         d["t_cam0_cam1"], Qc, sigma2)
+
+
+def problem_to_dict(pr):
+    d = dict(N=pr.N, F=pr.F, cam_q=pr.cam_q, cam_p=pr.cam_p, cam_q_null=pr.cam_q_null,
+             P=pr.P, gravity=pr.gravity, R_cam0_cam1=pr.R_cam0_cam1, t_cam0_cam1=pr.t_cam0_cam1,
+             obs_off=pr.obs_off, obs_cam=pr.obs_cam, obs_z=pr.obs_z)
+    for k, v in pr.imu.items():
+        d["imu_" + k] = v
+    return d
+
+
+def feature_obs(d, f):
+    a, b = int(d["obs_off"][f]), int(d["obs_off"][f + 1])
+    return [(int(c), d["obs_z"][r]) for r, c in zip(range(a, b), d["obs_cam"][a:b])]
+
+
+def oracle_update(d, row_cap=None, triangulate=True):
+    """Oracle restatement of the synthetic update: triangulate, jacobian,
+    gate (dof = M-1, the lost-feature path), stack, EKF update.
+    Returns (state, accept flags, tri positions, tri ok, gammas)."""
+    st = oracle_state_from_arrays(d)
+    F = int(d["F"])
+    tri_p = np.zeros((F, 3))
+    tri_ok = np.zeros(F, bool)
+    gam = np.full(F, np.nan)
+    acc = np.zeros(F, bool)
+    Hs, rs = [], []
+    count = 0
+    from msckf_amd import chi2_threshold
+    for f in range(F):
+        obs = feature_obs(d, f)
+        if triangulate:
+            p, ok, _ = O.triangulate(OrderedDict(obs), st.cams, st.R_cam0_cam1, st.t_cam0_cam1)
+        else:
+            p, ok = d["tri_p"][f], bool(d["tri_ok"][f])
+        tri_p[f], tri_ok[f] = p, ok
+        if not ok:
+            continue
+        H, r = O.feature_jacobian(st, p, obs)
+        g = O.gating_gamma(st, H, r)
+        gam[f] = g
+        if g < chi2_threshold(len(obs) - 1):
+            acc[f] = True
+            Hs.append(H)
+            rs.append(r)
+            count += H.shape[0]
+        if row_cap is not None and count > row_cap:
+            break
+    if Hs:
+        O.measurement_update(st, np.vstack(Hs), np.concatenate(rs))
+    return st, acc, tri_p, tri_ok, gam

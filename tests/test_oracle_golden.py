@@ -1,0 +1,151 @@
+"""The CPU oracle (oracle/msckf_oracle.py) pinned to golden vectors produced
+by running the reference filter itself (tools/gen_golden.py).  CPU only."""
+from collections import OrderedDict
+
+import numpy as np
+
+from conftest import golden, rel
+from helpers import oracle_state_from_arrays, feature_obs
+from oracle import msckf_oracle as O
+from msckf_amd import CHI2_05, geometry
+
+
+def test_math_helpers():
+    g = golden("math")
+    for i in range(len(g["qs"])):
+        np.testing.assert_allclose(O.to_rotation(g["qs"][i]), g["to_rotation"][i], rtol=0, atol=1e-15)
+        np.testing.assert_allclose(O.to_quaternion(g["to_rotation"][i]), g["to_quaternion"][i], atol=1e-15)
+        np.testing.assert_allclose(O.quaternion_multiplication(g["qs"][i], g["qs2"][i]), g["quat_mult"][i], atol=1e-15)
+        np.testing.assert_allclose(O.small_angle_quaternion(g["dtheta"][i]), g["small_angle"][i], atol=1e-15)
+        np.testing.assert_allclose(O.from_two_vectors(g["v0"][i], g["v1"][i]), g["from_two_vectors"][i], atol=1e-15)
+        # the package's host-side helpers agree too
+        np.testing.assert_allclose(geometry.to_rotation(g["qs"][i]), g["to_rotation"][i], atol=1e-15)
+        np.testing.assert_allclose(geometry.to_quaternion(g["to_rotation"][i]), g["to_quaternion"][i], atol=1e-15)
+        np.testing.assert_allclose(geometry.from_two_vectors(g["v0"][i], g["v1"][i]), g["from_two_vectors"][i], atol=1e-15)
+    assert tuple(g["chi2"]) == CHI2_05
+
+
+def test_process_model():
+    g = golden("process_model")
+    n = len(g["cam_q"])
+    cams = OrderedDict((i, O.CamState(i, 0.0, g["cam_q"][i], g["cam_p"][i], g["cam_q_null"][i])) for i in range(n))
+    imu = O.ImuState(q=g["init_q"].copy(), v=g["init_v"].copy(), p=g["init_p"].copy(),
+                     bg=g["init_bg"].copy(), ba=g["init_ba"].copy(), q_null=g["init_q_null"].copy(),
+                     nulls_alias=True, R_imu_cam0=g["R_imu_cam0"], t_cam0_imu=g["t_cam0_imu"], timestamp=float(g["t0"]))
+    st = O.FilterState(imu, cams, g["init_P"].copy(), g["gravity"], np.eye(3), np.zeros(3), g["Qc"], 0.035 ** 2)
+    F, G, Phi = O.process_model_matrices(g["gyro"][0] - imu.bg, O.to_rotation(imu.q), g["acc"][0] - imu.ba, 0.005)
+    np.testing.assert_allclose(F, g["F0"], atol=1e-15)
+    np.testing.assert_allclose(G, g["G0"], atol=1e-15)
+    np.testing.assert_allclose(Phi, g["Phi0_unedited"], atol=1e-15)
+    for k in range(20):
+        O.process_model(st, g["ts"][k], g["gyro"][k], g["acc"][k])
+        st.imu.timestamp = g["ts"][k]
+        np.testing.assert_allclose(st.imu.q, g["q"][k], atol=1e-14)
+        np.testing.assert_allclose(st.imu.v, g["v"][k], atol=1e-13)
+        np.testing.assert_allclose(st.imu.p, g["p"][k], atol=1e-13)
+    assert rel(st.P, g["P"]) < 1e-12
+
+
+def test_augment():
+    g = golden("augment")
+    st = oracle_state_from_arrays(g)
+    O.state_augmentation(st, 55.5, 99)
+    np.testing.assert_allclose(st.cams[99].q, g["new_q"], atol=1e-15)
+    np.testing.assert_allclose(st.cams[99].p, g["new_p"], atol=1e-15)
+    assert rel(st.P, g["P_out"]) < 1e-14
+
+
+def _check_update(name):
+    g = golden(name)
+    st = oracle_state_from_arrays(g)
+    F = int(g["F"])
+    # triangulation (feature.py:167-295)
+    for f in range(F):
+        p, ok, _ = O.triangulate(OrderedDict(feature_obs(g, f)), st.cams, st.R_cam0_cam1, st.t_cam0_cam1)
+        assert ok == bool(g["tri_ok"][f])
+        np.testing.assert_allclose(p, g["tri_p"][f], rtol=1e-10, atol=1e-12)
+    # raw jacobian blocks (msckf.py:429-498)
+    for f in range(F):
+        cid, z = feature_obs(g, f)[0]
+        Hx, Hf, r = O.measurement_jacobian(st, st.cams[cid], g["tri_p"][f], z)
+        np.testing.assert_allclose(Hx, g["mj_Hx"][f], rtol=1e-12, atol=1e-12)
+        np.testing.assert_allclose(Hf, g["mj_Hf"][f], rtol=1e-12, atol=1e-12)
+        np.testing.assert_allclose(r, g["mj_r"][f], rtol=1e-10, atol=1e-15)
+    # basis-free invariants of the nullspace projection + gating (msckf.py:500-614)
+    off = 0
+    sizes = g["HtH_sizes"]
+    Hs, rs = [], []
+    for f in range(F):
+        H, r = O.feature_jacobian(st, g["tri_p"][f], feature_obs(g, f))
+        assert H.shape[0] == g["rows"][f]
+        if f < len(sizes):
+            s = int(sizes[f])
+            Hc = H[:, 21:]
+            assert rel(Hc.T @ Hc, g["HtH"][off:off + s * s].reshape(s, s)) < 1e-12
+            off += s * s
+        np.testing.assert_allclose(r @ r, g["rtr"][f], rtol=1e-10)
+        gam = O.gating_gamma(st, H, r)
+        np.testing.assert_allclose(gam, g["gamma"][f], rtol=1e-9)
+        assert (gam < CHI2_05[len(feature_obs(g, f)) - 2]) == bool(g["accept"][f])
+        if g["accept"][f] and g["tri_ok"][f]:
+            Hs.append(H)
+            rs.append(r)
+    H = np.vstack(Hs)
+    assert H.shape[0] == int(g["stacked_rows"])
+    O.measurement_update(st, H, np.concatenate(rs))
+    assert rel(st.P, g["P_out"]) < 1e-11
+    np.testing.assert_allclose(st.imu.q, g["imu_q_out"], atol=1e-13)
+    np.testing.assert_allclose(st.imu.p, g["imu_p_out"], atol=1e-13)
+    np.testing.assert_allclose(st.imu.v, g["imu_v_out"], atol=1e-13)
+    np.testing.assert_allclose(np.stack([c.q for c in st.cams.values()]), g["cam_q_out"], atol=1e-13)
+    np.testing.assert_allclose(np.stack([c.p for c in st.cams.values()]), g["cam_p_out"], atol=1e-13)
+    np.testing.assert_allclose(st.imu.R_imu_cam0, g["R_imu_cam0_out"], atol=1e-13)
+
+
+def test_update_n10():
+    _check_update("update_n10_f40")
+
+
+def test_update_n20():
+    _check_update("update_n20_f100")
+
+
+def test_prune():
+    g = golden("prune")
+    st = oracle_state_from_arrays(g)
+    assert list(O.find_redundant_cam_states(st, 0.3)) == list(g["rm_3"])
+    assert list(O.find_redundant_cam_states(st, 0.9)) == list(g["rm_9"])
+    O.remove_cam_cov(st, [int(c) for c in g["rm"]])
+    np.testing.assert_array_equal(st.P, g["P_out"])
+
+
+def sequence_record(st, res, n_map):
+    imu = st.imu
+    P = st.P
+    return np.concatenate([
+        [res["timestamp"]], imu.q, imu.p, imu.v, imu.bg, imu.ba, imu.R_imu_cam0.ravel(), imu.t_cam0_imu,
+        [np.linalg.norm(P), np.trace(P), P.shape[0], len(st.cams), n_map],
+        res["cam0_pose"].R.ravel(), res["cam0_pose"].t])
+
+
+def test_sequence():
+    """200-frame synthetic stereo+IMU stream through the whole filter: every
+    gating decision and stacked-H shape identical, state to 1e-9."""
+    from msckf_amd import synth, FilterConfig, chi2_threshold
+    g = golden("sequence_s1")
+    seq = synth.make_sequence(int(g["n_frames"]), int(g["seed"]))
+    orc = O.OracleMSCKF(FilterConfig(), chi2_threshold)
+    recs = []
+    for kind, m in seq.events():
+        if kind == 0:
+            orc.imu_callback(m.vio_timestamp__, m.angular_velocity, m.linear_acceleration)
+            continue
+        res = orc.feature_callback(m.timestamp, [(f.id, f.u0, f.v0, f.u1, f.v1) for f in m.vio_features])
+        if res is not None:
+            recs.append(sequence_record(orc.st, res, len(orc.map)))
+    rec = np.array(recs)
+    np.testing.assert_array_equal(np.array(orc.gate_log), g["gates"])
+    np.testing.assert_array_equal(np.array(orc.shape_log), g["shapes"])
+    assert rec.shape == g["rec"].shape
+    np.testing.assert_allclose(rec, g["rec"], rtol=1e-9, atol=1e-10)
+    assert rel(orc.st.P, g["P_final"]) < 1e-9
