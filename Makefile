@@ -1,0 +1,23 @@
+# Builds the HIP extension in-tree for gfx950 (the .so travels to the GPU box
+# with the gpurun snapshot; it is git-ignored).
+PKG      := visual-inertial-odometry-msckf-stereo_amd
+SRC      := $(PKG)/csrc
+LIB      := $(PKG)/libmsckf_hip.so
+HIPCC    ?= /opt/rocm/bin/hipcc
+ARCH     ?= gfx950
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-result -Iinclude
+OBJS     := $(SRC)/msckf_kernels.o $(SRC)/msckf_api.o
+HDRS     := $(SRC)/msckf_common.h $(SRC)/msckf_launch.h include/msckf_hip.h
+
+all: $(LIB)
+
+$(SRC)/%.o: $(SRC)/%.hip $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
+
+clean:
+	rm -f $(OBJS) $(LIB)
+
+.PHONY: all clean

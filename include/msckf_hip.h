@@ -1,0 +1,139 @@
+/*
+ * msckf_hip.h -- C-ABI of the MI355X-native MSCKF stereo-VIO EKF hot path.
+ *
+ * The reference (NonStopEagle137/Visual-Inertial-Odometry-MSCKF-Stereo) has no
+ * FFI: its boundary is the Python class MSCKF (MSCKF/msckf.py:104-908) whose
+ * dense linear algebra sits in seven numba-jitted functions
+ * (MSCKF/jit_utils.py:6-187).  Each entry point below replaces one of those
+ * call sites; the Python host class (msckf_amd.msckf.MSCKF) keeps the
+ * reference's imu_callback / feature_callback API and calls these through
+ * ctypes.
+ *
+ * Conventions
+ *   - plain pointers and sizes; host arrays are caller-owned and copied in/out;
+ *     device buffers are context-owned.
+ *   - return 0 on success, >0 for a benign no-op, <0 for an error (HIP failure,
+ *     bad argument, non-positive-definite innovation covariance).  Nothing
+ *     throws across the ABI.  msckf_last_error() gives a message.
+ *   - a context holds B independent filters ("filter slots") of one scalar type
+ *     (4 = fp32, 8 = fp64) with a fixed cam-state capacity; a context is
+ *     single-threaded (the Python wrapper serialises calls with a lock).
+ *   - state layouts (all doubles at the ABI):
+ *       IMU record, MSCKF_IMU_LEN doubles:
+ *         [0:4] q (JPL x,y,z,w; world->IMU)  [4:7] p  [7:10] v  [10:13] bg
+ *         [13:16] ba  [16:20] q_null  [20:23] p_null  [23:26] v_null
+ *         [26:35] R_imu_cam0 (row-major)  [35:38] t_cam0_imu  [38:41] gravity
+ *         [41] nulls_alias (0/1, quirk Q5)
+ *       cam record, MSCKF_CAM_LEN doubles: [0:4] q (world->cam0)  [4:7] p
+ *         [7:11] q_null   (position_null aliases p, msckf.py:400)
+ *       covariance: D x D row-major, D = 21 + 6 * n_cams, error-state order
+ *         [dtheta, dbg, dv, dba, dp, dtheta_ic, dp_ic, (dtheta_c, dp_c) x N].
+ */
+#ifndef MSCKF_HIP_H
+#define MSCKF_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MSCKF_IMU_LEN 42
+#define MSCKF_CAM_LEN 11
+
+/* Filter parameters: the filter fields of ConfigEuRoC / OptimizationConfigEuRoC
+ * (MSCKF/config.py:5-124) plus the extrinsics MSCKF.__init__ derives
+ * (msckf.py:142-152). */
+typedef struct msckf_config_t {
+    double gyro_noise, acc_noise, gyro_bias_noise, acc_bias_noise; /* Qc, msckf.py:132-137 */
+    double observation_noise;                                     /* sigma^2, msckf.py:560 */
+    double R_cam0_cam1[9], t_cam0_cam1[3];                         /* T_cn_cnm1, msckf.py:148-152 */
+    double huber_epsilon, estimation_precision, initial_damping;  /* feature.py:92, 234-272 */
+    int32_t outer_loop_max_iteration, inner_loop_max_iteration;
+} msckf_config_t;
+
+typedef struct msckf_ctx msckf_ctx_t;
+
+/* Replaces MSCKF.__init__ (msckf.py:105-164): allocates the device state of
+ * n_filters filters of capacity n_cam_capacity cam states each. */
+int msckf_create(const msckf_config_t* cfg, int hip_device, int scalar_bytes,
+                 int n_filters, int n_cam_capacity, msckf_ctx_t** out);
+int msckf_destroy(msckf_ctx_t* ctx);
+const char* msckf_last_error(void);
+int msckf_scalar_bytes(const msckf_ctx_t* ctx);
+
+/* Whole-state upload / download of one filter slot (initialisation, resets,
+ * publish msckf.py:888-908, keyframe selection msckf.py:691-727, tests).
+ * cams / P may be NULL on get to skip them. */
+int msckf_set_state(msckf_ctx_t* ctx, int filter, const double* imu, int n_cams,
+                    const double* cams, const double* P);
+int msckf_get_state(msckf_ctx_t* ctx, int filter, double* imu, double* cams,
+                    double* P, int* n_cams);
+/* Covariance diagonal entries [i0, i0+n) (online_reset, msckf.py:869-871). */
+int msckf_get_cov_diag(msckf_ctx_t* ctx, int filter, int i0, int n, double* out);
+
+/* Replaces the per-sample loop of batch_imu_processing -> process_model
+ * (msckf.py:262-368) incl. _process_model, _predict_new_state and
+ * _propaget_state_Covariance (jit_utils.py:6-135): n samples applied in order,
+ * dt[k] = t_k - t_{k-1} (the host owns timestamps). */
+int msckf_propagate(msckf_ctx_t* ctx, int filter, int n, const double* dt,
+                    const double* gyro, const double* acc);
+
+/* Replaces state_augmentation (msckf.py:385-407) + _state_augmentation
+ * (jit_utils.py:137-167): appends a cam state cloned from the IMU pose and
+ * grows P by 6 rows / cols. */
+int msckf_augment(msckf_ctx_t* ctx, int filter);
+
+/* Replaces Feature.initialize_position (feature.py:167-295) for nf features:
+ * feature f observes cam slots obs_cam[obs_off[f]..obs_off[f+1]) with
+ * measurements obs_z (4 per observation, u0 v0 u1 v1). */
+int msckf_triangulate(msckf_ctx_t* ctx, int filter, int nf, const int32_t* obs_off,
+                      const int32_t* obs_cam, const double* obs_z,
+                      double* p_w_out, uint8_t* valid_out);
+
+/* Replaces the stacked update of remove_lost_features (msckf.py:661-685) or
+ * prune_cam_state_buffer (msckf.py:776-801): per-feature measurement_jacobian
+ * + feature_jacobian (msckf.py:429-541), gating_test (606-614) with the
+ * caller's per-feature chi2 thresholds, stacking in feature order with the
+ * row cap (msckf.py:676-679; row_cap <= 0 = no cap) and measurement_update
+ * (543-604, _fastQR / _fastSolve, jit_utils.py:173-179).
+ * accepted_out[f] = 1 iff feature f's rows went into the update; gamma_out[f]
+ * = its Mahalanobis distance (NaN if not evaluated).  Returns 1 (no-op) when
+ * no rows are stacked, like msckf.py:544-545. */
+int msckf_update(msckf_ctx_t* ctx, int filter, int nf, const int32_t* obs_off,
+                 const int32_t* obs_cam, const double* obs_z, const double* p_w,
+                 const double* chi2, int row_cap, uint8_t* accepted_out,
+                 double* gamma_out, int32_t* rows_out);
+
+/* Replaces the P compaction + cam-state removal loop (msckf.py:803-818):
+ * removes the given cam slots (any order). */
+int msckf_prune(msckf_ctx_t* ctx, int filter, int n, const int32_t* cam_slots);
+
+/* ---- throughput mode: B independent filters, one launch chain per step ----
+ * msckf_batch_load copies features for ALL filter slots to HBM once:
+ * feat_off[B+1] splits the nf features over slots.  msckf_batch_update then
+ * runs triangulation (if flags & MSCKF_TRIANGULATE) + the full update chain on
+ * the resident data, asynchronously; msckf_sync waits.  msckf_snapshot /
+ * msckf_restore copy the whole device state (P, IMU, cams) to / from a
+ * shadow buffer on the device (so repeated timed steps do identical work). */
+#define MSCKF_TRIANGULATE 1
+int msckf_batch_load(msckf_ctx_t* ctx, const int32_t* feat_off, const int32_t* obs_off,
+                     const int32_t* obs_cam, const double* obs_z, const double* p_w,
+                     const double* chi2);
+int msckf_batch_update(msckf_ctx_t* ctx, int row_cap, int flags);
+int msckf_batch_results(msckf_ctx_t* ctx, uint8_t* accepted_out, double* gamma_out,
+                        double* p_w_out, uint8_t* valid_out, int32_t* rows_out);
+int msckf_snapshot(msckf_ctx_t* ctx);
+int msckf_restore(msckf_ctx_t* ctx);
+int msckf_sync(msckf_ctx_t* ctx);
+
+/* Per-kernel device time (HIP events on the context stream), accumulated
+ * while profiling is on.  names: NUL-separated list written to names_out. */
+int msckf_set_profiling(msckf_ctx_t* ctx, int on);
+int msckf_kernel_times(msckf_ctx_t* ctx, int max_k, double* ms_total, int32_t* launches,
+                       char* names_out, int names_cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MSCKF_HIP_H */

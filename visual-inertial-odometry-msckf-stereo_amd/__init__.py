@@ -8,5 +8,8 @@ ctypes.  There is no CPU fallback: if ``libmsckf_hip.so`` is missing or no GPU
 is present, the filter raises.
 """
 from .config import FilterConfig, OptimizationConfig, CHI2_05, chi2_threshold  # noqa: F401
+from .msckf import MSCKF, VioResult  # noqa: F401
+from ._lib import Context, MsckfError, load_library  # noqa: F401
 
-__all__ = ["FilterConfig", "OptimizationConfig", "CHI2_05", "chi2_threshold"]
+__all__ = ["FilterConfig", "OptimizationConfig", "CHI2_05", "chi2_threshold", "MSCKF",
+           "VioResult", "Context", "MsckfError", "load_library"]

@@ -1,0 +1,709 @@
+// msckf_api.hip -- context management and the extern "C" ABI declared in
+// include/msckf_hip.h.  Host code only: argument checking, H2D/D2H staging
+// (double at the ABI <-> T on the device), launch sequencing on the context's
+// HIP stream.  No CPU arithmetic of the filter happens here.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/msckf_hip.h"
+#include "msckf_common.h"
+#include "msckf_launch.h"
+
+using namespace msckf;
+
+static thread_local std::string g_err;
+
+#define FAIL(code, ...)                                  \
+    do {                                                 \
+        char _b[512];                                    \
+        snprintf(_b, sizeof(_b), __VA_ARGS__);           \
+        g_err = _b;                                      \
+        return (code);                                   \
+    } while (0)
+
+#define HIPC(x)                                                                          \
+    do {                                                                                 \
+        hipError_t _e = (x);                                                             \
+        if (_e != hipSuccess) FAIL(-2, "%s failed: %s (%s:%d)", #x, hipGetErrorString(_e), \
+                                   __FILE__, __LINE__);                                   \
+    } while (0)
+
+namespace {
+
+template <typename T>
+struct DBuf {   // grow-only device buffer
+    T* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t c = std::max<size_t>(n, 64);
+        hipError_t e = hipMalloc(&p, c * sizeof(T));
+        if (e == hipSuccess) cap = c;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+}  // namespace
+
+struct msckf_ctx {
+    int device = 0, scalar = 8, B = 1, Nmax = 0, Dmax = 0, Cmax = 0;
+    hipStream_t stream = nullptr;
+    msckf_config_t cfg{};
+    std::vector<int> h_ncams;
+    // state
+    DBuf<unsigned char> P, imu, cams, P_snap, imu_snap, cams_snap;
+    DBuf<int> ncams, ncams_snap;
+    // update workspace
+    DBuf<unsigned char> Hthin, HP, S, dx;
+    DBuf<int> info;
+    // feature batch
+    int nf = 0;
+    std::vector<int> h_feat_off;
+    DBuf<int> feat_filter, feat_off, obs_off, obs_cam, row_off;
+    DBuf<long long> ysq_off;
+    DBuf<unsigned char> obs_z, chi2, p_w, obs_ws, tau, ysq, gamma;
+    DBuf<uint8_t> valid, accept, include;
+    // misc scratch
+    DBuf<unsigned char> scratch;
+    DBuf<int> iscratch;
+    KernelTimer timer;
+    bool has_snapshot = false;
+};
+
+namespace {
+
+template <typename T>
+Params<T> make_params(const msckf_ctx* c) {
+    Params<T> p{};
+    const msckf_config_t& k = c->cfg;
+    p.sigma2 = (T)k.observation_noise;
+    p.qc_gyro = (T)k.gyro_noise;
+    p.qc_gbias = (T)k.gyro_bias_noise;
+    p.qc_acc = (T)k.acc_noise;
+    p.qc_abias = (T)k.acc_bias_noise;
+    for (int i = 0; i < 9; ++i) p.R01[i] = (T)k.R_cam0_cam1[i];
+    for (int i = 0; i < 3; ++i) p.t01[i] = (T)k.t_cam0_cam1[i];
+    p.huber = (T)k.huber_epsilon;
+    p.precision = (T)k.estimation_precision;
+    p.damping = (T)k.initial_damping;
+    p.outer_max = k.outer_loop_max_iteration;
+    p.inner_max = k.inner_loop_max_iteration;
+    return p;
+}
+
+template <typename T>
+DevState<T> dev_state(msckf_ctx* c) {
+    DevState<T> s;
+    s.P = reinterpret_cast<T*>(c->P.p);
+    s.imu = reinterpret_cast<T*>(c->imu.p);
+    s.cams = reinterpret_cast<T*>(c->cams.p);
+    s.ncams = c->ncams.p;
+    s.B = c->B;
+    s.Nmax = c->Nmax;
+    s.Dmax = c->Dmax;
+    return s;
+}
+
+template <typename T>
+UpdWs<T> upd_ws(msckf_ctx* c) {
+    UpdWs<T> w;
+    w.Hthin = reinterpret_cast<T*>(c->Hthin.p);
+    w.HP = reinterpret_cast<T*>(c->HP.p);
+    w.S = reinterpret_cast<T*>(c->S.p);
+    w.dx = reinterpret_cast<T*>(c->dx.p);
+    w.info = c->info.p;
+    w.Cmax = c->Cmax;
+    return w;
+}
+
+template <typename T>
+FeatBatch<T> feat_batch(msckf_ctx* c) {
+    FeatBatch<T> f;
+    f.nf = c->nf;
+    f.feat_filter = c->feat_filter.p;
+    f.feat_off = c->feat_off.p;
+    f.obs_off = c->obs_off.p;
+    f.obs_cam = c->obs_cam.p;
+    f.obs_z = reinterpret_cast<const T*>(c->obs_z.p);
+    f.chi2 = reinterpret_cast<const T*>(c->chi2.p);
+    f.ysq_off = c->ysq_off.p;
+    f.p_w = reinterpret_cast<T*>(c->p_w.p);
+    f.valid = c->valid.p;
+    f.obs_ws = reinterpret_cast<T*>(c->obs_ws.p);
+    f.tau = reinterpret_cast<T*>(c->tau.p);
+    f.ysq = reinterpret_cast<T*>(c->ysq.p);
+    f.gamma = reinterpret_cast<T*>(c->gamma.p);
+    f.accept = c->accept.p;
+    f.include = c->include.p;
+    f.row_off = c->row_off.p;
+    return f;
+}
+
+template <typename T>
+std::vector<T> to_T(const double* x, size_t n) {
+    std::vector<T> v(n);
+    for (size_t i = 0; i < n; ++i) v[i] = (T)x[i];
+    return v;
+}
+
+// Copy a double host array to a device buffer of T (synchronous w.r.t. host).
+template <typename T>
+hipError_t upload(msckf_ctx* c, void* dst, const double* src, size_t n) {
+    if (n == 0) return hipSuccess;
+    std::vector<T> v = to_T<T>(src, n);
+    hipError_t e = hipMemcpyAsync(dst, v.data(), n * sizeof(T), hipMemcpyHostToDevice, c->stream);
+    if (e != hipSuccess) return e;
+    return hipStreamSynchronize(c->stream);
+}
+
+template <typename T>
+hipError_t download(msckf_ctx* c, double* dst, const void* src, size_t n) {
+    if (n == 0) return hipSuccess;
+    std::vector<T> v(n);
+    hipError_t e = hipMemcpyAsync(v.data(), src, n * sizeof(T), hipMemcpyDeviceToHost, c->stream);
+    if (e != hipSuccess) return e;
+    e = hipStreamSynchronize(c->stream);
+    for (size_t i = 0; i < n; ++i) dst[i] = (double)v[i];
+    return e;
+}
+
+int check_ctx(msckf_ctx* c, int filter) {
+    if (!c) FAIL(-1, "null context");
+    if (filter < 0 || filter >= c->B) FAIL(-1, "filter slot %d out of range [0,%d)", filter, c->B);
+    return 0;
+}
+
+// Load a feature batch (all filters) into HBM.  feat_off == nullptr means
+// all nf features belong to `single_filter`.
+template <typename T>
+int load_features(msckf_ctx* c, int nf, const int32_t* feat_off, int single_filter, const int32_t* obs_off,
+                  const int32_t* obs_cam, const double* obs_z, const double* p_w, const double* chi2) {
+    std::vector<int> h_off(c->B + 1, 0);
+    if (feat_off) {
+        for (int b = 0; b <= c->B; ++b) h_off[b] = feat_off[b];
+        nf = h_off[c->B];
+    } else {
+        for (int b = 0; b <= c->B; ++b) h_off[b] = b <= single_filter ? 0 : nf;
+    }
+    std::vector<int> h_filt(std::max(nf, 1), 0);
+    for (int b = 0; b < c->B; ++b) {
+        if (h_off[b + 1] < h_off[b]) FAIL(-1, "feat_off not monotone");
+        for (int f = h_off[b]; f < h_off[b + 1]; ++f) h_filt[f] = b;
+    }
+    if (obs_off[0] != 0) FAIL(-1, "obs_off[0] must be 0");
+    const size_t nobs = nf > 0 ? (size_t)obs_off[nf] : 0;
+    std::vector<long long> ysq(nf + 1, 0);
+    for (int f = 0; f < nf; ++f) {
+        int M = obs_off[f + 1] - obs_off[f];
+        int b = h_filt[f];
+        if (M < 1 || M > 128) FAIL(-1, "feature %d has %d observations (1..128 supported)", f, M);
+        if (M > c->h_ncams[b]) FAIL(-1, "feature %d has more observations than cam states", f);
+        for (int i = obs_off[f]; i < obs_off[f + 1]; ++i)
+            if (obs_cam[i] < 0 || obs_cam[i] >= c->h_ncams[b])
+                FAIL(-1, "feature %d observes cam slot %d (filter %d has %d)", f, obs_cam[i], b, c->h_ncams[b]);
+        ysq[f + 1] = ysq[f] + 16LL * M * M;
+    }
+    const size_t ts = sizeof(T);
+    HIPC(c->feat_filter.ensure(nf + 1));
+    HIPC(c->feat_off.ensure(c->B + 1));
+    HIPC(c->obs_off.ensure(nf + 1));
+    HIPC(c->obs_cam.ensure(nobs + 1));
+    HIPC(c->row_off.ensure(nf + 1));
+    HIPC(c->ysq_off.ensure(nf + 1));
+    HIPC(c->obs_z.ensure((nobs * 4 + 4) * ts));
+    HIPC(c->chi2.ensure((nf + 1) * ts));
+    HIPC(c->p_w.ensure((nf * 3 + 3) * ts));
+    HIPC(c->obs_ws.ensure((nobs * OBS_WS + OBS_WS) * ts));
+    HIPC(c->tau.ensure((nf * 4 + 4) * ts));
+    HIPC(c->ysq.ensure((size_t)(ysq[nf] + 16) * ts));
+    HIPC(c->gamma.ensure((nf + 1) * ts));
+    HIPC(c->valid.ensure(nf + 1));
+    HIPC(c->accept.ensure(nf + 1));
+    HIPC(c->include.ensure(nf + 1));
+    hipStream_t s = c->stream;
+    HIPC(hipMemcpyAsync(c->feat_filter.p, h_filt.data(), nf * sizeof(int), hipMemcpyHostToDevice, s));
+    HIPC(hipMemcpyAsync(c->feat_off.p, h_off.data(), (c->B + 1) * sizeof(int), hipMemcpyHostToDevice, s));
+    HIPC(hipMemcpyAsync(c->obs_off.p, obs_off, (nf + 1) * sizeof(int), hipMemcpyHostToDevice, s));
+    if (nobs) HIPC(hipMemcpyAsync(c->obs_cam.p, obs_cam, nobs * sizeof(int), hipMemcpyHostToDevice, s));
+    HIPC(hipMemcpyAsync(c->ysq_off.p, ysq.data(), (nf + 1) * sizeof(long long), hipMemcpyHostToDevice, s));
+    HIPC(hipStreamSynchronize(s));
+    HIPC(upload<T>(c, c->obs_z.p, obs_z, nobs * 4));
+    if (chi2) {
+        HIPC(upload<T>(c, c->chi2.p, chi2, nf));
+    } else {
+        std::vector<double> big(nf, 1e300);
+        HIPC(upload<T>(c, c->chi2.p, big.data(), nf));
+    }
+    if (p_w) {
+        HIPC(upload<T>(c, c->p_w.p, p_w, (size_t)nf * 3));
+        HIPC(hipMemsetAsync(c->valid.p, 1, nf, s));
+    } else {
+        HIPC(hipMemsetAsync(c->valid.p, 0, nf, s));
+    }
+    HIPC(hipStreamSynchronize(s));
+    c->nf = nf;
+    c->h_feat_off = h_off;
+    return 0;
+}
+
+template <typename T>
+int run_update_chain(msckf_ctx* c, int row_cap, bool triangulate) {
+    hipStream_t s = c->stream;
+    DevState<T> st = dev_state<T>(c);
+    Params<T> prm = make_params<T>(c);
+    FeatBatch<T> fb = feat_batch<T>(c);
+    UpdWs<T> ws = upd_ws<T>(c);
+    if (triangulate) {
+        c->timer.begin(s, "triangulate");
+        launch_triangulate<T>(s, st, prm, fb);
+        c->timer.end(s);
+    }
+    c->timer.begin(s, "feature_jacobian");
+    launch_feature<T>(s, st, prm, fb);
+    c->timer.end(s);
+    c->timer.begin(s, "gate");
+    launch_gate<T>(s, st, prm, fb);
+    c->timer.end(s);
+    c->timer.begin(s, "select");
+    launch_select<T>(s, st, fb, ws, row_cap);
+    c->timer.end(s);
+    c->timer.begin(s, "compress");
+    launch_compress<T>(s, st, fb, ws);
+    c->timer.end(s);
+    launch_kalman<T>(s, st, prm, ws, &c->timer);
+    HIPC(hipGetLastError());
+    return 0;
+}
+
+template <typename T>
+int read_results(msckf_ctx* c, uint8_t* accepted_out, double* gamma_out, double* p_w_out, uint8_t* valid_out,
+                 int32_t* rows_out) {
+    hipStream_t s = c->stream;
+    HIPC(hipStreamSynchronize(s));
+    c->timer.collect();
+    const int nf = c->nf;
+    if (accepted_out && nf) HIPC(hipMemcpy(accepted_out, c->include.p, nf, hipMemcpyDeviceToHost));
+    if (valid_out && nf) HIPC(hipMemcpy(valid_out, c->valid.p, nf, hipMemcpyDeviceToHost));
+    if (gamma_out && nf) HIPC(download<T>(c, gamma_out, c->gamma.p, nf));
+    if (p_w_out && nf) HIPC(download<T>(c, p_w_out, c->p_w.p, (size_t)nf * 3));
+    std::vector<int> info(4 * c->B);
+    HIPC(hipMemcpy(info.data(), c->info.p, info.size() * sizeof(int), hipMemcpyDeviceToHost));
+    int status = 0;
+    for (int b = 0; b < c->B; ++b) {
+        if (rows_out) rows_out[b] = info[4 * b];
+        if (info[4 * b + 3] < 0) status = -3;
+    }
+    if (status) FAIL(-3, "innovation covariance not positive definite");
+    return 0;
+}
+
+template <typename T>
+int do_create(msckf_ctx* c) {
+    const size_t ts = sizeof(T);
+    const size_t B = c->B;
+    HIPC(c->P.ensure(B * c->Dmax * c->Dmax * ts));
+    HIPC(c->imu.ensure(B * IMU_STRIDE * ts));
+    HIPC(c->cams.ensure(B * c->Nmax * CAM_STRIDE * ts));
+    HIPC(c->ncams.ensure(B));
+    HIPC(c->Hthin.ensure(B * c->Cmax * (c->Cmax + 1) * ts));
+    HIPC(c->HP.ensure(B * c->Cmax * c->Dmax * ts));
+    HIPC(c->S.ensure(B * c->Cmax * c->Cmax * ts));
+    HIPC(c->dx.ensure(B * c->Dmax * ts));
+    HIPC(c->info.ensure(4 * B));
+    HIPC(hipMemset(c->P.p, 0, c->P.cap));
+    HIPC(hipMemset(c->cams.p, 0, c->cams.cap));
+    HIPC(hipMemset(c->ncams.p, 0, B * sizeof(int)));
+    HIPC(hipMemset(c->info.p, 0, 4 * B * sizeof(int)));
+    std::vector<T> imu(B * IMU_STRIDE, T(0));
+    for (size_t b = 0; b < B; ++b) {
+        T* r = &imu[b * IMU_STRIDE];
+        r[I_Q + 3] = 1;
+        r[I_QN + 3] = 1;
+        r[I_RIC + 0] = r[I_RIC + 4] = r[I_RIC + 8] = 1;
+        r[I_G + 2] = T(-9.81);
+    }
+    HIPC(hipMemcpy(c->imu.p, imu.data(), imu.size() * ts, hipMemcpyHostToDevice));
+    c->h_ncams.assign(B, 0);
+    return 0;
+}
+
+template <typename T>
+int do_set_state(msckf_ctx* c, int f, const double* imu, int n_cams, const double* cams, const double* P) {
+    if (n_cams < 0 || n_cams > c->Nmax) FAIL(-1, "n_cams %d exceeds capacity %d", n_cams, c->Nmax);
+    const size_t ts = sizeof(T);
+    hipStream_t s = c->stream;
+    if (imu) {
+        std::vector<double> rec(IMU_STRIDE, 0.0);
+        std::memcpy(rec.data(), imu, MSCKF_IMU_LEN * sizeof(double));
+        HIPC(upload<T>(c, c->imu.p + (size_t)f * IMU_STRIDE * ts, rec.data(), IMU_STRIDE));
+    }
+    if (cams && n_cams) {
+        std::vector<double> rec((size_t)n_cams * CAM_STRIDE, 0.0);
+        for (int i = 0; i < n_cams; ++i)
+            std::memcpy(&rec[(size_t)i * CAM_STRIDE], cams + (size_t)i * MSCKF_CAM_LEN, MSCKF_CAM_LEN * sizeof(double));
+        HIPC(upload<T>(c, c->cams.p + (size_t)f * c->Nmax * CAM_STRIDE * ts, rec.data(), rec.size()));
+    }
+    if (P) {
+        const int D = 21 + 6 * n_cams;
+        std::vector<T> full((size_t)c->Dmax * c->Dmax, T(0));
+        for (int i = 0; i < D; ++i)
+            for (int j = 0; j < D; ++j) full[(size_t)i * c->Dmax + j] = (T)P[(size_t)i * D + j];
+        HIPC(hipMemcpyAsync(c->P.p + (size_t)f * c->Dmax * c->Dmax * ts, full.data(), full.size() * ts,
+                            hipMemcpyHostToDevice, s));
+        HIPC(hipStreamSynchronize(s));
+    }
+    HIPC(hipMemcpy(c->ncams.p + f, &n_cams, sizeof(int), hipMemcpyHostToDevice));
+    c->h_ncams[f] = n_cams;
+    return 0;
+}
+
+template <typename T>
+int do_get_state(msckf_ctx* c, int f, double* imu, double* cams, double* P, int* n_cams) {
+    const size_t ts = sizeof(T);
+    HIPC(hipStreamSynchronize(c->stream));
+    const int nc = c->h_ncams[f];
+    if (n_cams) *n_cams = nc;
+    if (imu) {
+        std::vector<double> rec(IMU_STRIDE);
+        HIPC(download<T>(c, rec.data(), c->imu.p + (size_t)f * IMU_STRIDE * ts, IMU_STRIDE));
+        std::memcpy(imu, rec.data(), MSCKF_IMU_LEN * sizeof(double));
+    }
+    if (cams && nc) {
+        std::vector<double> rec((size_t)nc * CAM_STRIDE);
+        HIPC(download<T>(c, rec.data(), c->cams.p + (size_t)f * c->Nmax * CAM_STRIDE * ts, rec.size()));
+        for (int i = 0; i < nc; ++i)
+            std::memcpy(cams + (size_t)i * MSCKF_CAM_LEN, &rec[(size_t)i * CAM_STRIDE], MSCKF_CAM_LEN * sizeof(double));
+    }
+    if (P) {
+        const int D = 21 + 6 * nc;
+        std::vector<double> full((size_t)c->Dmax * c->Dmax);
+        HIPC(download<T>(c, full.data(), c->P.p + (size_t)f * c->Dmax * c->Dmax * ts, full.size()));
+        for (int i = 0; i < D; ++i)
+            for (int j = 0; j < D; ++j) P[(size_t)i * D + j] = full[(size_t)i * c->Dmax + j];
+    }
+    return 0;
+}
+
+template <typename T>
+int do_propagate(msckf_ctx* c, int f, int n, const double* dt, const double* gyro, const double* acc) {
+    if (n <= 0) return 1;
+    std::vector<double> smp((size_t)n * 7);
+    for (int k = 0; k < n; ++k) {
+        smp[7 * k] = dt[k];
+        for (int i = 0; i < 3; ++i) {
+            smp[7 * k + 1 + i] = gyro[3 * k + i];
+            smp[7 * k + 4 + i] = acc[3 * k + i];
+        }
+    }
+    HIPC(c->scratch.ensure(smp.size() * sizeof(T)));
+    HIPC(upload<T>(c, c->scratch.p, smp.data(), smp.size()));
+    c->timer.begin(c->stream, "propagate");
+    launch_propagate<T>(c->stream, dev_state<T>(c), make_params<T>(c), f, n, reinterpret_cast<T*>(c->scratch.p));
+    c->timer.end(c->stream);
+    HIPC(hipGetLastError());
+    HIPC(hipStreamSynchronize(c->stream));
+    c->timer.collect();
+    return 0;
+}
+
+template <typename T>
+int do_augment(msckf_ctx* c, int f) {
+    if (c->h_ncams[f] >= c->Nmax) FAIL(-1, "cam-state capacity %d exhausted", c->Nmax);
+    c->timer.begin(c->stream, "augment");
+    launch_augment<T>(c->stream, dev_state<T>(c), f);
+    c->timer.end(c->stream);
+    HIPC(hipGetLastError());
+    HIPC(hipStreamSynchronize(c->stream));
+    c->timer.collect();
+    c->h_ncams[f] += 1;
+    return 0;
+}
+
+template <typename T>
+int do_prune(msckf_ctx* c, int f, int n, const int32_t* slots) {
+    const int nc = c->h_ncams[f];
+    std::vector<char> rm(nc, 0);
+    for (int i = 0; i < n; ++i) {
+        if (slots[i] < 0 || slots[i] >= nc) FAIL(-1, "prune slot %d out of range", slots[i]);
+        rm[slots[i]] = 1;
+    }
+    std::vector<int> keep, keep_cams;
+    for (int i = 0; i < 21; ++i) keep.push_back(i);
+    for (int cam = 0; cam < nc; ++cam)
+        if (!rm[cam]) {
+            keep_cams.push_back(cam);
+            for (int e = 0; e < 6; ++e) keep.push_back(21 + 6 * cam + e);
+        }
+    const int Dn = (int)keep.size();
+    HIPC(c->iscratch.ensure(keep.size() + keep_cams.size() + 1));
+    HIPC(c->scratch.ensure((size_t)Dn * Dn * sizeof(T)));
+    HIPC(hipMemcpy(c->iscratch.p, keep.data(), keep.size() * sizeof(int), hipMemcpyHostToDevice));
+    if (!keep_cams.empty())
+        HIPC(hipMemcpy(c->iscratch.p + keep.size(), keep_cams.data(), keep_cams.size() * sizeof(int),
+                       hipMemcpyHostToDevice));
+    c->timer.begin(c->stream, "prune");
+    launch_prune<T>(c->stream, dev_state<T>(c), f, c->iscratch.p, Dn, reinterpret_cast<T*>(c->scratch.p),
+                    c->iscratch.p + keep.size(), (int)keep_cams.size());
+    c->timer.end(c->stream);
+    HIPC(hipGetLastError());
+    HIPC(hipStreamSynchronize(c->stream));
+    c->timer.collect();
+    c->h_ncams[f] = (int)keep_cams.size();
+    return 0;
+}
+
+template <typename T>
+int do_triangulate(msckf_ctx* c, int f, int nf, const int32_t* obs_off, const int32_t* obs_cam,
+                   const double* obs_z, double* p_w_out, uint8_t* valid_out) {
+    if (nf <= 0) return 1;
+    int r = load_features<T>(c, nf, nullptr, f, obs_off, obs_cam, obs_z, nullptr, nullptr);
+    if (r) return r;
+    c->timer.begin(c->stream, "triangulate");
+    launch_triangulate<T>(c->stream, dev_state<T>(c), make_params<T>(c), feat_batch<T>(c));
+    c->timer.end(c->stream);
+    HIPC(hipGetLastError());
+    HIPC(hipStreamSynchronize(c->stream));
+    c->timer.collect();
+    HIPC(download<T>(c, p_w_out, c->p_w.p, (size_t)nf * 3));
+    HIPC(hipMemcpy(valid_out, c->valid.p, nf, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+template <typename T>
+int do_update(msckf_ctx* c, int f, int nf, const int32_t* obs_off, const int32_t* obs_cam, const double* obs_z,
+              const double* p_w, const double* chi2, int row_cap, uint8_t* accepted_out, double* gamma_out,
+              int32_t* rows_out) {
+    if (nf <= 0) {
+        if (rows_out) *rows_out = 0;
+        return 1;
+    }
+    int r = load_features<T>(c, nf, nullptr, f, obs_off, obs_cam, obs_z, p_w, chi2);
+    if (r) return r;
+    r = run_update_chain<T>(c, row_cap, false);
+    if (r) return r;
+    std::vector<int32_t> rows(c->B);
+    r = read_results<T>(c, accepted_out, gamma_out, nullptr, nullptr, rows.data());
+    if (rows_out) *rows_out = rows[f];
+    if (r) return r;
+    return rows[f] == 0 ? 1 : 0;
+}
+
+#define DISPATCH(c, fn, ...) ((c)->scalar == 4 ? fn<float>(__VA_ARGS__) : fn<double>(__VA_ARGS__))
+
+}  // namespace
+
+extern "C" {
+
+const char* msckf_last_error(void) { return g_err.c_str(); }
+
+int msckf_create(const msckf_config_t* cfg, int hip_device, int scalar_bytes, int n_filters, int n_cam_capacity,
+                 msckf_ctx_t** out) {
+    if (!cfg || !out) FAIL(-1, "null argument");
+    if (scalar_bytes != 4 && scalar_bytes != 8) FAIL(-1, "scalar_bytes must be 4 or 8");
+    if (n_filters < 1) FAIL(-1, "n_filters must be >= 1");
+    if (n_cam_capacity < 1 || n_cam_capacity > 128) FAIL(-1, "n_cam_capacity must be in [1, 128]");
+    int ndev = 0;
+    HIPC(hipGetDeviceCount(&ndev));
+    if (hip_device < 0 || hip_device >= ndev) FAIL(-1, "HIP device %d not present (%d visible)", hip_device, ndev);
+    HIPC(hipSetDevice(hip_device));
+    msckf_ctx* c = new msckf_ctx();
+    c->device = hip_device;
+    c->scalar = scalar_bytes;
+    c->B = n_filters;
+    c->Nmax = n_cam_capacity;
+    c->Dmax = 21 + 6 * n_cam_capacity;
+    c->Cmax = 6 * n_cam_capacity;
+    c->cfg = *cfg;
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete c;
+        FAIL(-2, "hipStreamCreate: %s", hipGetErrorString(e));
+    }
+    int r = DISPATCH(c, do_create, c);
+    if (r) {
+        msckf_destroy(c);
+        return r;
+    }
+    *out = c;
+    return 0;
+}
+
+int msckf_destroy(msckf_ctx_t* c) {
+    if (!c) return 0;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (auto* b : {&c->P, &c->imu, &c->cams, &c->P_snap, &c->imu_snap, &c->cams_snap, &c->Hthin, &c->HP, &c->S,
+                    &c->dx, &c->obs_z, &c->chi2, &c->p_w, &c->obs_ws, &c->tau, &c->ysq, &c->gamma, &c->scratch})
+        b->release();
+    for (auto* b : {&c->ncams, &c->ncams_snap, &c->info, &c->feat_filter, &c->feat_off, &c->obs_off, &c->obs_cam,
+                    &c->row_off, &c->iscratch})
+        b->release();
+    c->ysq_off.release();
+    c->valid.release();
+    c->accept.release();
+    c->include.release();
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return 0;
+}
+
+int msckf_scalar_bytes(const msckf_ctx_t* c) { return c ? c->scalar : 0; }
+
+int msckf_set_state(msckf_ctx_t* c, int filter, const double* imu, int n_cams, const double* cams, const double* P) {
+    if (int r = check_ctx(c, filter)) return r;
+    return DISPATCH(c, do_set_state, c, filter, imu, n_cams, cams, P);
+}
+
+int msckf_get_state(msckf_ctx_t* c, int filter, double* imu, double* cams, double* P, int* n_cams) {
+    if (int r = check_ctx(c, filter)) return r;
+    return DISPATCH(c, do_get_state, c, filter, imu, cams, P, n_cams);
+}
+
+int msckf_get_cov_diag(msckf_ctx_t* c, int filter, int i0, int n, double* out) {
+    if (int r = check_ctx(c, filter)) return r;
+    const int D = 21 + 6 * c->h_ncams[filter];
+    if (i0 < 0 || n < 0 || i0 + n > D) FAIL(-1, "diagonal range out of bounds");
+    HIPC(hipStreamSynchronize(c->stream));
+    const size_t ts = c->scalar;
+    for (int i = 0; i < n; ++i) {
+        size_t off = ((size_t)filter * c->Dmax * c->Dmax + (size_t)(i0 + i) * c->Dmax + (i0 + i)) * ts;
+        if (ts == 4) {
+            float v;
+            HIPC(hipMemcpy(&v, c->P.p + off, 4, hipMemcpyDeviceToHost));
+            out[i] = v;
+        } else {
+            HIPC(hipMemcpy(&out[i], c->P.p + off, 8, hipMemcpyDeviceToHost));
+        }
+    }
+    return 0;
+}
+
+int msckf_propagate(msckf_ctx_t* c, int filter, int n, const double* dt, const double* gyro, const double* acc) {
+    if (int r = check_ctx(c, filter)) return r;
+    if (n > 0 && (!dt || !gyro || !acc)) FAIL(-1, "null sample array");
+    return DISPATCH(c, do_propagate, c, filter, n, dt, gyro, acc);
+}
+
+int msckf_augment(msckf_ctx_t* c, int filter) {
+    if (int r = check_ctx(c, filter)) return r;
+    return DISPATCH(c, do_augment, c, filter);
+}
+
+int msckf_triangulate(msckf_ctx_t* c, int filter, int nf, const int32_t* obs_off, const int32_t* obs_cam,
+                      const double* obs_z, double* p_w_out, uint8_t* valid_out) {
+    if (int r = check_ctx(c, filter)) return r;
+    if (nf > 0 && (!obs_off || !obs_cam || !obs_z || !p_w_out || !valid_out)) FAIL(-1, "null argument");
+    return DISPATCH(c, do_triangulate, c, filter, nf, obs_off, obs_cam, obs_z, p_w_out, valid_out);
+}
+
+int msckf_update(msckf_ctx_t* c, int filter, int nf, const int32_t* obs_off, const int32_t* obs_cam,
+                 const double* obs_z, const double* p_w, const double* chi2, int row_cap, uint8_t* accepted_out,
+                 double* gamma_out, int32_t* rows_out) {
+    if (int r = check_ctx(c, filter)) return r;
+    if (nf > 0 && (!obs_off || !obs_cam || !obs_z || !p_w || !chi2)) FAIL(-1, "null argument");
+    return DISPATCH(c, do_update, c, filter, nf, obs_off, obs_cam, obs_z, p_w, chi2, row_cap, accepted_out,
+                    gamma_out, rows_out);
+}
+
+int msckf_prune(msckf_ctx_t* c, int filter, int n, const int32_t* cam_slots) {
+    if (int r = check_ctx(c, filter)) return r;
+    if (n <= 0) return 1;
+    return DISPATCH(c, do_prune, c, filter, n, cam_slots);
+}
+
+int msckf_batch_load(msckf_ctx_t* c, const int32_t* feat_off, const int32_t* obs_off, const int32_t* obs_cam,
+                     const double* obs_z, const double* p_w, const double* chi2) {
+    if (!c || !feat_off || !obs_off || !obs_cam || !obs_z) FAIL(-1, "null argument");
+    return DISPATCH(c, load_features, c, 0, feat_off, 0, obs_off, obs_cam, obs_z, p_w, chi2);
+}
+
+int msckf_batch_update(msckf_ctx_t* c, int row_cap, int flags) {
+    if (!c) FAIL(-1, "null context");
+    return DISPATCH(c, run_update_chain, c, row_cap, (flags & MSCKF_TRIANGULATE) != 0);
+}
+
+int msckf_batch_results(msckf_ctx_t* c, uint8_t* accepted_out, double* gamma_out, double* p_w_out,
+                        uint8_t* valid_out, int32_t* rows_out) {
+    if (!c) FAIL(-1, "null context");
+    return DISPATCH(c, read_results, c, accepted_out, gamma_out, p_w_out, valid_out, rows_out);
+}
+
+int msckf_snapshot(msckf_ctx_t* c) {
+    if (!c) FAIL(-1, "null context");
+    HIPC(c->P_snap.ensure(c->P.cap));
+    HIPC(c->imu_snap.ensure(c->imu.cap));
+    HIPC(c->cams_snap.ensure(c->cams.cap));
+    HIPC(c->ncams_snap.ensure(c->B));
+    HIPC(hipMemcpyAsync(c->P_snap.p, c->P.p, c->P.cap, hipMemcpyDeviceToDevice, c->stream));
+    HIPC(hipMemcpyAsync(c->imu_snap.p, c->imu.p, c->imu.cap, hipMemcpyDeviceToDevice, c->stream));
+    HIPC(hipMemcpyAsync(c->cams_snap.p, c->cams.p, c->cams.cap, hipMemcpyDeviceToDevice, c->stream));
+    HIPC(hipMemcpyAsync(c->ncams_snap.p, c->ncams.p, c->B * sizeof(int), hipMemcpyDeviceToDevice, c->stream));
+    HIPC(hipStreamSynchronize(c->stream));
+    c->has_snapshot = true;
+    return 0;
+}
+
+int msckf_restore(msckf_ctx_t* c) {
+    if (!c) FAIL(-1, "null context");
+    if (!c->has_snapshot) FAIL(-1, "no snapshot");
+    c->timer.begin(c->stream, "restore");
+    HIPC(hipMemcpyAsync(c->P.p, c->P_snap.p, c->P.cap, hipMemcpyDeviceToDevice, c->stream));
+    HIPC(hipMemcpyAsync(c->imu.p, c->imu_snap.p, c->imu.cap, hipMemcpyDeviceToDevice, c->stream));
+    HIPC(hipMemcpyAsync(c->cams.p, c->cams_snap.p, c->cams.cap, hipMemcpyDeviceToDevice, c->stream));
+    HIPC(hipMemcpyAsync(c->ncams.p, c->ncams_snap.p, c->B * sizeof(int), hipMemcpyDeviceToDevice, c->stream));
+    c->timer.end(c->stream);
+    return 0;
+}
+
+int msckf_sync(msckf_ctx_t* c) {
+    if (!c) FAIL(-1, "null context");
+    HIPC(hipStreamSynchronize(c->stream));
+    c->timer.collect();
+    return 0;
+}
+
+int msckf_set_profiling(msckf_ctx_t* c, int on) {
+    if (!c) FAIL(-1, "null context");
+    HIPC(hipStreamSynchronize(c->stream));
+    c->timer.collect();
+    c->timer.on = on != 0;
+    c->timer.reset();
+    return 0;
+}
+
+int msckf_kernel_times(msckf_ctx_t* c, int max_k, double* ms_total, int32_t* launches, char* names_out,
+                       int names_cap) {
+    if (!c) FAIL(-1, "null context");
+    HIPC(hipStreamSynchronize(c->stream));
+    c->timer.collect();
+    int k = std::min<int>(max_k, (int)c->timer.names.size());
+    std::string all;
+    for (int i = 0; i < k; ++i) {
+        ms_total[i] = c->timer.total_ms[i];
+        launches[i] = c->timer.launches[i];
+        all += c->timer.names[i];
+        all.push_back('\0');
+    }
+    if (names_out && names_cap > 0) {
+        int n = std::min<int>(names_cap - 1, (int)all.size());
+        std::memcpy(names_out, all.data(), n);
+        names_out[n] = 0;
+    }
+    return k;
+}
+
+}  // extern "C"

@@ -1,0 +1,187 @@
+// msckf_common.h -- device layouts, kernel argument structs and SO(3) /
+// JPL-quaternion device math shared by the MSCKF kernels (gfx950).
+//
+// Everything is templated on the arithmetic type T (float or double): one code
+// path, two instantiations (fp64 for sequence-level parity, fp32 for the
+// throughput configs).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace msckf {
+
+// ---------------------------------------------------------------- layouts --
+// Device IMU record: same field offsets as the ABI record (msckf_hip.h), padded.
+constexpr int IMU_STRIDE = 48;
+enum ImuField { I_Q = 0, I_P = 4, I_V = 7, I_BG = 10, I_BA = 13, I_QN = 16, I_PN = 20,
+                I_VN = 23, I_RIC = 26, I_TCI = 35, I_G = 38, I_ALIAS = 41 };
+// Device cam record (msckf_hip.h cam record + pad).
+constexpr int CAM_STRIDE = 12;
+enum CamField { C_Q = 0, C_P = 4, C_QN = 7 };
+
+// Per-observation workspace written by the feature kernel (units of T):
+//   Hx  4x6  measurement Jacobian block, observability-projected (msckf.py:480-490)
+//   V   4x3  rows of the 3 Householder vectors of H_f's QR
+//   W   3x6  this observation's 6 columns of w_j = v_j^T X_{j-1}
+//   Qr  4    rows of Q^T r
+constexpr int OBS_HX = 0, OBS_V = 24, OBS_W = 36, OBS_QR = 54, OBS_WS = 58;
+
+template <typename T>
+struct Params {
+    T sigma2;                 // observation noise variance (msckf.py:560)
+    T qc_gyro, qc_gbias, qc_acc, qc_abias;   // diag of Qc (msckf.py:132-137)
+    T R01[9], t01[3];         // cam0 -> cam1 (msckf.py:148-152)
+    T huber, precision, damping;              // feature.py LM
+    int outer_max, inner_max;
+};
+
+template <typename T>
+struct DevState {
+    T* P;          // [B][Dmax][Dmax]
+    T* imu;        // [B][IMU_STRIDE]
+    T* cams;       // [B][Nmax][CAM_STRIDE]
+    int* ncams;    // [B]
+    int B, Nmax, Dmax;
+};
+
+// Feature batch resident in HBM (msckf_batch_load / msckf_update).
+template <typename T>
+struct FeatBatch {
+    int nf;
+    const int* feat_filter;   // [nf] filter slot of each feature
+    const int* feat_off;      // [B+1] features of slot b: [feat_off[b], feat_off[b+1])
+    const int* obs_off;       // [nf+1]
+    const int* obs_cam;       // [sum M] cam slot
+    const T* obs_z;           // [sum M][4]
+    const T* chi2;            // [nf]
+    const long long* ysq_off; // [nf+1] offsets of the (4M)^2 gating scratch
+    T* p_w;                   // [nf][3]
+    uint8_t* valid;           // [nf] triangulation validity (1 if p_w given)
+    T* obs_ws;                // [sum M][OBS_WS]
+    T* tau;                   // [nf][4]
+    T* ysq;                   // gating scratch
+    T* gamma;                 // [nf]
+    uint8_t* accept;          // [nf] chi2 test passed
+    uint8_t* include;         // [nf] stacked into the update
+    int* row_off;             // [nf] first stacked row of the feature
+};
+
+// Per-filter update workspace.
+template <typename T>
+struct UpdWs {
+    T* Hthin;    // [B][Cmax][Cmax+1]   (H_thin | r_thin)
+    T* HP;       // [B][Cmax][Dmax]     H_thin P, then L^-1 H_thin P
+    T* S;        // [B][Cmax][Cmax]     innovation covariance -> its Cholesky factor
+    T* dx;       // [B][Dmax]
+    int* info;   // [B][4]: rows stacked, n (rows of H_thin), compress flag, status
+    int Cmax;
+};
+
+// ------------------------------------------------------------ device math --
+template <typename T> __device__ __forceinline__ T dsqrt(T x) { return sqrt(x); }
+
+template <typename T>
+__device__ __forceinline__ void skew3(const T* v, T* S) {
+    S[0] = 0;     S[1] = -v[2]; S[2] = v[1];
+    S[3] = v[2];  S[4] = 0;     S[5] = -v[0];
+    S[6] = -v[1]; S[7] = v[0];  S[8] = 0;
+}
+
+// utils.py:14-27 -- R = (2w^2-1) I - 2w [v]x + 2 v v^T, q normalised first.
+template <typename T>
+__device__ __forceinline__ void quat_to_rot(const T* q_in, T* R) {
+    T n = sqrt(q_in[0] * q_in[0] + q_in[1] * q_in[1] + q_in[2] * q_in[2] + q_in[3] * q_in[3]);
+    T x = q_in[0] / n, y = q_in[1] / n, z = q_in[2] / n, w = q_in[3] / n;
+    T v[3] = {x, y, z};
+    T S[9];
+    skew3(v, S);
+    T a = 2 * w * w - 1, tw = 2 * w;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+            R[3 * i + j] = (i == j ? a : T(0)) - tw * S[3 * i + j] + (2 * v[i]) * v[j];
+}
+
+// utils.py:29-53 (same branch structure -> same sign convention)
+template <typename T>
+__device__ __forceinline__ void rot_to_quat(const T* R, T* q) {
+    T t;
+    if (R[8] < 0) {
+        if (R[0] > R[4]) {
+            t = 1 + R[0] - R[4] - R[8];
+            q[0] = t; q[1] = R[1] + R[3]; q[2] = R[6] + R[2]; q[3] = R[5] - R[7];
+        } else {
+            t = 1 - R[0] + R[4] - R[8];
+            q[0] = R[1] + R[3]; q[1] = t; q[2] = R[7] + R[5]; q[3] = R[6] - R[2];
+        }
+    } else {
+        if (R[0] < -R[4]) {
+            t = 1 - R[0] - R[4] + R[8];
+            q[0] = R[2] + R[6]; q[1] = R[7] + R[5]; q[2] = t; q[3] = R[1] - R[3];
+        } else {
+            t = 1 + R[0] + R[4] + R[8];
+            q[0] = R[5] - R[7]; q[1] = R[6] - R[2]; q[2] = R[1] - R[3]; q[3] = t;
+        }
+    }
+    T n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    q[0] /= n; q[1] /= n; q[2] /= n; q[3] /= n;
+}
+
+// utils.py:67-82: q1 (x) q2 (both normalised first), result normalised.
+template <typename T>
+__device__ __forceinline__ void quat_mul(const T* a_in, const T* b_in, T* q) {
+    T na = sqrt(a_in[0] * a_in[0] + a_in[1] * a_in[1] + a_in[2] * a_in[2] + a_in[3] * a_in[3]);
+    T nb = sqrt(b_in[0] * b_in[0] + b_in[1] * b_in[1] + b_in[2] * b_in[2] + b_in[3] * b_in[3]);
+    T a[4] = {a_in[0] / na, a_in[1] / na, a_in[2] / na, a_in[3] / na};
+    T b[4] = {b_in[0] / nb, b_in[1] / nb, b_in[2] / nb, b_in[3] / nb};
+    T r[4];
+    r[0] = a[3] * b[0] + a[2] * b[1] - a[1] * b[2] + a[0] * b[3];
+    r[1] = -a[2] * b[0] + a[3] * b[1] + a[0] * b[2] + a[1] * b[3];
+    r[2] = a[1] * b[0] - a[0] * b[1] + a[3] * b[2] + a[2] * b[3];
+    r[3] = -a[0] * b[0] - a[1] * b[1] - a[2] * b[2] + a[3] * b[3];
+    T n = sqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2] + r[3] * r[3]);
+    q[0] = r[0] / n; q[1] = r[1] / n; q[2] = r[2] / n; q[3] = r[3] / n;
+}
+
+// utils.py:85-101
+template <typename T>
+__device__ __forceinline__ void small_angle_quat(const T* dth, T* q) {
+    T d0 = dth[0] / 2, d1 = dth[1] / 2, d2 = dth[2] / 2;
+    T n2 = d0 * d0 + d1 * d1 + d2 * d2;
+    if (n2 <= 1) {
+        q[0] = d0; q[1] = d1; q[2] = d2; q[3] = sqrt(1 - n2);
+    } else {
+        T s = sqrt(1 + n2);
+        q[0] = d0 / s; q[1] = d1 / s; q[2] = d2 / s; q[3] = 1 / s;
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ void mat3_vec(const T* A, const T* x, T* y) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) y[i] = A[3 * i] * x[0] + A[3 * i + 1] * x[1] + A[3 * i + 2] * x[2];
+}
+template <typename T>
+__device__ __forceinline__ void mat3T_vec(const T* A, const T* x, T* y) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) y[i] = A[i] * x[0] + A[3 + i] * x[1] + A[6 + i] * x[2];
+}
+template <typename T>
+__device__ __forceinline__ void mat3_mul(const T* A, const T* B, T* C) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+            C[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+}
+
+// ------------------------------------------------------ wave reductions --
+template <typename T>
+__device__ __forceinline__ T wave_sum(T x) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) x += __shfl_xor(x, m, 64);
+    return x;
+}
+
+}  // namespace msckf

@@ -1,0 +1,1365 @@
+// msckf_kernels.hip -- hand-written CDNA4 (gfx950) kernels for the MSCKF
+// stereo-VIO EKF hot path.  Every kernel is templated on T (float | double)
+// and handles a batch of independent filters (one HIP launch per stage for
+// all filters), so the single-filter API and the throughput mode share one
+// code path.
+//
+// Stage map (reference file:line -> kernel):
+//   process_model / _process_model / _predict_new_state /
+//   _propaget_state_Covariance  msckf.py:291-368, jit_utils.py:6-135 -> k_propagate
+//   state_augmentation / _state_augmentation msckf.py:385-407,
+//                                            jit_utils.py:137-167   -> k_augment
+//   Feature.initialize_position feature.py:167-295                  -> k_triangulate
+//   measurement_jacobian + feature_jacobian msckf.py:429-541        -> k_feature
+//   gating_test msckf.py:606-614                                    -> k_gate
+//   stacking + row cap msckf.py:661-682, 776-798                    -> k_select
+//   measurement_update QR msckf.py:549-556 (_fastQR)                -> k_compress
+//   measurement_update S, K, dx, P msckf.py:559-604 (_fastSolve)    -> k_hp, k_s,
+//                                  k_chol, k_trsm, k_dx, k_pupdate, k_correct
+//   P compaction msckf.py:803-818                                   -> k_prune_*
+#include "msckf_common.h"
+#include "msckf_launch.h"
+
+namespace msckf {
+
+// ===========================================================================
+// IMU propagation: one 256-thread workgroup per filter, the n samples of the
+// frame applied in order.  The 21x21 recursion lives in LDS; the IMU x cam
+// cross block is updated once with the product Phi_n...Phi_1 (the per-sample
+// full-P symmetrisation of msckf.py:362-363 is a no-op on the cam x cam
+// block and only re-rounds the cross block).
+// ===========================================================================
+template <typename T>
+__device__ void mm21(const T* A, const T* B, T* C, int tid) {   // C = A B (21x21)
+    for (int e = tid; e < 441; e += blockDim.x) {
+        int i = e / 21, j = e % 21;
+        T s = 0;
+        for (int k = 0; k < 21; ++k) s += A[i * 21 + k] * B[k * 21 + j];
+        C[e] = s;
+    }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_propagate(DevState<T> st, Params<T> prm, int filter,
+                                                   int n, const T* __restrict__ samples) {
+    __shared__ T F[441], Phi[441], Fdt2[441], Fdt3[441], A[441], Bm[441], P11[441], PhiT[441];
+    __shared__ T G[21 * 12], PG[21 * 12];
+    __shared__ T s_R[9], s_gyro[3], s_acc[3], s_dt;
+    __shared__ T s_imu[IMU_STRIDE];
+    const int tid = threadIdx.x;
+    const int b = filter;
+    T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
+    const int ld = st.Dmax;
+    T* imu = st.imu + (size_t)b * IMU_STRIDE;
+    const int D = 21 + 6 * st.ncams[b];
+    for (int e = tid; e < IMU_STRIDE; e += blockDim.x) s_imu[e] = imu[e];
+    for (int e = tid; e < 441; e += blockDim.x) {
+        P11[e] = P[(e / 21) * ld + e % 21];
+        PhiT[e] = (e / 21 == e % 21) ? T(1) : T(0);
+    }
+    __syncthreads();
+    for (int k = 0; k < n; ++k) {
+        const T* smp = samples + 7 * k;
+        if (tid == 0) {
+            s_dt = smp[0];
+            for (int i = 0; i < 3; ++i) {
+                s_gyro[i] = smp[1 + i] - s_imu[I_BG + i];
+                s_acc[i] = smp[4 + i] - s_imu[I_BA + i];
+            }
+            quat_to_rot(s_imu + I_Q, s_R);
+        }
+        __syncthreads();
+        const T dt = s_dt;
+        // F, G  (jit_utils.py:25-34); R = R_w_i
+        for (int e = tid; e < 441; e += blockDim.x) {
+            int i = e / 21, j = e % 21;
+            T f = 0;
+            if (i < 3 && j < 3) {   // -skew(gyro)
+                const T* w = s_gyro;
+                T sk[9] = {0, -w[2], w[1], w[2], 0, -w[0], -w[1], w[0], 0};
+                f = -sk[3 * i + j];
+            } else if (i < 3 && j >= 3 && j < 6) {
+                f = (i == j - 3) ? T(-1) : T(0);
+            } else if (i >= 6 && i < 9 && j < 3) {   // -R^T skew(acc)
+                const T* a = s_acc;
+                T sk[9] = {0, -a[2], a[1], a[2], 0, -a[0], -a[1], a[0], 0};
+                int r = i - 6;
+                f = -s_R[r] * sk[j] + -s_R[3 + r] * sk[3 + j] + -s_R[6 + r] * sk[6 + j];
+            } else if (i >= 6 && i < 9 && j >= 9 && j < 12) {
+                f = -s_R[3 * (j - 9) + (i - 6)];
+            } else if (i >= 12 && i < 15 && j >= 6 && j < 9) {
+                f = (i - 12 == j - 6) ? T(1) : T(0);
+            }
+            F[e] = f * dt;   // Fdt
+        }
+        for (int e = tid; e < 252; e += blockDim.x) {
+            int i = e / 12, j = e % 12;
+            T g = 0;
+            if (i < 3 && j < 3) g = (i == j) ? T(-1) : T(0);
+            else if (i >= 3 && i < 6 && j >= 3 && j < 6) g = (i - 3 == j - 3) ? T(1) : T(0);
+            else if (i >= 6 && i < 9 && j >= 6 && j < 9) g = -s_R[3 * (j - 6) + (i - 6)];
+            else if (i >= 9 && i < 12 && j >= 9 && j < 12) g = (i - 9 == j - 9) ? T(1) : T(0);
+            G[e] = g;
+        }
+        __syncthreads();
+        mm21(F, F, Fdt2, tid);
+        __syncthreads();
+        mm21(Fdt2, F, Fdt3, tid);
+        __syncthreads();
+        for (int e = tid; e < 441; e += blockDim.x) {
+            T id = (e / 21 == e % 21) ? T(1) : T(0);
+            Phi[e] = id + F[e] + Fdt2[e] / T(2) + Fdt3[e] / T(6);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            // ---- _predict_new_state (jit_utils.py:46-128), quirk Q1 ----
+            T* q = s_imu + I_Q;
+            T* v = s_imu + I_V;
+            T* p = s_imu + I_P;
+            const T* g = s_imu + I_G;
+            const T* w = s_gyro;
+            const T* acc = s_acc;
+            const bool alias = s_imu[I_ALIAS] != T(0);
+            T v_null[3], p_null[3];
+            for (int i = 0; i < 3; ++i) {   // Q5: entry values once aliased
+                v_null[i] = alias ? v[i] : s_imu[I_VN + i];
+                p_null[i] = alias ? p[i] : s_imu[I_PN + i];
+            }
+            T gn = sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+            T Om[16] = {0, w[2], -w[1], w[0],
+                        -w[2], 0, w[0], w[1],
+                        w[1], -w[0], 0, w[2],
+                        -w[0], -w[1], -w[2], 0};
+            T dq[4], dq2[4];
+            if (gn > T(1e-5)) {
+                T c1 = cos(gn * dt * T(0.5)), s1 = sin(gn * dt * T(0.5)) / gn;
+                T c2 = cos(gn * dt * T(0.25)), s2 = sin(gn * dt * T(0.25)) / gn;
+                for (int i = 0; i < 4; ++i) {
+                    T a1 = 0, a2 = 0;
+                    for (int j = 0; j < 4; ++j) {
+                        T id = (i == j) ? T(1) : T(0);
+                        a1 += (c1 * id + s1 * Om[4 * i + j]) * q[j];
+                        a2 += (c2 * id + s2 * Om[4 * i + j]) * q[j];
+                    }
+                    dq[i] = a1; dq2[i] = a2;
+                }
+            } else {
+                T c1 = cos(gn * dt * T(0.5)), c2 = cos(gn * dt * T(0.25));
+                for (int i = 0; i < 4; ++i) {
+                    T a1 = 0, a2 = 0;
+                    for (int j = 0; j < 4; ++j) {
+                        T id = (i == j) ? T(1) : T(0);
+                        a1 += c1 * (id + Om[4 * i + j] * dt * T(0.5)) * q[j];
+                        a2 += c2 * (id + Om[4 * i + j] * dt * T(0.25)) * q[j];
+                    }
+                    dq[i] = a1; dq2[i] = a2;
+                }
+            }
+            T nq = sqrt(dq[0] * dq[0] + dq[1] * dq[1] + dq[2] * dq[2] + dq[3] * dq[3]);
+            for (int i = 0; i < 4; ++i) dq[i] /= nq;
+            T S1[9];
+            skew3(dq, S1);   // reused for dR_dt2 and k1 (Q1)
+            T dRT[9], dR2T[9], Rk[9];
+            {
+                T ww = dq[3];
+                for (int i = 0; i < 3; ++i)
+                    for (int j = 0; j < 3; ++j)   // transpose stored
+                        dRT[3 * j + i] = (i == j ? 2 * ww * ww - 1 : T(0)) - 2 * ww * S1[3 * i + j] + (2 * dq[i]) * dq[j];
+            }
+            T nq2 = sqrt(dq2[0] * dq2[0] + dq2[1] * dq2[1] + dq2[2] * dq2[2] + dq2[3] * dq2[3]);
+            for (int i = 0; i < 4; ++i) dq2[i] /= nq2;
+            {
+                T ww = dq2[3];
+                for (int i = 0; i < 3; ++i)
+                    for (int j = 0; j < 3; ++j)
+                        dR2T[3 * j + i] = (i == j ? 2 * ww * ww - 1 : T(0)) - 2 * ww * S1[3 * i + j] + (2 * dq2[i]) * dq2[j];
+            }
+            T nq0 = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+            T qn[4] = {q[0] / nq0, q[1] / nq0, q[2] / nq0, q[3] / nq0};
+            {
+                T ww = qn[3];
+                for (int i = 0; i < 3; ++i)
+                    for (int j = 0; j < 3; ++j)
+                        Rk[3 * i + j] = (i == j ? 2 * ww * ww - 1 : T(0)) - 2 * ww * S1[3 * i + j] + (2 * qn[i]) * qn[j];
+            }
+            T k1v[3], k2v[3], k3v[3], k4v[3], v1[3], v2[3], v3[3], tmp[3];
+            mat3T_vec(Rk, acc, tmp);
+            for (int i = 0; i < 3; ++i) k1v[i] = tmp[i] + g[i];
+            for (int i = 0; i < 3; ++i) v1[i] = v[i] + k1v[i] * dt / T(2);
+            mat3_vec(dR2T, acc, tmp);
+            for (int i = 0; i < 3; ++i) k2v[i] = tmp[i] + g[i];
+            for (int i = 0; i < 3; ++i) v2[i] = v[i] + k2v[i] * dt / T(2);
+            for (int i = 0; i < 3; ++i) k3v[i] = tmp[i] + g[i];
+            for (int i = 0; i < 3; ++i) v3[i] = v[i] + k3v[i] * dt;
+            mat3_vec(dRT, acc, tmp);
+            for (int i = 0; i < 3; ++i) k4v[i] = tmp[i] + g[i];
+            T nn = sqrt(dq[0] * dq[0] + dq[1] * dq[1] + dq[2] * dq[2] + dq[3] * dq[3]);
+            T vn[3], pn[3];
+            for (int i = 0; i < 3; ++i) {
+                vn[i] = v[i] + (k1v[i] + 2 * k2v[i] + 2 * k3v[i] + k4v[i]) * dt / T(6);
+                pn[i] = p[i] + (v[i] + 2 * v1[i] + 2 * v2[i] + v3[i]) * dt / T(6);
+            }
+            for (int i = 0; i < 4; ++i) q[i] = dq[i] / nn;
+            for (int i = 0; i < 3; ++i) { v[i] = vn[i]; p[i] = pn[i]; }
+            // ---- Phi edits (msckf.py:329-344) ----
+            T Rkk1[9], Rq[9], Phi00[9];
+            quat_to_rot(s_imu + I_QN, Rkk1);
+            quat_to_rot(q, Rq);
+            for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 3; ++j)
+                    Phi00[3 * i + j] = Rq[3 * i] * Rkk1[3 * j] + Rq[3 * i + 1] * Rkk1[3 * j + 1] + Rq[3 * i + 2] * Rkk1[3 * j + 2];
+            for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 3; ++j) Phi[21 * i + j] = Phi00[3 * i + j];
+            T u[3];
+            mat3_vec(Rkk1, g, u);
+            T uu = u[0] * u[0] + u[1] * u[1] + u[2] * u[2];
+            T s[3] = {u[0] / uu, u[1] / uu, u[2] / uu};
+            T dv[3] = {v_null[0] - v[0], v_null[1] - v[1], v_null[2] - v[2]};
+            T Sk[9], w1[3], w2[3];
+            skew3(dv, Sk);
+            mat3_vec(Sk, g, w1);
+            T dp[3];
+            for (int i = 0; i < 3; ++i) dp[i] = dt * v_null[i] + p_null[i] - p[i];
+            skew3(dp, Sk);
+            mat3_vec(Sk, g, w2);
+            for (int blk = 0; blk < 2; ++blk) {
+                int r0 = blk == 0 ? 6 : 12;
+                const T* wv = blk == 0 ? w1 : w2;
+                T A1[9];
+                for (int i = 0; i < 3; ++i)
+                    for (int j = 0; j < 3; ++j) A1[3 * i + j] = Phi[21 * (r0 + i) + j];
+                for (int i = 0; i < 3; ++i) {
+                    T au = A1[3 * i] * u[0] + A1[3 * i + 1] * u[1] + A1[3 * i + 2] * u[2];
+                    T c = au - wv[i];
+                    for (int j = 0; j < 3; ++j) Phi[21 * (r0 + i) + j] = A1[3 * i + j] - c * s[j];
+                }
+            }
+            for (int i = 0; i < 4; ++i) s_imu[I_QN + i] = q[i];
+            for (int i = 0; i < 3; ++i) { s_imu[I_VN + i] = v[i]; s_imu[I_PN + i] = p[i]; }
+            s_imu[I_ALIAS] = T(1);
+        }
+        __syncthreads();
+        // ---- Q = Phi G Qc G^T Phi^T dt ; P11 = Phi P11 Phi^T + Q (jit_utils.py:130-135)
+        for (int e = tid; e < 252; e += blockDim.x) {
+            int i = e / 12, j = e % 12;
+            T sacc = 0;
+            for (int k2 = 0; k2 < 21; ++k2) sacc += Phi[i * 21 + k2] * G[k2 * 12 + j];
+            T qc = j < 3 ? prm.qc_gyro : (j < 6 ? prm.qc_gbias : (j < 9 ? prm.qc_acc : prm.qc_abias));
+            PG[e] = sacc * qc;
+        }
+        for (int e = tid; e < 441; e += blockDim.x) {   // A = Phi P11
+            int i = e / 21, j = e % 21;
+            T sacc = 0;
+            for (int k2 = 0; k2 < 21; ++k2) sacc += Phi[i * 21 + k2] * P11[k2 * 21 + j];
+            A[e] = sacc;
+        }
+        __syncthreads();
+        for (int e = tid; e < 441; e += blockDim.x) {   // Bm = (Phi G Qc) G^T ; Fdt2 = A Phi^T
+            int i = e / 21, j = e % 21;
+            T s1 = 0, s2 = 0;
+            for (int k2 = 0; k2 < 12; ++k2) s1 += PG[i * 12 + k2] * G[j * 12 + k2];
+            for (int k2 = 0; k2 < 21; ++k2) s2 += A[i * 21 + k2] * Phi[j * 21 + k2];
+            Bm[e] = s1;
+            Fdt2[e] = s2;
+        }
+        __syncthreads();
+        for (int e = tid; e < 441; e += blockDim.x) {   // Q = Bm Phi^T dt ; P11' = A Phi^T + Q
+            int i = e / 21, j = e % 21;
+            T s1 = 0;
+            for (int k2 = 0; k2 < 21; ++k2) s1 += Bm[i * 21 + k2] * Phi[j * 21 + k2];
+            Fdt3[e] = Fdt2[e] + s1 * dt;
+        }
+        mm21(Phi, PhiT, A, tid);   // cumulative Phi
+        __syncthreads();
+        for (int e = tid; e < 441; e += blockDim.x) {
+            int i = e / 21, j = e % 21;
+            P11[e] = (Fdt3[e] + Fdt3[j * 21 + i]) / T(2);
+            PhiT[e] = A[e];
+        }
+        __syncthreads();
+    }
+    // write back P11, IMU record; cross blocks with the cumulative Phi
+    for (int e = tid; e < 441; e += blockDim.x) P[(e / 21) * ld + e % 21] = P11[e];
+    for (int e = tid; e < IMU_STRIDE; e += blockDim.x) imu[e] = s_imu[e];
+    if (n > 0) {
+        for (int j = 21 + tid; j < D; j += blockDim.x) {
+            T col[21], out[21];
+            for (int m = 0; m < 21; ++m) col[m] = P[m * ld + j];
+            for (int i = 0; i < 21; ++i) {
+                T sacc = 0;
+                for (int m = 0; m < 21; ++m) sacc += PhiT[i * 21 + m] * col[m];
+                out[i] = sacc;
+            }
+            for (int i = 0; i < 21; ++i) {
+                P[i * ld + j] = out[i];
+                P[(size_t)j * ld + i] = out[i];
+            }
+        }
+    }
+}
+
+// ===========================================================================
+// State augmentation: one workgroup per filter.
+// ===========================================================================
+template <typename T>
+__global__ void __launch_bounds__(256) k_augment(DevState<T> st, int filter) {
+    __shared__ T J[6 * 21];
+    __shared__ T X[36];
+    const int tid = threadIdx.x;
+    const int b = filter;
+    T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
+    const int ld = st.Dmax;
+    const T* imu = st.imu + (size_t)b * IMU_STRIDE;
+    const int nc = st.ncams[b];
+    const int D = 21 + 6 * nc;
+    if (tid == 0) {
+        T Rwi[9], Rwc[9], t[3], q[4];
+        quat_to_rot(imu + I_Q, Rwi);
+        const T* Ric = imu + I_RIC;
+        mat3_mul(Ric, Rwi, Rwc);
+        mat3T_vec(Rwi, imu + I_TCI, t);          // R_w_i^T t_c_i
+        rot_to_quat(Rwc, q);
+        T* cam = st.cams + ((size_t)b * st.Nmax + nc) * CAM_STRIDE;
+        for (int i = 0; i < 4; ++i) { cam[C_Q + i] = q[i]; cam[C_QN + i] = q[i]; }
+        for (int i = 0; i < 3; ++i) cam[C_P + i] = imu[I_P + i] + t[i];
+        for (int e = 0; e < 126; ++e) J[e] = 0;
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) J[21 * i + j] = Ric[3 * i + j];
+        for (int i = 0; i < 3; ++i) J[21 * i + 15 + i] = 1;
+        T Sk[9];
+        skew3(t, Sk);
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) J[21 * (3 + i) + j] = Sk[3 * i + j];
+        for (int i = 0; i < 3; ++i) { J[21 * (3 + i) + 12 + i] = 1; J[21 * (3 + i) + 18 + i] = 1; }
+    }
+    __syncthreads();
+    for (int j = tid; j < D; j += blockDim.x) {      // J P[0:21, j]
+        T col[21];
+        for (int m = 0; m < 21; ++m) col[m] = P[m * ld + j];
+        for (int r = 0; r < 6; ++r) {
+            T s = 0;
+            for (int m = 0; m < 21; ++m) s += J[21 * r + m] * col[m];
+            P[(size_t)(D + r) * ld + j] = s;
+            P[(size_t)j * ld + D + r] = s;
+        }
+    }
+    if (tid < 36) {                                  // J P11 J^T
+        int r = tid / 6, c = tid % 6;
+        T s = 0;
+        for (int m = 0; m < 21; ++m) {
+            T jp = 0;
+            for (int l = 0; l < 21; ++l) jp += J[21 * r + l] * P[l * ld + m];
+            s += jp * J[21 * c + m];
+        }
+        X[tid] = s;
+    }
+    __syncthreads();
+    if (tid < 36) {
+        int r = tid / 6, c = tid % 6;
+        P[(size_t)(D + r) * ld + D + c] = (X[tid] + X[c * 6 + r]) / T(2);
+    }
+    if (tid == 0) st.ncams[b] = nc + 1;
+}
+
+// ===========================================================================
+// P compaction (msckf.py:803-818): gather kept rows/cols into scratch, copy back.
+// ===========================================================================
+template <typename T>
+__global__ void k_prune_gather(DevState<T> st, int filter, const int* __restrict__ keep, int Dn,
+                               T* __restrict__ scratch) {
+    const T* P = st.P + (size_t)filter * st.Dmax * st.Dmax;
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < Dn * Dn; e += gridDim.x * blockDim.x) {
+        int i = e / Dn, j = e % Dn;
+        scratch[e] = P[(size_t)keep[i] * st.Dmax + keep[j]];
+    }
+}
+
+template <typename T>
+__global__ void k_prune_scatter(DevState<T> st, int filter, int Dn, const T* __restrict__ scratch,
+                                const int* __restrict__ keep_cams, int nkeep) {
+    T* P = st.P + (size_t)filter * st.Dmax * st.Dmax;
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < Dn * Dn; e += gridDim.x * blockDim.x) {
+        int i = e / Dn, j = e % Dn;
+        P[(size_t)i * st.Dmax + j] = scratch[e];
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        T* cams = st.cams + (size_t)filter * st.Nmax * CAM_STRIDE;
+        for (int c = 0; c < nkeep; ++c) {   // keep_cams ascending, in-place forward copy
+            int src = keep_cams[c];
+            if (src != c)
+                for (int e = 0; e < CAM_STRIDE; ++e) cams[c * CAM_STRIDE + e] = cams[src * CAM_STRIDE + e];
+        }
+        st.ncams[filter] = nkeep;
+    }
+}
+
+// ===========================================================================
+// Triangulation: one wavefront per feature, the 2M views spread over the 64
+// lanes (<= 4 per lane), LM sums reduced with xor-shuffles so every lane holds
+// bit-identical totals and runs the (scalar) LM control flow redundantly.
+// ===========================================================================
+constexpr int TRI_VPL = 4;   // views per lane -> up to 128 observations
+
+template <typename T>
+__device__ __forceinline__ void lu3_solve(T A[9], T b[3], T x[3]) {
+    // dgesv-style partial pivoting on a 3x3 system.
+    int piv[3] = {0, 1, 2};
+    for (int k = 0; k < 3; ++k) {
+        int p = k;
+        T m = fabs(A[3 * k + k]);
+        for (int i = k + 1; i < 3; ++i)
+            if (fabs(A[3 * i + k]) > m) { m = fabs(A[3 * i + k]); p = i; }
+        if (p != k) {
+            for (int j = 0; j < 3; ++j) { T t = A[3 * k + j]; A[3 * k + j] = A[3 * p + j]; A[3 * p + j] = t; }
+            T t = b[k]; b[k] = b[p]; b[p] = t;
+            int ti = piv[k]; piv[k] = piv[p]; piv[p] = ti;
+        }
+        for (int i = k + 1; i < 3; ++i) {
+            T l = A[3 * i + k] / A[3 * k + k];
+            A[3 * i + k] = l;
+            for (int j = k + 1; j < 3; ++j) A[3 * i + j] -= l * A[3 * k + j];
+            b[i] -= l * b[k];
+        }
+    }
+    for (int i = 2; i >= 0; --i) {
+        T s = b[i];
+        for (int j = i + 1; j < 3; ++j) s -= A[3 * i + j] * x[j];
+        x[i] = s / A[3 * i + i];
+    }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_triangulate(DevState<T> st, Params<T> prm, FeatBatch<T> fb,
+                                                     int f0, int nfeat) {
+    const int lane = threadIdx.x & 63;
+    const int f = f0 + blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (f >= f0 + nfeat) return;
+    const int b = fb.feat_filter[f];
+    const int o0 = fb.obs_off[f], M = fb.obs_off[f + 1] - o0;
+    const int nv = 2 * M;
+    const T* cams = st.cams + (size_t)b * st.Nmax * CAM_STRIDE;
+    // T_c1_c0 = Iso(R01, t01).inverse()
+    T R10[9], t10[3];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) R10[3 * i + j] = prm.R01[3 * j + i];
+    {
+        T tmp[3];
+        mat3_vec(R10, prm.t01, tmp);
+        for (int i = 0; i < 3; ++i) t10[i] = -tmp[i];
+    }
+    // pose of view v (cam -> world): cam0 = (R_wc^T, p); cam1 = cam0 * T_c1_c0
+    auto view_pose = [&](int v, T* R, T* t) {
+        const T* c = cams + (size_t)fb.obs_cam[o0 + (v >> 1)] * CAM_STRIDE;
+        T Rwc[9];
+        quat_to_rot(c + C_Q, Rwc);
+        T R0[9];
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) R0[3 * i + j] = Rwc[3 * j + i];
+        if ((v & 1) == 0) {
+            for (int e = 0; e < 9; ++e) R[e] = R0[e];
+            for (int i = 0; i < 3; ++i) t[i] = c[C_P + i];
+        } else {
+            mat3_mul(R0, R10, R);
+            T tmp[3];
+            mat3_vec(R0, t10, tmp);
+            for (int i = 0; i < 3; ++i) t[i] = tmp[i] + c[C_P + i];
+        }
+    };
+    T R0w[9], t0w[3];
+    view_pose(0, R0w, t0w);   // T_c0_w
+    // relative poses T_v = pose_v^-1 * T_c0_w (feature.py:209-213)
+    T VR[TRI_VPL][9], Vt[TRI_VPL][3], Vz[TRI_VPL][2];
+#pragma unroll
+    for (int s = 0; s < TRI_VPL; ++s) {
+        int v = lane + 64 * s;
+        if (v < nv) {
+            T R[9], t[3];
+            view_pose(v, R, t);
+            T RT[9];
+            for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 3; ++j) RT[3 * i + j] = R[3 * j + i];
+            mat3_mul(RT, R0w, VR[s]);
+            T a[3], c[3];
+            mat3_vec(RT, t0w, a);
+            mat3_vec(RT, t, c);
+            for (int i = 0; i < 3; ++i) Vt[s][i] = a[i] + -c[i];
+            const T* z = fb.obs_z + (size_t)(o0 + (v >> 1)) * 4 + 2 * (v & 1);
+            Vz[s][0] = z[0];
+            Vz[s][1] = z[1];
+        } else {
+            for (int e = 0; e < 9; ++e) VR[s][e] = 0;
+            for (int i = 0; i < 3; ++i) Vt[s][i] = 0;
+            Vz[s][0] = Vz[s][1] = 0;
+        }
+    }
+    // initial guess from view 0 and the LAST cam0 view (nv-2)  (feature.py:99-122, 216-218)
+    T x[3];
+    {
+        int vl = nv - 2, sl = vl >> 6, ll = vl & 63;
+        T R12[9], t12[3], z2[2], z1[2];
+        // broadcast view vl's transform from its lane (static slot index)
+        for (int e = 0; e < 9; ++e) {
+            T val = VR[0][e];
+#pragma unroll
+            for (int s = 1; s < TRI_VPL; ++s) val = (sl == s) ? VR[s][e] : val;
+            R12[e] = __shfl(val, ll, 64);
+        }
+        for (int i = 0; i < 3; ++i) {
+            T val = Vt[0][i];
+#pragma unroll
+            for (int s = 1; s < TRI_VPL; ++s) val = (sl == s) ? Vt[s][i] : val;
+            t12[i] = __shfl(val, ll, 64);
+        }
+        for (int i = 0; i < 2; ++i) {
+            T val = Vz[0][i];
+#pragma unroll
+            for (int s = 1; s < TRI_VPL; ++s) val = (sl == s) ? Vz[s][i] : val;
+            z2[i] = __shfl(val, ll, 64);
+            z1[i] = __shfl(Vz[0][i], 0, 64);
+        }
+        T z1h[3] = {z1[0], z1[1], T(1)};
+        T m[3];
+        mat3_vec(R12, z1h, m);
+        T a0 = m[0] - z2[0] * m[2], a1 = m[1] - z2[1] * m[2];
+        T b0 = z2[0] * t12[2] - t12[0], b1 = z2[1] * t12[2] - t12[1];
+        T depth = (a0 * b0 + a1 * b1) / (a0 * a0 + a1 * a1);
+        T p0[3] = {z1[0] * depth, z1[1] * depth, depth};
+        x[0] = p0[0] / p0[2];
+        x[1] = p0[1] / p0[2];
+        x[2] = T(1) / p0[2];
+    }
+    auto total_cost = [&](const T* xx) {
+        T c = 0;
+#pragma unroll
+        for (int s = 0; s < TRI_VPL; ++s) {
+            if (lane + 64 * s < nv) {
+                T h[3];
+                for (int i = 0; i < 3; ++i)
+                    h[i] = VR[s][3 * i] * xx[0] + VR[s][3 * i + 1] * xx[1] + VR[s][3 * i + 2] + xx[2] * Vt[s][i];
+                T e0 = h[0] / h[2] - Vz[s][0], e1 = h[1] / h[2] - Vz[s][1];
+                c += e0 * e0 + e1 * e1;
+            }
+        }
+        return wave_sum(c);
+    };
+    T lam = prm.damping;
+    T cost = total_cost(x);
+    bool reduced = false;
+    T dnorm = T(INFINITY);
+    int outer = 0;
+    while (outer < prm.outer_max && dnorm > prm.precision) {
+        // Q2: once a step has been accepted the inner loop never runs again and
+        // the solution cannot change any more -> done.
+        if (reduced) break;
+        T A[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, bb[3] = {0, 0, 0};
+#pragma unroll
+        for (int s = 0; s < TRI_VPL; ++s) {
+            if (lane + 64 * s < nv) {
+                T h[3];
+                for (int i = 0; i < 3; ++i)
+                    h[i] = VR[s][3 * i] * x[0] + VR[s][3 * i + 1] * x[1] + VR[s][3 * i + 2] + x[2] * Vt[s][i];
+                T W[9];
+                for (int i = 0; i < 3; ++i) { W[3 * i] = VR[s][3 * i]; W[3 * i + 1] = VR[s][3 * i + 1]; W[3 * i + 2] = Vt[s][i]; }
+                T J[6];
+                for (int j = 0; j < 3; ++j) {
+                    J[j] = W[j] / h[2] - W[6 + j] * h[0] / (h[2] * h[2]);
+                    J[3 + j] = W[3 + j] / h[2] - W[6 + j] * h[1] / (h[2] * h[2]);
+                }
+                T r0 = h[0] / h[2] - Vz[s][0], r1 = h[1] / h[2] - Vz[s][1];
+                T e = sqrt(r0 * r0 + r1 * r1);
+                T w = e <= prm.huber ? T(1) : prm.huber / (2 * e);
+                T w2 = w * w;
+                for (int i = 0; i < 3; ++i) {
+                    for (int j = 0; j < 3; ++j) A[3 * i + j] += (w2 * J[i]) * J[j] + (w2 * J[3 + i]) * J[3 + j];
+                    bb[i] += (w2 * J[i]) * r0 + (w2 * J[3 + i]) * r1;
+                }
+            }
+        }
+        for (int e = 0; e < 9; ++e) A[e] = wave_sum(A[e]);
+        for (int e = 0; e < 3; ++e) bb[e] = wave_sum(bb[e]);
+        int inner = 0;
+        while (inner < prm.inner_max && !reduced) {
+            T Al[9], bl[3], delta[3];
+            for (int e = 0; e < 9; ++e) Al[e] = A[e];
+            Al[0] += lam; Al[4] += lam; Al[8] += lam;
+            for (int e = 0; e < 3; ++e) bl[e] = bb[e];
+            lu3_solve(Al, bl, delta);
+            T xn[3] = {x[0] - delta[0], x[1] - delta[1], x[2] - delta[2]};
+            dnorm = sqrt(delta[0] * delta[0] + delta[1] * delta[1] + delta[2] * delta[2]);
+            T nc = total_cost(xn);
+            if (nc < cost) {
+                reduced = true;
+                x[0] = xn[0]; x[1] = xn[1]; x[2] = xn[2];
+                cost = nc;
+                lam = fmax(lam / T(10), T(1e-10));
+            } else {
+                reduced = false;
+                lam = fmin(lam * T(10), T(1e12));
+            }
+            ++inner;
+        }
+        ++outer;
+    }
+    T pf[3] = {x[0] / x[2], x[1] / x[2], T(1) / x[2]};
+    bool ok = true;
+#pragma unroll
+    for (int s = 0; s < TRI_VPL; ++s) {
+        if (lane + 64 * s < nv) {
+            T z = VR[s][6] * pf[0] + VR[s][7] * pf[1] + VR[s][8] * pf[2] + Vt[s][2];
+            if (z <= 0) ok = false;
+        }
+    }
+    ok = __all(ok);
+    if (lane == 0) {
+        T pw[3];
+        mat3_vec(R0w, pf, pw);
+        for (int i = 0; i < 3; ++i) fb.p_w[3 * f + i] = pw[i] + t0w[i];
+        fb.valid[f] = ok ? 1 : 0;
+    }
+}
+
+// ===========================================================================
+// Feature Jacobian + left-nullspace projection: one wavefront per feature,
+// lane i owns observation i (and i+64).  Computes the observability-projected
+// 4x6 / 4x3 blocks and residual, Householder-QRs H_f (4M x 3) across the wave
+// with xor-shuffle reductions (LAPACK dlarfg sign convention), and stores the
+// compact factors of H0 = (Q^T Hx)[3:] = (Hx - V diag(tau) W^T)[3:] plus Q^T r.
+// The nullspace basis differs from the reference's SVD basis by an orthogonal
+// transform, to which gating and the update are invariant (quirk Q4).
+// ===========================================================================
+constexpr int FEAT_OPL = 2;   // observations per lane -> M <= 128
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_feature(DevState<T> st, Params<T> prm, FeatBatch<T> fb,
+                                                 int f0, int nfeat) {
+    const int lane = threadIdx.x & 63;
+    const int f = f0 + blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (f >= f0 + nfeat) return;
+    if (!fb.valid[f]) return;
+    const int b = fb.feat_filter[f];
+    const int o0 = fb.obs_off[f], M = fb.obs_off[f + 1] - o0;
+    const T* cams = st.cams + (size_t)b * st.Nmax * CAM_STRIDE;
+    const T* g = st.imu + (size_t)b * IMU_STRIDE + I_G;
+    const T pw[3] = {fb.p_w[3 * f], fb.p_w[3 * f + 1], fb.p_w[3 * f + 2]};
+    T Hx[FEAT_OPL][24], Hf[FEAT_OPL][12], r[FEAT_OPL][4];
+#pragma unroll
+    for (int s = 0; s < FEAT_OPL; ++s) {
+        const int i = lane + 64 * s;
+        for (int e = 0; e < 24; ++e) Hx[s][e] = 0;
+        for (int e = 0; e < 12; ++e) Hf[s][e] = 0;
+        for (int e = 0; e < 4; ++e) r[s][e] = 0;
+        if (i >= M) continue;
+        const T* c = cams + (size_t)fb.obs_cam[o0 + i] * CAM_STRIDE;
+        const T* z = fb.obs_z + (size_t)(o0 + i) * 4;
+        T R0[9], R1[9], t1[3], tmp[3];
+        quat_to_rot(c + C_Q, R0);
+        mat3_mul(prm.R01, R0, R1);
+        mat3T_vec(R1, prm.t01, tmp);
+        for (int k = 0; k < 3; ++k) t1[k] = c[C_P + k] - tmp[k];
+        T d0[3], d1[3], pc0[3], pc1[3];
+        for (int k = 0; k < 3; ++k) { d0[k] = pw[k] - c[C_P + k]; d1[k] = pw[k] - t1[k]; }
+        mat3_vec(R0, d0, pc0);
+        mat3_vec(R1, d1, pc1);
+        // dz/dpc (msckf.py:457-467)
+        T a00 = 1 / pc0[2], a02 = -pc0[0] / (pc0[2] * pc0[2]), a12 = -pc0[1] / (pc0[2] * pc0[2]);
+        T b00 = 1 / pc1[2], b02 = -pc1[0] / (pc1[2] * pc1[2]), b12 = -pc1[1] / (pc1[2] * pc1[2]);
+        // dpc/dxc (msckf.py:469-475): [skew(pc0) | -R0], [R01 skew(pc0) | -R1]
+        T Sk[9], RS[9];
+        skew3(pc0, Sk);
+        mat3_mul(prm.R01, Sk, RS);
+        T D0[18], D1[18];
+        for (int k = 0; k < 3; ++k)
+            for (int l = 0; l < 3; ++l) {
+                D0[6 * k + l] = Sk[3 * k + l];
+                D0[6 * k + 3 + l] = -R0[3 * k + l];
+                D1[6 * k + l] = RS[3 * k + l];
+                D1[6 * k + 3 + l] = -R1[3 * k + l];
+            }
+        T H[24];
+        for (int l = 0; l < 6; ++l) {
+            H[l] = a00 * D0[l] + a02 * D0[12 + l];
+            H[6 + l] = a00 * D0[6 + l] + a12 * D0[12 + l];
+            H[12 + l] = b00 * D1[l] + b02 * D1[12 + l];
+            H[18 + l] = b00 * D1[6 + l] + b12 * D1[12 + l];
+        }
+        // observability constraint (msckf.py:484-490)
+        T u[6], Rn[9], dp[3];
+        quat_to_rot(c + C_QN, Rn);
+        mat3_vec(Rn, g, u);
+        for (int k = 0; k < 3; ++k) dp[k] = pw[k] - c[C_P + k];
+        skew3(dp, Sk);
+        mat3_vec(Sk, g, u + 3);
+        T uu = 0;
+        for (int k = 0; k < 6; ++k) uu += u[k] * u[k];
+        for (int a = 0; a < 4; ++a) {
+            T au = 0;
+            for (int k = 0; k < 6; ++k) au += H[6 * a + k] * u[k];
+            for (int k = 0; k < 6; ++k) Hx[s][6 * a + k] = H[6 * a + k] - au * u[k] / uu;
+            for (int k = 0; k < 3; ++k) Hf[s][3 * a + k] = -Hx[s][6 * a + 3 + k];
+        }
+        r[s][0] = z[0] - pc0[0] / pc0[2];
+        r[s][1] = z[1] - pc0[1] / pc0[2];
+        r[s][2] = z[2] - pc1[0] / pc1[2];
+        r[s][3] = z[3] - pc1[1] / pc1[2];
+    }
+    // ---- Householder QR of H_f across the wave (rows 4i..4i+3 in lane i) ----
+    T V[FEAT_OPL][12];
+    T tau[3];
+#pragma unroll
+    for (int s = 0; s < FEAT_OPL; ++s)
+        for (int e = 0; e < 12; ++e) V[s][e] = 0;
+    for (int j = 0; j < 3; ++j) {
+        T alpha = __shfl(Hf[0][3 * j + j], 0, 64);   // pivot row j lives in lane 0
+        T xs = 0;
+#pragma unroll
+        for (int s = 0; s < FEAT_OPL; ++s)
+            for (int a = 0; a < 4; ++a) {
+                int row = 4 * (lane + 64 * s) + a;
+                if (row > j && lane + 64 * s < M) xs += Hf[s][3 * a + j] * Hf[s][3 * a + j];
+            }
+        xs = wave_sum(xs);
+        T tj = 0, scale = 0, beta = alpha;
+        if (xs != T(0)) {
+            T nrm = sqrt(alpha * alpha + xs);
+            beta = alpha >= 0 ? -nrm : nrm;
+            tj = (beta - alpha) / beta;
+            scale = T(1) / (alpha - beta);
+        }
+        tau[j] = tj;
+        // v_j: v[j] = 1, v[row > j] = Hf[row][j] * scale, 0 above
+#pragma unroll
+        for (int s = 0; s < FEAT_OPL; ++s)
+            for (int a = 0; a < 4; ++a) {
+                int row = 4 * (lane + 64 * s) + a;
+                T v = 0;
+                if (lane + 64 * s < M) v = row == j ? T(1) : (row > j ? Hf[s][3 * a + j] * scale : T(0));
+                V[s][3 * a + j] = v;
+            }
+        // apply H_j to the remaining H_f columns and to r
+        for (int c = j + 1; c <= 3; ++c) {
+            T w = 0;
+#pragma unroll
+            for (int s = 0; s < FEAT_OPL; ++s)
+                for (int a = 0; a < 4; ++a) w += V[s][3 * a + j] * (c < 3 ? Hf[s][3 * a + c] : r[s][a]);
+            w = wave_sum(w);
+#pragma unroll
+            for (int s = 0; s < FEAT_OPL; ++s)
+                for (int a = 0; a < 4; ++a) {
+                    if (c < 3) Hf[s][3 * a + c] -= tj * V[s][3 * a + j] * w;
+                    else r[s][a] -= tj * V[s][3 * a + j] * w;
+                }
+        }
+    }
+    // ---- w_j = v_j^T X_{j-1}: 6 columns per observation, local to the lane ----
+    T d10 = 0, d20 = 0, d21 = 0;
+#pragma unroll
+    for (int s = 0; s < FEAT_OPL; ++s)
+        for (int a = 0; a < 4; ++a) {
+            d10 += V[s][3 * a + 1] * V[s][3 * a];
+            d20 += V[s][3 * a + 2] * V[s][3 * a];
+            d21 += V[s][3 * a + 2] * V[s][3 * a + 1];
+        }
+    d10 = wave_sum(d10);
+    d20 = wave_sum(d20);
+    d21 = wave_sum(d21);
+#pragma unroll
+    for (int s = 0; s < FEAT_OPL; ++s) {
+        const int i = lane + 64 * s;
+        if (i >= M) continue;
+        T W[18];
+        for (int c = 0; c < 6; ++c) {
+            T w0 = 0, w1 = 0, w2 = 0;
+            for (int a = 0; a < 4; ++a) {
+                w0 += V[s][3 * a] * Hx[s][6 * a + c];
+                w1 += V[s][3 * a + 1] * Hx[s][6 * a + c];
+                w2 += V[s][3 * a + 2] * Hx[s][6 * a + c];
+            }
+            w1 -= tau[0] * d10 * w0;
+            w2 -= tau[0] * d20 * w0 + tau[1] * d21 * w1;
+            W[c] = w0; W[6 + c] = w1; W[12 + c] = w2;
+        }
+        T* ws = fb.obs_ws + (size_t)(o0 + i) * OBS_WS;
+        for (int e = 0; e < 24; ++e) ws[OBS_HX + e] = Hx[s][e];
+        for (int e = 0; e < 12; ++e) ws[OBS_V + e] = V[s][e];
+        for (int e = 0; e < 18; ++e) ws[OBS_W + e] = W[e];
+        for (int e = 0; e < 4; ++e) ws[OBS_QR + e] = r[s][e];
+    }
+    if (lane == 0)
+        for (int j = 0; j < 3; ++j) fb.tau[4 * f + j] = tau[j];
+}
+
+// Dense row `row` (0 <= row < 4M) of Q^T Hx for observation column block i.
+template <typename T>
+__device__ __forceinline__ T qthx_entry(const T* ws_row_obs, const T* ws_col_obs, const T* tau,
+                                        int row, int i, int c) {
+    // ws_row_obs: workspace of the observation owning `row`; ws_col_obs: of obs i
+    const int a = row & 3;
+    T v = ((row >> 2) == i) ? ws_row_obs[OBS_HX + 6 * a + c] : T(0);
+    const T* V = ws_row_obs + OBS_V + 3 * a;
+    const T* W = ws_col_obs + OBS_W;
+    return v - (tau[0] * V[0] * W[c] + tau[1] * V[1] * W[6 + c] + tau[2] * V[2] * W[12 + c]);
+}
+
+// ===========================================================================
+// Gating (msckf.py:606-614): one workgroup per feature.
+// S = H0 P H0^T + sigma^2 I is formed in observation space:
+//   Y = Hx P Hx^T (4M x 4M, 4x4 blocks Hx_i P_{s_i s_l} Hx_l^T), then
+//   Q^T Y Q by the three reflectors applied two-sided, S = (Q^T Y Q)[3:,3:] + s2 I,
+// followed by a Cholesky factorisation and a forward solve: gamma = |L^-1 r0|^2.
+// (Same value as the reference's rows-space S; ~10x fewer flops.)
+// ===========================================================================
+template <typename T>
+__global__ void __launch_bounds__(256) k_gate(DevState<T> st, Params<T> prm, FeatBatch<T> fb, int f0) {
+    const int f = f0 + blockIdx.x;
+    const int tid = threadIdx.x;
+    if (!fb.valid[f]) {
+        if (tid == 0) { fb.gamma[f] = T(NAN); fb.accept[f] = 0; }
+        return;
+    }
+    const int b = fb.feat_filter[f];
+    const int o0 = fb.obs_off[f], M = fb.obs_off[f + 1] - o0;
+    const int n4 = 4 * M;
+    const T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
+    const int ld = st.Dmax;
+    T* Y = fb.ysq + fb.ysq_off[f];
+    const T* ws = fb.obs_ws + (size_t)o0 * OBS_WS;
+    __shared__ T s_v[3][512], s_p[512], s_w[512], s_r[512];
+    __shared__ T s_scalar[2];
+    __shared__ int s_fail;
+    // 1. Y blocks (i <= l)
+    const int npairs = M * (M + 1) / 2;
+    for (int pidx = tid; pidx < npairs; pidx += blockDim.x) {
+        int i = 0, rem = pidx;
+        while (rem >= M - i) { rem -= M - i; ++i; }
+        int l = i + rem;
+        const T* Hi = ws + (size_t)i * OBS_WS + OBS_HX;
+        const T* Hl = ws + (size_t)l * OBS_WS + OBS_HX;
+        const int si = fb.obs_cam[o0 + i], sl = fb.obs_cam[o0 + l];
+        const T* Pb = P + (size_t)(21 + 6 * si) * ld + 21 + 6 * sl;
+        T T1[24];
+        for (int a = 0; a < 4; ++a)
+            for (int c = 0; c < 6; ++c) {
+                T s = 0;
+                for (int k = 0; k < 6; ++k) s += Hi[6 * a + k] * Pb[(size_t)k * ld + c];
+                T1[6 * a + c] = s;
+            }
+        for (int a = 0; a < 4; ++a)
+            for (int c = 0; c < 4; ++c) {
+                T s = 0;
+                for (int k = 0; k < 6; ++k) s += T1[6 * a + k] * Hl[6 * c + k];
+                Y[(size_t)(4 * i + a) * n4 + 4 * l + c] = s;
+                Y[(size_t)(4 * l + c) * n4 + 4 * i + a] = s;
+            }
+    }
+    for (int row = tid; row < n4; row += blockDim.x) {
+        const T* w = ws + (size_t)(row >> 2) * OBS_WS;
+        for (int j = 0; j < 3; ++j) s_v[j][row] = w[OBS_V + 3 * (row & 3) + j];
+        s_r[row] = w[OBS_QR + (row & 3)];
+    }
+    __syncthreads();
+    // 2. two-sided reflectors: Y <- H_j Y H_j
+    for (int j = 0; j < 3; ++j) {
+        const T tj = fb.tau[4 * f + j];
+        if (tj == T(0)) continue;
+        for (int a = tid; a < n4; a += blockDim.x) {
+            T s = 0;
+            for (int c = j; c < n4; ++c) s += Y[(size_t)a * n4 + c] * s_v[j][c];
+            s_p[a] = s;
+        }
+        __syncthreads();
+        if (tid < 64) {
+            T s = 0;
+            for (int a = tid; a < n4; a += 64) s += s_v[j][a] * s_p[a];
+            s = wave_sum(s);
+            if (tid == 0) s_scalar[0] = s;
+        }
+        __syncthreads();
+        const T K = tj * tj * s_scalar[0] / T(2);
+        for (int a = tid; a < n4; a += blockDim.x) s_w[a] = tj * s_p[a] - K * s_v[j][a];
+        __syncthreads();
+        for (int e = tid; e < n4 * n4; e += blockDim.x) {
+            int a = e / n4, c = e % n4;
+            Y[e] -= s_v[j][a] * s_w[c] + s_w[a] * s_v[j][c];
+        }
+        __syncthreads();
+    }
+    // 3. S = Y[3:,3:] + s2 I ; Cholesky + forward solve fused (gamma = |L^-1 r0|^2)
+    const int k = n4 - 3;
+    T* S = Y + 3 * (size_t)n4 + 3;
+    if (tid == 0) s_fail = 0;
+    for (int a = tid; a < k; a += blockDim.x) S[(size_t)a * n4 + a] += prm.sigma2;
+    __syncthreads();
+    T gam = 0;
+    for (int j = 0; j < k; ++j) {
+        if (tid == 0) {
+            T d = S[(size_t)j * n4 + j];
+            if (!(d > 0)) { s_fail = 1; d = T(1); }
+            T l = sqrt(d);
+            S[(size_t)j * n4 + j] = l;
+            T y = s_r[3 + j] / l;
+            s_scalar[1] = y;
+            gam += y * y;
+        }
+        __syncthreads();
+        const T ljj = S[(size_t)j * n4 + j];
+        const T yj = s_scalar[1];
+        for (int i = j + 1 + tid; i < k; i += blockDim.x) {
+            T lij = S[(size_t)i * n4 + j] / ljj;
+            S[(size_t)i * n4 + j] = lij;
+            s_r[3 + i] -= lij * yj;
+        }
+        __syncthreads();
+        const int m = k - j - 1;
+        for (int e = tid; e < m * m; e += blockDim.x) {
+            int i = j + 1 + e / m, l = j + 1 + e % m;
+            if (l <= i) S[(size_t)i * n4 + l] -= S[(size_t)i * n4 + j] * S[(size_t)l * n4 + j];
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        if (s_fail) gam = T(INFINITY);
+        fb.gamma[f] = gam;
+        fb.accept[f] = (gam < fb.chi2[f]) ? 1 : 0;
+    }
+}
+
+// ===========================================================================
+// Stacking in feature order with the row cap (msckf.py:671-679): one thread
+// per filter walks its features; decides the compression (msckf.py:549).
+// ===========================================================================
+template <typename T>
+__global__ void k_select(DevState<T> st, FeatBatch<T> fb, UpdWs<T> ws, int row_cap) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= st.B) return;
+    int count = 0;
+    bool capped = false;
+    for (int f = fb.feat_off[b]; f < fb.feat_off[b + 1]; ++f) {
+        fb.include[f] = 0;
+        fb.row_off[f] = 0;
+        if (capped || !fb.valid[f]) continue;
+        if (fb.accept[f]) {
+            const int M = fb.obs_off[f + 1] - fb.obs_off[f];
+            fb.include[f] = 1;
+            fb.row_off[f] = count;
+            count += 4 * M - 3;
+        }
+        if (row_cap > 0 && count > row_cap) capped = true;
+    }
+    const int C = 6 * st.ncams[b];
+    int* info = ws.info + 4 * b;
+    info[0] = count;
+    info[1] = count > C ? C : count;
+    info[2] = count > C ? 1 : 0;
+    info[3] = 0;
+}
+
+// ===========================================================================
+// Stacked-H assembly / QR compression (msckf.py:549-556): one workgroup per
+// filter.  Rows of each included feature are materialised densely over the
+// C cam columns + the residual column in LDS, CHUNK rows at a time, then
+// either copied out (R <= C: no compression, as the reference) or merged into
+// the running triangular factor [R | Q^T r] with one Householder reflector
+// per column (a sequential TSQR; any orthogonal row transform of (H, r)
+// leaves the update unchanged -- quirk Q4).
+// ===========================================================================
+template <typename T> struct CompressCfg;
+template <> struct CompressCfg<float> { static constexpr int CHUNK = 32; };
+template <> struct CompressCfg<double> { static constexpr int CHUNK = 16; };
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_compress(DevState<T> st, FeatBatch<T> fb, UpdWs<T> ws) {
+    constexpr int CH = CompressCfg<T>::CHUNK;
+    // one 16-B aligned dynamic LDS region (Guideline 17): [CH][C+1] chunk, then
+    // the reflector vector, the feature's cam slots and scalars
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    const int C = 6 * st.ncams[blockIdx.x];
+    const int ldb = C + 1;
+    T* Bk = reinterpret_cast<T*>(smem_raw);
+    T* s_v = Bk + (size_t)CH * ((ws.Cmax + 2) & ~1);
+    T* s_sc = s_v + CH;                  // [0] tau of the column reflector, [1..3] tau_f
+    int* s_slot = reinterpret_cast<int*>(s_sc + 4);
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int* info = ws.info + 4 * b;
+    const int R = info[0], n = info[1], compress = info[2];
+    if (R == 0) return;
+    const int ldh = ws.Cmax + 1;
+    T* H = ws.Hthin + (size_t)b * ws.Cmax * ldh;     // column Cmax holds r
+    for (int e = tid; e < n * ldh; e += blockDim.x) H[e] = 0;
+    __syncthreads();
+    for (int f = fb.feat_off[b]; f < fb.feat_off[b + 1]; ++f) {
+        if (!fb.include[f]) continue;
+        const int o0 = fb.obs_off[f], M = fb.obs_off[f + 1] - o0;
+        const T* wsf = fb.obs_ws + (size_t)o0 * OBS_WS;
+        int smin = 1 << 30;
+        for (int i = 0; i < M; ++i) smin = min(smin, fb.obs_cam[o0 + i]);
+        __syncthreads();
+        for (int i = tid; i < M; i += blockDim.x) s_slot[i] = fb.obs_cam[o0 + i];
+        if (tid < 3) s_sc[1 + tid] = fb.tau[4 * f + tid];
+        const int c0 = 6 * smin;
+        const int n4 = 4 * M;
+        for (int a0 = 3; a0 < n4; a0 += CH) {
+            const int nr = min(CH, n4 - a0);
+            __syncthreads();
+            for (int e = tid; e < CH * ldb; e += blockDim.x) Bk[e] = 0;
+            __syncthreads();
+            for (int e = tid; e < nr * M * 6; e += blockDim.x) {
+                int rr = e / (M * 6), q = e % (M * 6), i = q / 6, c = q % 6;
+                int row = a0 + rr;
+                Bk[rr * ldb + 6 * s_slot[i] + c] =
+                    qthx_entry(wsf + (size_t)(row >> 2) * OBS_WS, wsf + (size_t)i * OBS_WS, s_sc + 1, row, i, c);
+            }
+            for (int rr = tid; rr < nr; rr += blockDim.x) {
+                int row = a0 + rr;
+                Bk[rr * ldb + C] = wsf[(size_t)(row >> 2) * OBS_WS + OBS_QR + (row & 3)];
+            }
+            __syncthreads();
+            if (!compress) {   // R <= C: the stacked rows are H_thin (msckf.py:554-556)
+                const int base = fb.row_off[f] + (a0 - 3);
+                for (int e = tid; e < nr * ldb; e += blockDim.x) {
+                    int rr = e / ldb, c = e % ldb;
+                    H[(size_t)(base + rr) * ldh + (c == C ? ws.Cmax : c)] = Bk[e];
+                }
+                continue;
+            }
+            // merge the chunk into [R | Q^T r], one reflector per column
+            for (int c = c0; c < C; ++c) {
+                if (tid < 64) {
+                    T xv = tid < nr ? Bk[tid * ldb + c] : T(0);
+                    T xs = wave_sum(xv * xv);
+                    T alpha = H[(size_t)c * ldh + c];
+                    T tj = 0, scale = 0, beta = alpha;
+                    if (xs != T(0)) {
+                        T nrm = sqrt(alpha * alpha + xs);
+                        beta = alpha >= 0 ? -nrm : nrm;
+                        tj = (beta - alpha) / beta;
+                        scale = T(1) / (alpha - beta);
+                    }
+                    if (tid < nr) s_v[tid] = xv * scale;
+                    if (tid == 0) { s_sc[0] = tj; H[(size_t)c * ldh + c] = beta; }
+                }
+                __syncthreads();
+                const T tj = s_sc[0];
+                if (tj != T(0)) {
+                    for (int j = c + 1 + tid; j <= C; j += blockDim.x) {
+                        T* hj = H + (size_t)c * ldh + (j == C ? ws.Cmax : j);
+                        T w = *hj;
+                        for (int rr = 0; rr < nr; ++rr) w += s_v[rr] * Bk[rr * ldb + j];
+                        T tw = tj * w;
+                        *hj -= tw;
+                        for (int rr = 0; rr < nr; ++rr) Bk[rr * ldb + j] -= s_v[rr] * tw;
+                    }
+                }
+                __syncthreads();
+            }
+        }
+    }
+}
+
+// ===========================================================================
+// Kalman update (msckf.py:559-604) on H_thin (n x C, IMU columns zero):
+//   HP = H_thin P[21:D, :]              k_hp      (n x D)
+//   S  = HP[:, 21:] H_thin^T + s2 I     k_s       (n x n)
+//   S = L L^T ; y_r = L^-1 r_thin        k_chol
+//   Y = L^-1 HP                          k_trsm
+//   dx = Y^T y_r                         k_dx      (= K r_thin)
+//   P <- P - Y^T Y                       k_pupdate (= (I - K H) P, symmetric)
+//   state correction                     k_correct
+// The GEMMs are 32x32 LDS-tiled, one tile per workgroup, batched over filters.
+// ===========================================================================
+constexpr int TB = 32;
+
+// C[i][j] (+)= sum_k A(i,k) B(k,j) with accessor lambdas; tile (ti, tj) of a
+// m x nn output, K = kk, 256 threads, 2x2 outputs per thread.
+template <typename T, typename FA, typename FB, typename FC>
+__device__ __forceinline__ void tile_gemm(int m, int nn, int kk, int ti, int tj, FA A, FB Bf, FC Cf) {
+    __shared__ T sa[TB][TB + 1], sb[TB][TB + 1];
+    const int tid = threadIdx.x;
+    const int tx = tid % 16, ty = tid / 16;
+    T acc[2][2] = {{0, 0}, {0, 0}};
+    for (int k0 = 0; k0 < kk; k0 += TB) {
+        for (int e = tid; e < TB * TB; e += blockDim.x) {
+            int r = e / TB, c = e % TB;
+            int gi = ti * TB + r, gk = k0 + c;
+            sa[r][c] = (gi < m && gk < kk) ? A(gi, gk) : T(0);
+            int gk2 = k0 + r, gj = tj * TB + c;
+            sb[r][c] = (gk2 < kk && gj < nn) ? Bf(gk2, gj) : T(0);
+        }
+        __syncthreads();
+#pragma unroll 8
+        for (int q = 0; q < TB; ++q) {
+            T a0 = sa[ty][q], a1 = sa[ty + 16][q];
+            T b0 = sb[q][tx], b1 = sb[q][tx + 16];
+            acc[0][0] += a0 * b0; acc[0][1] += a0 * b1;
+            acc[1][0] += a1 * b0; acc[1][1] += a1 * b1;
+        }
+        __syncthreads();
+    }
+    for (int u = 0; u < 2; ++u)
+        for (int v = 0; v < 2; ++v) {
+            int gi = ti * TB + ty + 16 * u, gj = tj * TB + tx + 16 * v;
+            if (gi < m && gj < nn) Cf(gi, gj, acc[u][v]);
+        }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_hp(DevState<T> st, UpdWs<T> ws) {
+    const int b = blockIdx.z;
+    const int n = ws.info[4 * b + 1];
+    const int C = 6 * st.ncams[b], D = 21 + C;
+    const int ti = blockIdx.y, tj = blockIdx.x;
+    if (ti * TB >= n || tj * TB >= D) return;
+    const T* H = ws.Hthin + (size_t)b * ws.Cmax * (ws.Cmax + 1);
+    const T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
+    T* HP = ws.HP + (size_t)b * ws.Cmax * st.Dmax;
+    const int ldh = ws.Cmax + 1, ld = st.Dmax;
+    tile_gemm<T>(n, D, C, ti, tj,
+                 [&](int i, int k) { return H[(size_t)i * ldh + k]; },
+                 [&](int k, int j) { return P[(size_t)(21 + k) * ld + j]; },
+                 [&](int i, int j, T v) { HP[(size_t)i * ld + j] = v; });
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_s(DevState<T> st, Params<T> prm, UpdWs<T> ws) {
+    const int b = blockIdx.z;
+    const int n = ws.info[4 * b + 1];
+    const int C = 6 * st.ncams[b];
+    const int ti = blockIdx.y, tj = blockIdx.x;
+    if (ti * TB >= n || tj * TB >= n || tj > ti) return;   // lower triangle of tiles
+    const T* H = ws.Hthin + (size_t)b * ws.Cmax * (ws.Cmax + 1);
+    const T* HP = ws.HP + (size_t)b * ws.Cmax * st.Dmax;
+    T* S = ws.S + (size_t)b * ws.Cmax * ws.Cmax;
+    const int ldh = ws.Cmax + 1, ld = st.Dmax, lds = ws.Cmax;
+    const T s2 = prm.sigma2;
+    tile_gemm<T>(n, n, C, ti, tj,
+                 [&](int i, int k) { return HP[(size_t)i * ld + 21 + k]; },
+                 [&](int k, int j) { return H[(size_t)j * ldh + k]; },
+                 [&](int i, int j, T v) { S[(size_t)i * lds + j] = v + (i == j ? s2 : T(0)); });
+}
+
+// Cholesky of S (lower, in place) + y_r = L^-1 r_thin; one workgroup per filter.
+template <typename T>
+__global__ void __launch_bounds__(256) k_chol(DevState<T> st, UpdWs<T> ws) {
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int n = ws.info[4 * b + 1];
+    if (n == 0) return;
+    T* S = ws.S + (size_t)b * ws.Cmax * ws.Cmax;
+    const int lds = ws.Cmax;
+    const T* H = ws.Hthin + (size_t)b * ws.Cmax * (ws.Cmax + 1);
+    const int ldh = ws.Cmax + 1;
+    __shared__ T s_y[512];
+    __shared__ int s_fail;
+    for (int i = tid; i < n; i += blockDim.x) s_y[i] = H[(size_t)i * ldh + ws.Cmax];
+    if (tid == 0) s_fail = 0;
+    __syncthreads();
+    for (int j = 0; j < n; ++j) {
+        if (tid == 0) {
+            T d = S[(size_t)j * lds + j];
+            if (!(d > 0)) { s_fail = 1; d = T(1); }
+            T l = sqrt(d);
+            S[(size_t)j * lds + j] = l;
+            s_y[j] = s_y[j] / l;
+        }
+        __syncthreads();
+        const T ljj = S[(size_t)j * lds + j];
+        const T yj = s_y[j];
+        for (int i = j + 1 + tid; i < n; i += blockDim.x) {
+            T lij = S[(size_t)i * lds + j] / ljj;
+            S[(size_t)i * lds + j] = lij;
+            s_y[i] -= lij * yj;
+        }
+        __syncthreads();
+        const int m = n - j - 1;
+        for (int e = tid; e < m * m; e += blockDim.x) {
+            int i = j + 1 + e / m, l = j + 1 + e % m;
+            if (l <= i) S[(size_t)i * lds + l] -= S[(size_t)i * lds + j] * S[(size_t)l * lds + j];
+        }
+        __syncthreads();
+    }
+    // store y_r in the residual column of H_thin (no longer needed as r_thin)
+    T* Hw = ws.Hthin + (size_t)b * ws.Cmax * (ws.Cmax + 1);
+    for (int i = tid; i < n; i += blockDim.x) Hw[(size_t)i * ldh + ws.Cmax] = s_y[i];
+    if (tid == 0 && s_fail) ws.info[4 * b + 3] = -1;
+}
+
+// Y = L^-1 HP, one thread per column of HP.
+template <typename T>
+__global__ void __launch_bounds__(256) k_trsm(DevState<T> st, UpdWs<T> ws) {
+    const int b = blockIdx.y;
+    const int n = ws.info[4 * b + 1];
+    const int D = 21 + 6 * st.ncams[b];
+    const int col = blockIdx.x * blockDim.x + threadIdx.x;
+    if (n == 0 || col >= D) return;
+    const T* L = ws.S + (size_t)b * ws.Cmax * ws.Cmax;
+    T* HP = ws.HP + (size_t)b * ws.Cmax * st.Dmax;
+    const int lds = ws.Cmax, ld = st.Dmax;
+    for (int i = 0; i < n; ++i) {
+        T s = HP[(size_t)i * ld + col];
+        for (int j = 0; j < i; ++j) s -= L[(size_t)i * lds + j] * HP[(size_t)j * ld + col];
+        HP[(size_t)i * ld + col] = s / L[(size_t)i * lds + i];
+    }
+}
+
+// dx = Y^T y_r
+template <typename T>
+__global__ void __launch_bounds__(256) k_dx(DevState<T> st, UpdWs<T> ws) {
+    const int b = blockIdx.x;
+    const int n = ws.info[4 * b + 1];
+    const int D = 21 + 6 * st.ncams[b];
+    if (n == 0) return;
+    const T* Y = ws.HP + (size_t)b * ws.Cmax * st.Dmax;
+    const T* H = ws.Hthin + (size_t)b * ws.Cmax * (ws.Cmax + 1);
+    const int ldh = ws.Cmax + 1;
+    T* dx = ws.dx + (size_t)b * st.Dmax;
+    for (int col = threadIdx.x; col < D; col += blockDim.x) {
+        T s = 0;
+        for (int i = 0; i < n; ++i) s += Y[(size_t)i * st.Dmax + col] * H[(size_t)i * ldh + ws.Cmax];
+        dx[col] = s;
+    }
+}
+
+// P <- P - Y^T Y (symmetric by construction: entry (i,j) and (j,i) use the
+// same products in the same order)
+template <typename T>
+__global__ void __launch_bounds__(256) k_pupdate(DevState<T> st, UpdWs<T> ws) {
+    const int b = blockIdx.z;
+    const int n = ws.info[4 * b + 1];
+    const int D = 21 + 6 * st.ncams[b];
+    const int ti = blockIdx.y, tj = blockIdx.x;
+    if (n == 0 || ti * TB >= D || tj * TB >= D) return;
+    const T* Y = ws.HP + (size_t)b * ws.Cmax * st.Dmax;
+    T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
+    const int ld = st.Dmax;
+    tile_gemm<T>(D, D, n, ti, tj,
+                 [&](int i, int k) { return Y[(size_t)k * ld + i]; },
+                 [&](int k, int j) { return Y[(size_t)k * ld + j]; },
+                 [&](int i, int j, T v) { P[(size_t)i * ld + j] -= v; });
+}
+
+// State correction (msckf.py:566-595).
+template <typename T>
+__global__ void __launch_bounds__(64) k_correct(DevState<T> st, UpdWs<T> ws) {
+    const int b = blockIdx.x;
+    const int n = ws.info[4 * b + 1];
+    if (n == 0) return;
+    const T* dx = ws.dx + (size_t)b * st.Dmax;
+    T* imu = st.imu + (size_t)b * IMU_STRIDE;
+    const int nc = st.ncams[b];
+    const int tid = threadIdx.x;
+    if (tid == 0) {
+        T dq[4], q[4];
+        small_angle_quat(dx, dq);
+        quat_mul(dq, imu + I_Q, q);
+        for (int i = 0; i < 4; ++i) imu[I_Q + i] = q[i];
+        for (int i = 0; i < 3; ++i) {
+            imu[I_BG + i] += dx[3 + i];
+            imu[I_V + i] += dx[6 + i];
+            imu[I_BA + i] += dx[9 + i];
+            imu[I_P + i] += dx[12 + i];
+        }
+        T dqe[4], Re[9], Rn[9];
+        small_angle_quat(dx + 15, dqe);
+        quat_to_rot(dqe, Re);
+        mat3_mul(Re, imu + I_RIC, Rn);
+        for (int e = 0; e < 9; ++e) imu[I_RIC + e] = Rn[e];
+        for (int i = 0; i < 3; ++i) imu[I_TCI + i] += dx[18 + i];
+    }
+    T* cams = st.cams + (size_t)b * st.Nmax * CAM_STRIDE;
+    for (int c = tid; c < nc; c += blockDim.x) {
+        const T* d = dx + 21 + 6 * c;
+        T dq[4], q[4];
+        small_angle_quat(d, dq);
+        quat_mul(dq, cams + (size_t)c * CAM_STRIDE + C_Q, q);
+        for (int i = 0; i < 4; ++i) cams[(size_t)c * CAM_STRIDE + C_Q + i] = q[i];
+        for (int i = 0; i < 3; ++i) cams[(size_t)c * CAM_STRIDE + C_P + i] += d[3 + i];
+    }
+}
+
+// ===========================================================================
+// Host launchers
+// ===========================================================================
+template <typename T>
+void launch_propagate(hipStream_t s, const DevState<T>& st, const Params<T>& prm, int filter, int n,
+                      const T* samples) {
+    hipLaunchKernelGGL(k_propagate<T>, dim3(1), dim3(256), 0, s, st, prm, filter, n, samples);
+}
+template <typename T>
+void launch_augment(hipStream_t s, const DevState<T>& st, int filter) {
+    hipLaunchKernelGGL(k_augment<T>, dim3(1), dim3(256), 0, s, st, filter);
+}
+template <typename T>
+void launch_prune(hipStream_t s, const DevState<T>& st, int filter, const int* keep, int Dn, T* scratch,
+                  const int* keep_cams, int nkeep) {
+    int nb = (Dn * Dn + 255) / 256;
+    nb = nb < 1024 ? nb : 1024;
+    hipLaunchKernelGGL(k_prune_gather<T>, dim3(nb), dim3(256), 0, s, st, filter, keep, Dn, scratch);
+    hipLaunchKernelGGL(k_prune_scatter<T>, dim3(nb), dim3(256), 0, s, st, filter, Dn, scratch, keep_cams, nkeep);
+}
+template <typename T>
+void launch_triangulate(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const FeatBatch<T>& fb) {
+    if (fb.nf == 0) return;
+    hipLaunchKernelGGL(k_triangulate<T>, dim3((fb.nf + 3) / 4), dim3(256), 0, s, st, prm, fb, 0, fb.nf);
+}
+template <typename T>
+void launch_feature(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const FeatBatch<T>& fb) {
+    if (fb.nf == 0) return;
+    hipLaunchKernelGGL(k_feature<T>, dim3((fb.nf + 3) / 4), dim3(256), 0, s, st, prm, fb, 0, fb.nf);
+}
+template <typename T>
+void launch_gate(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const FeatBatch<T>& fb) {
+    if (fb.nf == 0) return;
+    hipLaunchKernelGGL(k_gate<T>, dim3(fb.nf), dim3(256), 0, s, st, prm, fb, 0);
+}
+template <typename T>
+void launch_select(hipStream_t s, const DevState<T>& st, const FeatBatch<T>& fb, const UpdWs<T>& ws,
+                   int row_cap) {
+    hipLaunchKernelGGL(k_select<T>, dim3((st.B + 63) / 64), dim3(64), 0, s, st, fb, ws, row_cap);
+}
+template <typename T>
+void launch_compress(hipStream_t s, const DevState<T>& st, const FeatBatch<T>& fb, const UpdWs<T>& ws) {
+    const int CH = CompressCfg<T>::CHUNK;
+    size_t lds = ((size_t)CH * ((ws.Cmax + 2) & ~1) + CH + 4) * sizeof(T) + 128 * sizeof(int);
+    hipLaunchKernelGGL(k_compress<T>, dim3(st.B), dim3(256), lds, s, st, fb, ws);
+}
+template <typename T>
+void launch_kalman(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const UpdWs<T>& ws,
+                   KernelTimer* kt) {
+    const int tc = (ws.Cmax + TB - 1) / TB, td = (st.Dmax + TB - 1) / TB;
+    kt->begin(s, "kalman_hp");
+    hipLaunchKernelGGL(k_hp<T>, dim3(td, tc, st.B), dim3(256), 0, s, st, ws);
+    kt->end(s);
+    kt->begin(s, "kalman_s");
+    hipLaunchKernelGGL(k_s<T>, dim3(tc, tc, st.B), dim3(256), 0, s, st, prm, ws);
+    kt->end(s);
+    kt->begin(s, "kalman_chol");
+    hipLaunchKernelGGL(k_chol<T>, dim3(st.B), dim3(256), 0, s, st, ws);
+    kt->end(s);
+    kt->begin(s, "kalman_trsm");
+    hipLaunchKernelGGL(k_trsm<T>, dim3((st.Dmax + 255) / 256, st.B), dim3(256), 0, s, st, ws);
+    kt->end(s);
+    kt->begin(s, "kalman_dx");
+    hipLaunchKernelGGL(k_dx<T>, dim3(st.B), dim3(256), 0, s, st, ws);
+    kt->end(s);
+    kt->begin(s, "kalman_pupdate");
+    hipLaunchKernelGGL(k_pupdate<T>, dim3(td, td, st.B), dim3(256), 0, s, st, ws);
+    kt->end(s);
+    kt->begin(s, "kalman_correct");
+    hipLaunchKernelGGL(k_correct<T>, dim3(st.B), dim3(64), 0, s, st, ws);
+    kt->end(s);
+}
+
+#define INSTANTIATE(T)                                                                                    \
+    template void launch_propagate<T>(hipStream_t, const DevState<T>&, const Params<T>&, int, int, const T*); \
+    template void launch_augment<T>(hipStream_t, const DevState<T>&, int);                               \
+    template void launch_prune<T>(hipStream_t, const DevState<T>&, int, const int*, int, T*, const int*, int); \
+    template void launch_triangulate<T>(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&); \
+    template void launch_feature<T>(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&); \
+    template void launch_gate<T>(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&); \
+    template void launch_select<T>(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const UpdWs<T>&, int); \
+    template void launch_compress<T>(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const UpdWs<T>&); \
+    template void launch_kalman<T>(hipStream_t, const DevState<T>&, const Params<T>&, const UpdWs<T>&, KernelTimer*);
+INSTANTIATE(float)
+INSTANTIATE(double)
+
+}  // namespace msckf

@@ -1,0 +1,82 @@
+// msckf_launch.h -- host-side launcher declarations + per-kernel HIP-event timer.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "msckf_common.h"
+
+namespace msckf {
+
+// Accumulates device time per kernel name from HIP events recorded on the
+// launch stream (so the measurement sees exactly the stream the kernel runs on).
+struct KernelTimer {
+    bool on = false;
+    struct Pending { std::string name; hipEvent_t a, b; };
+    std::vector<Pending> pending;
+    std::vector<std::string> names;
+    std::vector<double> total_ms;
+    std::vector<int> launches;
+    std::vector<hipEvent_t> pool;
+
+    hipEvent_t get() {
+        if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
+        hipEvent_t e;
+        (void)hipEventCreate(&e);
+        return e;
+    }
+    void begin(hipStream_t s, const char* name) {
+        if (!on) return;
+        Pending p{name, get(), get()};
+        (void)hipEventRecord(p.a, s);
+        pending.push_back(p);
+    }
+    void end(hipStream_t s) {
+        if (!on || pending.empty()) return;
+        (void)hipEventRecord(pending.back().b, s);
+    }
+    // call after the stream is synchronised
+    void collect() {
+        for (auto& p : pending) {
+            float ms = 0.f;
+            (void)hipEventElapsedTime(&ms, p.a, p.b);
+            size_t k = 0;
+            while (k < names.size() && names[k] != p.name) ++k;
+            if (k == names.size()) { names.push_back(p.name); total_ms.push_back(0); launches.push_back(0); }
+            total_ms[k] += ms;
+            launches[k] += 1;
+            pool.push_back(p.a);
+            pool.push_back(p.b);
+        }
+        pending.clear();
+    }
+    void reset() { names.clear(); total_ms.clear(); launches.clear(); }
+    ~KernelTimer() {
+        for (auto& p : pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
+        for (auto e : pool) (void)hipEventDestroy(e);
+    }
+};
+
+template <typename T>
+void launch_propagate(hipStream_t, const DevState<T>&, const Params<T>&, int filter, int n, const T* samples);
+template <typename T>
+void launch_augment(hipStream_t, const DevState<T>&, int filter);
+template <typename T>
+void launch_prune(hipStream_t, const DevState<T>&, int filter, const int* keep, int Dn, T* scratch,
+                  const int* keep_cams, int nkeep);
+template <typename T>
+void launch_triangulate(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&);
+template <typename T>
+void launch_feature(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&);
+template <typename T>
+void launch_gate(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&);
+template <typename T>
+void launch_select(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const UpdWs<T>&, int row_cap);
+template <typename T>
+void launch_compress(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const UpdWs<T>&);
+template <typename T>
+void launch_kalman(hipStream_t, const DevState<T>&, const Params<T>&, const UpdWs<T>&, KernelTimer*);
+
+}  // namespace msckf

@@ -1,0 +1,365 @@
+"""Drop-in host class for the reference filter (MSCKF/msckf.py:104-908).
+
+``MSCKF(config)`` keeps the reference's public API -- ``imu_callback(imu_msg)``
+and ``feature_callback(feature_msg) -> vio_result | None`` with the same
+message tuples -- so it sits behind the existing stereo front-end unchanged.
+
+What stays in Python (host bookkeeping, as SURVEY.md section 8(b) prescribes):
+the IMU message buffer walk, the feature map and its observation dicts, cam-id
+<-> slot bookkeeping, the chi2 table lookup, the ordered 1500-row cap inputs,
+keyframe selection, the online-reset decision and ``publish``.
+What runs on the GPU (through the C-ABI, libmsckf_hip.so): IMU covariance
+propagation, state augmentation, triangulation, measurement Jacobians +
+nullspace projection, gating, stacking, QR compression, the Kalman update and
+covariance compaction.  There is no CPU fallback.
+
+Differences from the reference that are deliberate:
+* the reference's IMU-buffer race between the IMU and vio threads
+  (msckf.py:173 vs 287) is removed -- every call holds the context lock;
+* class-level globals (gravity, next ids, cam0->cam1 extrinsics; quirk Q7) are
+  per-instance, so several filters can live in one process.
+"""
+from __future__ import annotations
+
+import threading
+from collections import OrderedDict, namedtuple
+
+import numpy as np
+
+from . import _lib
+from .config import FilterConfig, chi2_threshold
+from .geometry import Isometry3d, from_two_vectors, to_quaternion, to_rotation
+
+VioResult = namedtuple("vio_result", ["timestamp", "pose", "velocity", "cam0_pose"])
+
+
+class Feature:
+    """Host record of a map feature (reference Feature fields, feature.py:15-31)."""
+    __slots__ = ("id", "observations", "position", "is_initialized")
+
+    def __init__(self, fid):
+        self.id = fid
+        self.observations: "OrderedDict[int, np.ndarray]" = OrderedDict()
+        self.position = np.zeros(3)
+        self.is_initialized = False
+
+
+class MSCKF:
+    ROW_CAP = 1500   # msckf.py:678
+
+    def __init__(self, config=None, dtype=np.float64, device=0, cam_capacity=None):
+        if config is None:
+            config = FilterConfig()
+        elif not isinstance(config, FilterConfig):
+            config = FilterConfig.from_reference(config)
+        self.config = config
+        cap = cam_capacity or (config.max_cam_state_size + 2)
+        self.ctx = _lib.Context(config, n_filters=1, n_cam_capacity=cap, dtype=dtype, device=device)
+        self._lock = threading.RLock()
+        self.imu_msg_buffer = []
+        self.map_server: "OrderedDict[int, Feature]" = OrderedDict()
+        self.cam_ids: list = []            # cam-state ids in slot order (oldest first)
+        self.imu_timestamp = None
+        self.imu_id = None
+        self._next_id = 0
+        self.tracking_rate = None
+        self.is_gravity_set = False
+        self.is_first_img = True
+        self.gate_log = []                 # (frame, dof, rows, accepted) like tools/gen_golden.py
+        self.shape_log = []
+        self._n_published = 0
+        T_cam0_imu = np.linalg.inv(config.T_imu_cam0)
+        self._T_imu_body = Isometry3d(config.T_imu_body[:3, :3], config.T_imu_body[:3, 3])
+        imu = _lib.pack_imu(q=[0, 0, 0, 1], p=np.zeros(3), v=config.velocity, bg=np.zeros(3), ba=np.zeros(3),
+                            q_null=[0, 0, 0, 1], p_null=np.zeros(3), v_null=np.zeros(3),
+                            R_imu_cam0=T_cam0_imu[:3, :3].T, t_cam0_imu=T_cam0_imu[:3, 3],
+                            gravity=config.gravity, alias=False)
+        self.ctx.set_state(0, imu, None, self._initial_cov())
+
+    # ------------------------------------------------------------ helpers --
+    def _initial_cov(self):
+        """msckf.py:820-830"""
+        c = self.config
+        P = np.zeros((21, 21))
+        P[3:6, 3:6] = c.gyro_bias_cov * np.eye(3)
+        P[6:9, 6:9] = c.velocity_cov * np.eye(3)
+        P[9:12, 9:12] = c.acc_bias_cov * np.eye(3)
+        P[15:18, 15:18] = c.extrinsic_rotation_cov * np.eye(3)
+        P[18:21, 18:21] = c.extrinsic_translation_cov * np.eye(3)
+        return P
+
+    def imu_state(self):
+        imu, _, _ = self.ctx.get_state(0, want_P=False)
+        return _lib.unpack_imu(imu)
+
+    def cam_states(self):
+        """OrderedDict cam id -> dict(q, p, q_null) in slot order."""
+        _, cams, _ = self.ctx.get_state(0, want_P=False)
+        return OrderedDict((cid, dict(q=cams[i, 0:4], p=cams[i, 4:7], q_null=cams[i, 7:11]))
+                           for i, cid in enumerate(self.cam_ids))
+
+    def state_cov(self):
+        return self.ctx.get_state(0, want_P=True)[2]
+
+    # ----------------------------------------------------------- callbacks --
+    def imu_callback(self, imu_msg):
+        """msckf.py:166-178"""
+        with self._lock:
+            self.imu_msg_buffer.append(imu_msg)
+            if not self.is_gravity_set and len(self.imu_msg_buffer) >= 200:
+                self._initialize_gravity_and_bias()
+                self.is_gravity_set = True
+
+    def _initialize_gravity_and_bias(self):
+        """msckf.py:235-258"""
+        sw = np.zeros(3)
+        sa = np.zeros(3)
+        for m in self.imu_msg_buffer:
+            sw += m.angular_velocity
+            sa += m.linear_acceleration
+        bg = sw / len(self.imu_msg_buffer)
+        g_imu = sa / len(self.imu_msg_buffer)
+        g = np.array([0.0, 0.0, -np.linalg.norm(g_imu)])
+        imu, _, _ = self.ctx.get_state(0, want_P=False)
+        imu[_lib.I_BG:_lib.I_BG + 3] = bg
+        imu[_lib.I_G:_lib.I_G + 3] = g
+        imu[_lib.I_Q:_lib.I_Q + 4] = from_two_vectors(-g, g_imu)
+        self.ctx.set_state(0, imu, None, self._initial_cov() if not self.cam_ids else None)
+
+    def feature_callback(self, feature_msg):
+        """msckf.py:180-233"""
+        with self._lock:
+            if not self.is_gravity_set:
+                return None
+            if self.is_first_img:
+                self.is_first_img = False
+                self.imu_timestamp = feature_msg.timestamp
+            self._batch_imu_processing(feature_msg.timestamp)
+            self._state_augmentation()
+            self._add_feature_observations(feature_msg)
+            self._remove_lost_features()
+            self._prune_cam_state_buffer()
+            try:
+                return self.publish(feature_msg.timestamp)
+            finally:
+                self._n_published += 1
+                self._online_reset()
+
+    # ---------------------------------------------------------- propagation --
+    def _batch_imu_processing(self, time_bound):
+        """msckf.py:262-287: host walks the buffer, the device applies the samples."""
+        used = 0
+        dts, ws, accs = [], [], []
+        t_state = self.imu_timestamp
+        for m in self.imu_msg_buffer:
+            t = m.vio_timestamp__
+            if t < t_state:
+                used += 1
+                continue
+            if t > time_bound:
+                break
+            dts.append(t - t_state)
+            ws.append(m.angular_velocity)
+            accs.append(m.linear_acceleration)
+            used += 1
+            t_state = t
+        if dts:
+            self.ctx.propagate(0, np.array(dts), np.array(ws), np.array(accs))
+        self.imu_timestamp = t_state
+        self.imu_id = self._next_id
+        self._next_id += 1
+        self.imu_msg_buffer = self.imu_msg_buffer[used:]
+
+    def _state_augmentation(self):
+        """msckf.py:385-407"""
+        self.ctx.augment(0)
+        self.cam_ids.append(self.imu_id)
+
+    def _add_feature_observations(self, feature_msg):
+        """msckf.py:409-427"""
+        sid = self.imu_id
+        cur = len(self.map_server)
+        tracked = 0
+        for f in feature_msg.vio_features:
+            z = np.array([f.u0, f.v0, f.u1, f.v1], dtype=float)
+            feat = self.map_server.get(f.id)
+            if feat is None:
+                feat = Feature(f.id)
+                feat.observations[sid] = z
+                self.map_server[f.id] = feat
+            else:
+                feat.observations[sid] = z
+                tracked += 1
+        self.tracking_rate = tracked / (cur + 1e-5)
+
+    # -------------------------------------------------------------- updates --
+    def _pack(self, feats, cam_lists):
+        slot = {cid: i for i, cid in enumerate(self.cam_ids)}
+        off = [0]
+        cams, zs = [], []
+        for feat, cl in zip(feats, cam_lists):
+            for cid in cl:
+                cams.append(slot[cid])
+                zs.append(feat.observations[cid])
+            off.append(len(cams))
+        return (np.array(off, np.int32), np.array(cams, np.int32),
+                np.array(zs, float).reshape(-1, 4))
+
+    def _triangulate(self, feats):
+        """Feature.initialize_position (feature.py:167-295) for a batch of
+        features, one wavefront each on the device."""
+        if not feats:
+            return
+        off, cams, zs = self._pack(feats, [list(f.observations.keys()) for f in feats])
+        p, ok = self.ctx.triangulate(0, off, cams, zs)
+        for f, pi, oki in zip(feats, p, ok):
+            f.position = pi
+            f.is_initialized = bool(oki)
+
+    def _update(self, feats, cam_lists, dofs, row_cap):
+        """Stacked update over ``feats`` in order (device: jacobian, gating,
+        stacking with the row cap, QR, Kalman).  Returns accepted flags."""
+        if not feats:
+            return np.zeros(0, bool)
+        off, cams, zs = self._pack(feats, cam_lists)
+        chi2 = np.array([chi2_threshold(d) for d in dofs])
+        pw = np.array([f.position for f in feats])
+        acc, gam, rows = self.ctx.update(0, off, cams, zs, pw, chi2, row_cap)
+        # reproduce the reference's decision log: features after the row-cap
+        # break are never gated (msckf.py:678-679)
+        count = 0
+        D = 21 + 6 * len(self.cam_ids)
+        for i, f in enumerate(feats):
+            k = 4 * len(cam_lists[i]) - 3
+            ok = bool(gam[i] < chi2[i])
+            self.gate_log.append((self._n_published, dofs[i], k, int(ok)))
+            if ok:
+                count += k
+            if row_cap and count > row_cap:
+                break
+        self.shape_log.append((self._n_published, rows, D))
+        return acc
+
+    def _remove_lost_features(self):
+        """msckf.py:616-689"""
+        sid = self.imu_id
+        invalid, candidates = [], []
+        for feat in self.map_server.values():
+            if sid in feat.observations:
+                continue
+            if len(feat.observations) < 3:
+                invalid.append(feat.id)
+                continue
+            candidates.append(feat)
+        # check_motion is always True with the EuRoC config (translation
+        # threshold -1, config.py:10); triangulations are independent of each
+        # other, so they are batched into one launch.
+        if self.config.optimization.translation_threshold >= 0:
+            raise NotImplementedError("check_motion with a positive translation threshold")
+        self._triangulate([f for f in candidates if not f.is_initialized])
+        processed = []
+        for feat in candidates:
+            if not feat.is_initialized:
+                invalid.append(feat.id)
+            else:
+                processed.append(feat)
+        for fid in invalid:
+            del self.map_server[fid]
+        if not processed:
+            return
+        cam_lists = [list(f.observations.keys()) for f in processed]
+        dofs = [len(cl) - 1 for cl in cam_lists]
+        self._update(processed, cam_lists, dofs, self.ROW_CAP)
+        for feat in processed:
+            del self.map_server[feat.id]
+
+    def _find_redundant_cam_states(self):
+        """msckf.py:691-727 (host; needs the cam poses)."""
+        cams = list(self.cam_states().items())
+        key = len(cams) - 4
+        ci = key + 1
+        first = 0
+        kp = cams[key][1]["p"]
+        kR = to_rotation(cams[key][1]["q"])
+        rm = []
+        for _ in range(2):
+            pos = cams[ci][1]["p"]
+            Rc = to_rotation(cams[ci][1]["q"])
+            dist = np.linalg.norm(pos - kp)
+            ang = 2 * np.arccos(to_quaternion(Rc @ kR.T)[-1])
+            if ang < 0.2618 and dist < 0.4 and self.tracking_rate > 0.5:
+                rm.append(cams[ci][0])
+                ci += 1
+            else:
+                rm.append(cams[first][0])
+                first += 1
+                ci += 1
+        return sorted(rm)
+
+    def _prune_cam_state_buffer(self):
+        """msckf.py:730-818"""
+        if len(self.cam_ids) < self.config.max_cam_state_size:
+            return
+        rm = self._find_redundant_cam_states()
+        to_init = []
+        for feat in self.map_server.values():
+            inv = [c for c in rm if c in feat.observations]
+            if len(inv) == 0:
+                continue
+            if len(inv) == 1:
+                del feat.observations[inv[0]]
+                continue
+            if not feat.is_initialized:
+                to_init.append(feat)
+        self._triangulate(to_init)
+        for feat in to_init:
+            if not feat.is_initialized:
+                for c in rm:
+                    if c in feat.observations:
+                        del feat.observations[c]
+        feats, cam_lists = [], []
+        for feat in self.map_server.values():
+            inv = [c for c in rm if c in feat.observations]
+            if len(inv) == 0:
+                continue
+            feats.append(feat)
+            cam_lists.append(inv)
+        if feats:
+            self._update(feats, cam_lists, [len(cl) for cl in cam_lists], 0)
+        else:   # the reference still calls measurement_update with an empty H
+            self.shape_log.append((self._n_published, 0, 21 + 6 * len(self.cam_ids)))
+        for feat, cl in zip(feats, cam_lists):
+            for c in cl:
+                del feat.observations[c]
+        slots = [self.cam_ids.index(c) for c in rm]
+        self.ctx.prune(0, slots)
+        for c in rm:
+            self.cam_ids.remove(c)
+
+    # ------------------------------------------------------ output / reset --
+    def publish(self, time):
+        """msckf.py:888-908"""
+        s = self.imu_state()
+        T_i_w = Isometry3d(to_rotation(s["q"]).T, s["p"])
+        Tb = self._T_imu_body
+        T_b_w = Tb * T_i_w * Tb.inverse()
+        body_velocity = Tb._vio_R__ @ s["v"]
+        R_w_c = s["R_imu_cam0"] @ T_i_w._vio_R__.T
+        t_c_w = s["p"] + T_i_w._vio_R__ @ s["t_cam0_imu"]
+        return VioResult(time, T_b_w, body_velocity, Isometry3d(R_w_c.T, t_c_w))
+
+    def _online_reset(self):
+        """msckf.py:859-886"""
+        thr = self.config.position_std_threshold
+        if thr <= 0:
+            return
+        d = self.ctx.cov_diag(0, 12, 3)
+        if np.max(np.sqrt(d)) < thr:
+            return
+        self.cam_ids.clear()
+        self.map_server.clear()
+        imu, _, _ = self.ctx.get_state(0, want_P=False)
+        self.ctx.set_state(0, imu, None, self._initial_cov())
+
+    def close(self):
+        self.ctx.close()
