@@ -1,0 +1,211 @@
+"""Throughput bench: EKF measurement updates/s at 30 cam-states x 200 features.
+
+One "step" = one batched EKF measurement update of B independent filters
+(SURVEY.md 8(d) unit of work): triangulation of every feature, per-feature
+Jacobian + nullspace projection + chi2 gating, stacking (no row cap), QR
+compression and the Kalman / covariance update -- on inputs already resident in
+HBM.  Each step first restores the filters' pristine state on the device (a
+D2D copy that is counted inside the timed region) so every step does
+identical work.
+
+  python bench.py [--gpus N --steps K --warmup W --batch B --N 30 --F 200 --dtype fp32]
+
+For N > 1 it runs under torch.distributed.run, one rank per GPU; ranks are
+independent replicas (the filter does not shard); RCCL is only
+used for the start/stop barriers and the max-over-ranks of the timing.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+import msckf_pkg  # noqa: E402,F401
+from msckf_amd import synth, FilterConfig, CHI2_05  # noqa: E402
+from msckf_amd._lib import Context, pack_imu, pack_cams  # noqa: E402
+
+METRIC = "EKF measurement updates/sec at 30 cam-states x 200 features; ATE RMSE vs ref"
+HBM_PEAK_GBS = 8000.0
+FP32_PEAK_TFLOPS = 157.3      # MI355X dense FP32 (vector = MFMA f32 rate), MI355X_MICROARCH.md
+FP64_PEAK_TFLOPS = 78.6
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=512, help="independent filters per GPU per step")
+    ap.add_argument("--N", type=int, default=30)
+    ap.add_argument("--F", type=int, default=200)
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "fp64"])
+    ap.add_argument("--unique", type=int, default=32, help="distinct synthetic problems tiled over the batch")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-baseline sample")
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def build_batch(args, rank):
+    probs = [synth.make_update_problem(args.N, args.F, seed=1000 * rank + u) for u in range(min(args.unique, args.batch))]
+    B = args.batch
+    dtype = np.float32 if args.dtype == "fp32" else np.float64
+    ctx = Context(FilterConfig(), n_filters=B, n_cam_capacity=args.N, dtype=dtype,
+                  device=int(os.environ.get("LOCAL_RANK", 0)))
+    feat_off, obs_off, cams, zs, chi = [0], [0], [], [], []
+    for b in range(B):
+        p = probs[b % len(probs)]
+        imu = pack_imu(q=p.imu["q"], p=p.imu["p"], v=p.imu["v"], bg=p.imu["bg"], ba=p.imu["ba"],
+                       q_null=p.imu["q_null"], p_null=p.imu["p_null"], v_null=p.imu["v_null"],
+                       R_imu_cam0=p.imu["R_imu_cam0"], t_cam0_imu=p.imu["t_cam0_imu"], gravity=p.gravity,
+                       alias=True)
+        ctx.set_state(b, imu, pack_cams(p.cam_q, p.cam_p, p.cam_q_null), p.P)
+        feat_off.append(feat_off[-1] + p.F)
+        obs_off.extend(list(obs_off[-1] + p.obs_off[1:]))
+        cams.append(p.obs_cam)
+        zs.append(p.obs_z)
+        chi.extend(CHI2_05[m - 2] for m in p.track_lengths())
+    ctx.batch_load(np.array(feat_off), np.array(obs_off), np.concatenate(cams), np.concatenate(zs),
+                   None, np.array(chi))
+    ctx.snapshot()
+    return ctx, probs
+
+
+def flops_model(probs, B, accepted, feat_off):
+    """Algorithmic flops of one step, per kernel, from the realised shapes.
+    'canonical' = SURVEY.md 8(d) per-update formula (dense Householder QR on
+    the stacked R x C matrix, rows-space gating)."""
+    tot = {"canonical": 0.0, "compress": 0.0, "gate": 0.0}
+    for b in range(B):
+        p = probs[b % len(probs)]
+        C = 6 * p.N
+        D = 21 + C
+        M = p.track_lengths()
+        acc = accepted[feat_off[b]:feat_off[b + 1]]
+        k = 4 * M - 3
+        # gating as the kernel does it: Y blocks (480 M^2 / 2 pair flops x2), 3 two-sided reflectors, Cholesky
+        tot["gate"] += float(np.sum(480.0 * M * (M + 1) / 2 + 3 * 6 * (4 * M) ** 2 + k ** 3 / 3 + 2 * k ** 2))
+        # compress: per included feature, each of its k rows is merged column by column from its first cam
+        c0 = 6 * np.array([p.obs_cam[p.obs_off[f]:p.obs_off[f + 1]].min() for f in range(p.F)])
+        w = (C - c0).astype(float)
+        tot["compress"] += float(np.sum(acc * 2.0 * k * w * (w + 1)))
+        R = float(np.sum(k * acc))
+        n = min(R, C)
+        F_proj = float(np.sum(48.0 * M * (6 * M + 1)))
+        F_gate = float(np.sum(2 * k * (6 * M) ** 2 + 2 * k ** 2 * (6 * M) + k ** 3 / 3 + 2 * k ** 2))
+        F_qr = 2 * C * C * (R - C / 3) + 4 * R * C if R > C else 0.0
+        F_kal = 2 * n * C * D + 2 * n * n * C + n ** 3 / 3 + 2 * n * n * D + 2 * n * D + 2 * n * D * D + D * D
+        tot["canonical"] += F_proj + F_gate + F_qr + F_kal
+    return tot
+
+
+def cpu_baseline(args, probs):
+    """Oracle (numpy restatement of the reference, 1 BLAS thread) on a bounded
+    sample of the same workload."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from helpers import problem_to_dict, oracle_update
+    try:
+        from threadpoolctl import threadpool_limits
+        lim = threadpool_limits(1)
+    except Exception:
+        lim = None
+    done, t0 = 0, time.perf_counter()
+    oracle_update(problem_to_dict(probs[0]))          # warm-up
+    t0 = time.perf_counter()
+    while True:
+        oracle_update(problem_to_dict(probs[done % len(probs)]))
+        done += 1
+        el = time.perf_counter() - t0
+        if el > args.cpu_seconds or done >= 20:
+            break
+    if lim is not None:
+        lim.unregister() if hasattr(lim, "unregister") else None
+    return {"value": done / el, "unit": "updates/s", "cores": 1, "kind": "port",
+            "sample": "%d synthetic %dx%d updates (triangulation + jacobian + gating + QR + Kalman), "
+                      "numpy/OpenBLAS 1 thread, oracle/msckf_oracle.py" % (done, args.N, args.F)}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        lr = int(os.environ.get("LOCAL_RANK", 0))
+        torch.cuda.set_device(lr)
+        dist.init_process_group("nccl")
+    ctx, probs = build_batch(args, rank)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        ctx.restore()
+        ctx.batch_update(row_cap=0, triangulate=True)
+    ctx.sync()
+    acc, gam, pw, valid, rows = ctx.batch_results()
+    ctx.set_profiling(True)
+    barrier()
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ctx.restore()
+        ctx.batch_update(row_cap=0, triangulate=True)
+    ctx.sync()
+    barrier()
+    el = time.perf_counter() - t0
+    times = ctx.kernel_times()
+    if dist is not None:
+        import torch
+        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    updates = args.batch * world * args.steps
+    value = updates / el
+    feat_off = np.concatenate([[0], np.cumsum([probs[b % len(probs)].F for b in range(args.batch)])])
+    fl = flops_model(probs, args.batch, acc, feat_off)
+    # dominant kernel by device time
+    kern = {k: v for k, v in times.items() if k != "restore"}
+    dom = max(kern, key=lambda k: kern[k][0])
+    dom_ms = kern[dom][0] / max(kern[dom][1], 1)
+    dom_flops = fl.get(dom.replace("kalman_", ""), None)
+    peak = FP32_PEAK_TFLOPS if args.dtype == "fp32" else FP64_PEAK_TFLOPS
+    roof = None
+    if dom_flops:
+        ach = dom_flops / (dom_ms * 1e-3) / 1e12
+        roof = {"bound": "mfma", "kernel": dom, "achieved": round(ach, 3), "peak": peak, "unit": "TFLOP/s",
+                "frac": round(ach / peak, 5), "traffic": None, "avg_launch_ms": round(dom_ms, 4),
+                "flops_per_launch": dom_flops}
+    out = {
+        "metric": METRIC, "value": round(value, 2), "unit": "updates/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f32" if args.dtype == "fp32" else "f64",
+        "data": "synthetic (SURVEY.md 8(d) generator: %d distinct problems tiled over %d filters per GPU)"
+                % (len(probs), args.batch),
+        "config": {"workload": "batched EKF measurement update, %d cam-states x %d features, %d filters/GPU, "
+                               "triangulation + jacobian + gating + QR + Kalman, no row cap" % (args.N, args.F, args.batch),
+                   "cam_states": args.N, "features": args.F, "filters_per_gpu": args.batch,
+                   "stacked_rows_mean": float(np.mean(rows)), "parallelism": "replicas%d" % world},
+        "roofline": roof,
+        "kernel_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in sorted(times.items(), key=lambda kv: -kv[1][0])},
+        "canonical_gflop_per_update": round(fl["canonical"] / args.batch / 1e9, 4),
+        "canonical_tflops": round(fl["canonical"] * args.steps * world / el / 1e12, 3),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(args, probs)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

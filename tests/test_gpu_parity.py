@@ -279,10 +279,12 @@ def test_sequence_golden():
     np.testing.assert_array_equal(np.array(flt.shape_log), g["shapes"])
     assert rec.shape == g["rec"].shape
     ref = g["rec"]
-    # state vector rows: q, p, v, bg, ba, R_ic, t_ci  (cols 1..31)
+    # record: t | q p v bg ba R_ic t_ci (cols 1..28) | |P|_F trace(P) | D #cams #features | cam0 pose
     for k in range(len(ref)):
-        x, xr = rec[k, 1:32], ref[k, 1:32]
+        x, xr = rec[k, 1:29], ref[k, 1:29]
         assert np.linalg.norm(x - xr) <= 1e-6 * np.linalg.norm(xr), k
-        assert abs(rec[k, 32] - ref[k, 32]) <= 1e-6 * ref[k, 32], k     # |P|_F
-    np.testing.assert_array_equal(rec[:, 34:37], ref[:, 34:37])          # D, #cams, #features
+        assert abs(rec[k, 29] - ref[k, 29]) <= 1e-6 * ref[k, 29], k     # |P|_F
+    np.testing.assert_array_equal(rec[:, 31:34], ref[:, 31:34])          # D, #cams, #features
+    worst = max(np.linalg.norm(rec[k, 1:29] - ref[k, 1:29]) / np.linalg.norm(ref[k, 1:29]) for k in range(len(ref)))
+    print("sequence: worst per-frame state deviation %.3e" % worst)
     assert rel(flt.state_cov(), g["P_final"]) < 1e-6
