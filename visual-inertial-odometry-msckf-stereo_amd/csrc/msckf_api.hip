@@ -71,7 +71,7 @@ struct msckf_ctx {
     DBuf<unsigned char> Hthin, HP, S, dx;
     DBuf<int> info;
     // feature batch
-    int nf = 0;
+    int nf = 0, maxM = 0;
     std::vector<int> h_feat_off;
     DBuf<int> feat_filter, feat_off, obs_off, obs_cam, row_off;
     DBuf<long long> ysq_off;
@@ -207,8 +207,10 @@ int load_features(msckf_ctx* c, int nf, const int32_t* feat_off, int single_filt
     if (obs_off[0] != 0) FAIL(-1, "obs_off[0] must be 0");
     const size_t nobs = nf > 0 ? (size_t)obs_off[nf] : 0;
     std::vector<long long> ysq(nf + 1, 0);
+    int maxM = 0;
     for (int f = 0; f < nf; ++f) {
         int M = obs_off[f + 1] - obs_off[f];
+        maxM = std::max(maxM, M);
         int b = h_filt[f];
         if (M < 1 || M > 128) FAIL(-1, "feature %d has %d observations (1..128 supported)", f, M);
         if (M > c->h_ncams[b]) FAIL(-1, "feature %d has more observations than cam states", f);
@@ -256,6 +258,7 @@ int load_features(msckf_ctx* c, int nf, const int32_t* feat_off, int single_filt
     }
     HIPC(hipStreamSynchronize(s));
     c->nf = nf;
+    c->maxM = maxM;
     c->h_feat_off = h_off;
     return 0;
 }
@@ -276,7 +279,7 @@ int run_update_chain(msckf_ctx* c, int row_cap, bool triangulate) {
     launch_feature<T>(s, st, prm, fb);
     c->timer.end(s);
     c->timer.begin(s, "gate");
-    launch_gate<T>(s, st, prm, fb);
+    launch_gate<T>(s, st, prm, fb, c->maxM);
     c->timer.end(s);
     c->timer.begin(s, "select");
     launch_select<T>(s, st, fb, ws, row_cap);

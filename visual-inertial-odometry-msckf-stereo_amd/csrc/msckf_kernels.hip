@@ -13,7 +13,7 @@
 //   measurement_jacobian + feature_jacobian msckf.py:429-541        -> k_feature
 //   gating_test msckf.py:606-614                                    -> k_gate
 //   stacking + row cap msckf.py:661-682, 776-798                    -> k_select
-//   measurement_update QR msckf.py:549-556 (_fastQR)                -> k_compress
+//   measurement_update QR msckf.py:549-556 (_fastQR)                -> k_compress_reg
 //   measurement_update S, K, dx, P msckf.py:559-604 (_fastSolve)    -> k_hp, k_s,
 //                                  k_chol, k_trsm, k_dx, k_pupdate, k_correct
 //   P compaction msckf.py:803-818                                   -> k_prune_*
@@ -923,6 +923,125 @@ __global__ void __launch_bounds__(256) k_gate(DevState<T> st, Params<T> prm, Fea
     }
 }
 
+// Fast path of k_gate with Y / S resident in LDS (ld = 4M+1, odd: conflict-free
+// row and column sweeps) and gamma from an LDL^T elimination with the residual
+// carried along as an extra column: gamma = sum_j r~_j^2 / d_j.  One barrier
+// per pivot; the column being eliminated is read-only during its step.
+template <typename T>
+__global__ void __launch_bounds__(256) k_gate_lds(DevState<T> st, Params<T> prm, FeatBatch<T> fb, int f0) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    const int f = f0 + blockIdx.x;
+    const int tid = threadIdx.x;
+    if (!fb.valid[f]) {
+        if (tid == 0) { fb.gamma[f] = T(NAN); fb.accept[f] = 0; }
+        return;
+    }
+    const int b = fb.feat_filter[f];
+    const int o0 = fb.obs_off[f], M = fb.obs_off[f + 1] - o0;
+    const int n4 = 4 * M, ld = n4 + 1;
+    const T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
+    const int ldp = st.Dmax;
+    const T* ws = fb.obs_ws + (size_t)o0 * OBS_WS;
+    T* Y = reinterpret_cast<T*>(smem_raw);                       // [n4][n4+1]
+    T* s_hx = Y + (((size_t)n4 * ld + 1) & ~(size_t)1);           // [n4][6]
+    T* s_v = s_hx + 6 * n4;                                       // [3][n4]
+    T* s_r = s_v + 3 * n4;                                        // [n4]
+    T* s_p = s_r + n4;                                            // [n4]
+    T* s_w = s_p + n4;                                            // [n4]
+    T* s_sc = s_w + n4;                                           // [4]
+    int* s_slot = reinterpret_cast<int*>(s_sc + 4);               // [M]
+    for (int e = tid; e < n4 * 6; e += blockDim.x) s_hx[e] = ws[(size_t)(e / 24) * OBS_WS + OBS_HX + e % 24];
+    for (int row = tid; row < n4; row += blockDim.x) {
+        const T* w = ws + (size_t)(row >> 2) * OBS_WS;
+        for (int j = 0; j < 3; ++j) s_v[j * n4 + row] = w[OBS_V + 3 * (row & 3) + j];
+        s_r[row] = w[OBS_QR + (row & 3)];
+    }
+    for (int i = tid; i < M; i += blockDim.x) s_slot[i] = fb.obs_cam[o0 + i];
+    __syncthreads();
+    // 1. Y = Hx P Hx^T, 4x4 blocks
+    const int npairs = M * (M + 1) / 2;
+    for (int pidx = tid; pidx < npairs; pidx += blockDim.x) {
+        int i = 0, rem = pidx;
+        while (rem >= M - i) { rem -= M - i; ++i; }
+        const int l = i + rem;
+        const T* Hi = s_hx + 24 * i;
+        const T* Hl = s_hx + 24 * l;
+        const T* Pb = P + (size_t)(21 + 6 * s_slot[i]) * ldp + 21 + 6 * s_slot[l];
+        T Pl[36];
+        for (int k = 0; k < 6; ++k)
+            for (int c = 0; c < 6; ++c) Pl[6 * k + c] = Pb[(size_t)k * ldp + c];
+        T T1[24];
+        for (int a = 0; a < 4; ++a)
+            for (int c = 0; c < 6; ++c) {
+                T sacc = 0;
+                for (int k = 0; k < 6; ++k) sacc += Hi[6 * a + k] * Pl[6 * k + c];
+                T1[6 * a + c] = sacc;
+            }
+        for (int a = 0; a < 4; ++a)
+            for (int c = 0; c < 4; ++c) {
+                T sacc = 0;
+                for (int k = 0; k < 6; ++k) sacc += T1[6 * a + k] * Hl[6 * c + k];
+                Y[(4 * i + a) * ld + 4 * l + c] = sacc;
+                Y[(4 * l + c) * ld + 4 * i + a] = sacc;
+            }
+    }
+    __syncthreads();
+    // 2. Y <- H_j Y H_j for the three reflectors
+    for (int j = 0; j < 3; ++j) {
+        const T tj = fb.tau[4 * f + j];
+        if (tj == T(0)) continue;
+        const T* v = s_v + j * n4;
+        for (int a = tid; a < n4; a += blockDim.x) {
+            T sacc = 0;
+            for (int c = j; c < n4; ++c) sacc += Y[a * ld + c] * v[c];
+            s_p[a] = sacc;
+        }
+        __syncthreads();
+        if (tid < 64) {
+            T sacc = 0;
+            for (int a = tid; a < n4; a += 64) sacc += v[a] * s_p[a];
+            sacc = wave_sum(sacc);
+            if (tid == 0) s_sc[0] = sacc;
+        }
+        __syncthreads();
+        const T K = tj * tj * s_sc[0] / T(2);
+        for (int a = tid; a < n4; a += blockDim.x) s_w[a] = tj * s_p[a] - K * v[a];
+        __syncthreads();
+        for (int e = tid; e < n4 * n4; e += blockDim.x) {
+            int a = e / n4, c = e % n4;
+            Y[a * ld + c] -= v[a] * s_w[c] + s_w[a] * v[c];
+        }
+        __syncthreads();
+    }
+    // 3. S = Y[3:,3:] + s2 I ; LDL^T with the residual as an extra column
+    const int k = n4 - 3;
+    T* S = Y + 3 * ld + 3;
+    T* r = s_r + 3;
+    for (int a = tid; a < k; a += blockDim.x) S[a * ld + a] += prm.sigma2;
+    __syncthreads();
+    T gam = 0;
+    bool fail = false;
+    for (int j = 0; j < k; ++j) {
+        const T d = S[j * ld + j];
+        if (!(d > 0)) { fail = true; break; }   // uniform: every thread reads the same d
+        const T inv = T(1) / d;
+        const T rj = r[j];
+        if (tid == 0) gam += rj * rj * inv;
+        const int m = k - j - 1;
+        for (int e = tid; e < m * m; e += blockDim.x) {
+            const int i = j + 1 + e / m, l = j + 1 + e % m;
+            if (l <= i) S[i * ld + l] -= (S[i * ld + j] * inv) * S[l * ld + j];
+        }
+        for (int i = j + 1 + tid; i < k; i += blockDim.x) r[i] -= (S[i * ld + j] * inv) * rj;
+        __syncthreads();
+    }
+    if (tid == 0) {
+        if (fail) gam = T(INFINITY);
+        fb.gamma[f] = gam;
+        fb.accept[f] = (gam < fb.chi2[f]) ? 1 : 0;
+    }
+}
+
 // ===========================================================================
 // Stacking in feature order with the row cap (msckf.py:671-679): one thread
 // per filter walks its features; decides the compression (msckf.py:549).
@@ -955,103 +1074,182 @@ __global__ void k_select(DevState<T> st, FeatBatch<T> fb, UpdWs<T> ws, int row_c
 
 // ===========================================================================
 // Stacked-H assembly / QR compression (msckf.py:549-556): one workgroup per
-// filter.  Rows of each included feature are materialised densely over the
-// C cam columns + the residual column in LDS, CHUNK rows at a time, then
-// either copied out (R <= C: no compression, as the reference) or merged into
-// the running triangular factor [R | Q^T r] with one Householder reflector
-// per column (a sequential TSQR; any orthogonal row transform of (H, r)
-// leaves the update unchanged -- quirk Q4).
-// ===========================================================================
-template <typename T> struct CompressCfg;
-template <> struct CompressCfg<float> { static constexpr int CHUNK = 32; };
-template <> struct CompressCfg<double> { static constexpr int CHUNK = 16; };
-
-template <typename T>
-__global__ void __launch_bounds__(256) k_compress(DevState<T> st, FeatBatch<T> fb, UpdWs<T> ws) {
-    constexpr int CH = CompressCfg<T>::CHUNK;
-    // one 16-B aligned dynamic LDS region (Guideline 17): [CH][C+1] chunk, then
-    // the reflector vector, the feature's cam slots and scalars
+// filter.  When R > C the included features' rows are merged, chunk by chunk,
+// into the running triangular factor [R | Q^T r] with one Householder
+// reflector per column (a sequential TSQR; any orthogonal row transform of
+// (H, r) leaves the update unchanged -- quirk Q4); when R <= C the stacked rows
+// are copied out as H_thin, as the reference does.
+// Register-resident merge (the production path of the QR compression).
+// Thread t owns columns j = t + 256u (u < COLS) of [R | Q^T r]; the CH rows of
+// the current chunk of the feature's projected block live in its registers
+// (b[u][0..CH)), generated directly from the compact factors (Hx, V, tau, W)
+// without an LDS tile.  Per column c one barrier: every owner of a column
+// j > c applies the reflector (v broadcast from LDS), and the owner of column
+// c+1 forms the next reflector from its registers (look-ahead).  R lives in
+// LDS when it fits, else in global memory with R[c+1][j] prefetched one step
+// ahead (row c+1 is not touched by step c).
+template <typename T, int CH, int COLS, bool R_LDS>
+__global__ void __launch_bounds__(256) k_compress_reg(DevState<T> st, FeatBatch<T> fb, UpdWs<T> ws) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    const int C = 6 * st.ncams[blockIdx.x];
-    const int ldb = C + 1;
-    T* Bk = reinterpret_cast<T*>(smem_raw);
-    T* s_v = Bk + (size_t)CH * ((ws.Cmax + 2) & ~1);
-    T* s_sc = s_v + CH;                  // [0] tau of the column reflector, [1..3] tau_f
-    int* s_slot = reinterpret_cast<int*>(s_sc + 4);
     const int b = blockIdx.x;
     const int tid = threadIdx.x;
     const int* info = ws.info + 4 * b;
-    const int R = info[0], n = info[1], compress = info[2];
-    if (R == 0) return;
+    const int Rn = info[0], n = info[1], compress = info[2];
+    if (Rn == 0) return;
+    const int C = 6 * st.ncams[b];
     const int ldh = ws.Cmax + 1;
-    T* H = ws.Hthin + (size_t)b * ws.Cmax * ldh;     // column Cmax holds r
-    for (int e = tid; e < n * ldh; e += blockDim.x) H[e] = 0;
-    __syncthreads();
+    T* H = ws.Hthin + (size_t)b * ws.Cmax * ldh;
+    const int ldr = R_LDS ? (C + 1) : ldh;
+    T* s_v = reinterpret_cast<T*>(smem_raw);                  // [2][CH]
+    T* s_sc = s_v + 2 * CH;                                   // tau[2] | tau_f[3]
+    T* s_V = s_sc + 8;                                        // [CH][4] chunk rows of V, [..][3] = Qr
+    int* s_obs = reinterpret_cast<int*>(s_V + 4 * CH);        // [Nmax] obs index of each cam slot
+    T* Rm = R_LDS ? reinterpret_cast<T*>(s_obs + ((st.Nmax + 3) & ~3)) : H;   // [C][ldr]
+    auto Ridx = [&](int r, int c) -> T& { return Rm[(size_t)r * ldr + (R_LDS ? c : (c == C ? ws.Cmax : c))]; };
+    if (compress)
+        for (int e = tid; e < C * (C + 1); e += blockDim.x) Ridx(e / (C + 1), e % (C + 1)) = 0;
+    else
+        for (int e = tid; e < n * ldh; e += blockDim.x) H[e] = 0;
     for (int f = fb.feat_off[b]; f < fb.feat_off[b + 1]; ++f) {
         if (!fb.include[f]) continue;
         const int o0 = fb.obs_off[f], M = fb.obs_off[f + 1] - o0;
         const T* wsf = fb.obs_ws + (size_t)o0 * OBS_WS;
+        __syncthreads();
+        for (int i = tid; i < st.Nmax; i += blockDim.x) s_obs[i] = -1;
+        if (tid < 3) s_sc[2 + tid] = fb.tau[4 * f + tid];
+        __syncthreads();
         int smin = 1 << 30;
         for (int i = 0; i < M; ++i) smin = min(smin, fb.obs_cam[o0 + i]);
+        for (int i = tid; i < M; i += blockDim.x) s_obs[fb.obs_cam[o0 + i]] = i;
         __syncthreads();
-        for (int i = tid; i < M; i += blockDim.x) s_slot[i] = fb.obs_cam[o0 + i];
-        if (tid < 3) s_sc[1 + tid] = fb.tau[4 * f + tid];
+        const T t0 = s_sc[2], t1 = s_sc[3], t2 = s_sc[4];
+        // per owned column: its observation (if any), its W entries, its Hx rows
+        int oi[COLS];
+        T w0[COLS], w1[COLS], w2[COLS], hx[COLS][4];
+#pragma unroll
+        for (int u = 0; u < COLS; ++u) {
+            const int j = tid + 256 * u;
+            oi[u] = (j < C) ? s_obs[j / 6] : -1;
+            w0[u] = w1[u] = w2[u] = 0;
+            hx[u][0] = hx[u][1] = hx[u][2] = hx[u][3] = 0;
+            if (oi[u] >= 0) {
+                const T* wo = wsf + (size_t)oi[u] * OBS_WS;
+                const int c = j % 6;
+                w0[u] = t0 * wo[OBS_W + c];
+                w1[u] = t1 * wo[OBS_W + 6 + c];
+                w2[u] = t2 * wo[OBS_W + 12 + c];
+#pragma unroll
+                for (int a = 0; a < 4; ++a) hx[u][a] = wo[OBS_HX + 6 * a + c];
+            }
+        }
         const int c0 = 6 * smin;
         const int n4 = 4 * M;
         for (int a0 = 3; a0 < n4; a0 += CH) {
             const int nr = min(CH, n4 - a0);
             __syncthreads();
-            for (int e = tid; e < CH * ldb; e += blockDim.x) Bk[e] = 0;
-            __syncthreads();
-            for (int e = tid; e < nr * M * 6; e += blockDim.x) {
-                int rr = e / (M * 6), q = e % (M * 6), i = q / 6, c = q % 6;
-                int row = a0 + rr;
-                Bk[rr * ldb + 6 * s_slot[i] + c] =
-                    qthx_entry(wsf + (size_t)(row >> 2) * OBS_WS, wsf + (size_t)i * OBS_WS, s_sc + 1, row, i, c);
+            for (int rr = tid; rr < CH; rr += blockDim.x) {
+                const int row = a0 + rr;
+                if (rr < nr) {
+                    const T* wr = wsf + (size_t)(row >> 2) * OBS_WS;
+                    s_V[4 * rr + 0] = wr[OBS_V + 3 * (row & 3) + 0];
+                    s_V[4 * rr + 1] = wr[OBS_V + 3 * (row & 3) + 1];
+                    s_V[4 * rr + 2] = wr[OBS_V + 3 * (row & 3) + 2];
+                    s_V[4 * rr + 3] = wr[OBS_QR + (row & 3)];
+                } else {
+                    s_V[4 * rr + 0] = s_V[4 * rr + 1] = s_V[4 * rr + 2] = s_V[4 * rr + 3] = 0;
+                }
             }
-            for (int rr = tid; rr < nr; rr += blockDim.x) {
-                int row = a0 + rr;
-                Bk[rr * ldb + C] = wsf[(size_t)(row >> 2) * OBS_WS + OBS_QR + (row & 3)];
-            }
             __syncthreads();
+            T bv[COLS][CH];
+#pragma unroll
+            for (int u = 0; u < COLS; ++u) {
+                const int j = tid + 256 * u;
+#pragma unroll
+                for (int rr = 0; rr < CH; ++rr) {
+                    const int row = a0 + rr;
+                    T x = 0;
+                    if (j == C) {
+                        x = s_V[4 * rr + 3];
+                    } else if (oi[u] >= 0) {
+                        const T h = ((row >> 2) == oi[u]) ? hx[u][row & 3] : T(0);
+                        x = h - (s_V[4 * rr] * w0[u] + s_V[4 * rr + 1] * w1[u] + s_V[4 * rr + 2] * w2[u]);
+                        if (rr >= nr) x = 0;
+                    }
+                    bv[u][rr] = x;
+                }
+            }
             if (!compress) {   // R <= C: the stacked rows are H_thin (msckf.py:554-556)
                 const int base = fb.row_off[f] + (a0 - 3);
-                for (int e = tid; e < nr * ldb; e += blockDim.x) {
-                    int rr = e / ldb, c = e % ldb;
-                    H[(size_t)(base + rr) * ldh + (c == C ? ws.Cmax : c)] = Bk[e];
+#pragma unroll
+                for (int u = 0; u < COLS; ++u) {
+                    const int j = tid + 256 * u;
+                    if (j > C) continue;
+                    const int col = (j == C) ? ws.Cmax : j;
+#pragma unroll
+                    for (int rr = 0; rr < CH; ++rr)
+                        if (rr < nr) H[(size_t)(base + rr) * ldh + col] = bv[u][rr];
                 }
                 continue;
             }
-            // merge the chunk into [R | Q^T r], one reflector per column
-            for (int c = c0; c < C; ++c) {
-                if (tid < 64) {
-                    T xv = tid < nr ? Bk[tid * ldb + c] : T(0);
-                    T xs = wave_sum(xv * xv);
-                    T alpha = H[(size_t)c * ldh + c];
-                    T tj = 0, scale = 0, beta = alpha;
-                    if (xs != T(0)) {
-                        T nrm = sqrt(alpha * alpha + xs);
-                        beta = alpha >= 0 ? -nrm : nrm;
-                        tj = (beta - alpha) / beta;
-                        scale = T(1) / (alpha - beta);
-                    }
-                    if (tid < nr) s_v[tid] = xv * scale;
-                    if (tid == 0) { s_sc[0] = tj; H[(size_t)c * ldh + c] = beta; }
+            // reflector of column c from (R[c][c], bv[u]) by the owner of column c
+            auto reflector = [&](int c, int u, int buf) {
+                T xs = 0;
+#pragma unroll
+                for (int rr = 0; rr < CH; ++rr) xs += bv[u][rr] * bv[u][rr];
+                T alpha = Ridx(c, c);
+                T tj = 0, scale = 0, beta = alpha;
+                if (xs != T(0)) {
+                    T nrm = sqrt(alpha * alpha + xs);
+                    beta = alpha >= 0 ? -nrm : nrm;
+                    tj = (beta - alpha) / beta;
+                    scale = T(1) / (alpha - beta);
                 }
-                __syncthreads();
-                const T tj = s_sc[0];
-                if (tj != T(0)) {
-                    for (int j = c + 1 + tid; j <= C; j += blockDim.x) {
-                        T* hj = H + (size_t)c * ldh + (j == C ? ws.Cmax : j);
-                        T w = *hj;
-                        for (int rr = 0; rr < nr; ++rr) w += s_v[rr] * Bk[rr * ldb + j];
-                        T tw = tj * w;
-                        *hj -= tw;
-                        for (int rr = 0; rr < nr; ++rr) Bk[rr * ldb + j] -= s_v[rr] * tw;
+#pragma unroll
+                for (int rr = 0; rr < CH; ++rr) s_v[buf * CH + rr] = bv[u][rr] * scale;
+                s_sc[buf] = tj;
+                Ridx(c, c) = beta;
+            };
+#pragma unroll
+            for (int u = 0; u < COLS; ++u)
+                if (tid + 256 * u == c0) reflector(c0, u, 0);
+            T rnext[COLS];
+#pragma unroll
+            for (int u = 0; u < COLS; ++u) {
+                const int j = tid + 256 * u;
+                rnext[u] = (j <= C && j > c0) ? Ridx(c0, j) : T(0);
+            }
+            __syncthreads();
+            for (int c = c0; c < C; ++c) {
+                const int buf = (c - c0) & 1;
+                const T tj = s_sc[buf];
+                T v[CH];
+#pragma unroll
+                for (int rr = 0; rr < CH; ++rr) v[rr] = s_v[buf * CH + rr];
+#pragma unroll
+                for (int u = 0; u < COLS; ++u) {
+                    const int j = tid + 256 * u;
+                    const T rcur = rnext[u];
+                    if (j > c + 1 && j <= C) rnext[u] = Ridx(c + 1, j);   // prefetch next row
+                    if (j > c && j <= C && tj != T(0)) {
+                        T w = rcur;
+#pragma unroll
+                        for (int rr = 0; rr < CH; ++rr) w += v[rr] * bv[u][rr];
+                        const T tw = tj * w;
+                        Ridx(c, j) = rcur - tw;
+#pragma unroll
+                        for (int rr = 0; rr < CH; ++rr) bv[u][rr] -= v[rr] * tw;
                     }
+                    if (j == c + 1 && j < C) reflector(j, u, buf ^ 1);
                 }
                 __syncthreads();
             }
+        }
+    }
+    if (R_LDS && compress) {
+        __syncthreads();
+        for (int e = tid; e < C * (C + 1); e += blockDim.x) {
+            const int r = e / (C + 1), c = e % (C + 1);
+            H[(size_t)r * ldh + (c == C ? ws.Cmax : c)] = Rm[e];
         }
     }
 }
@@ -1307,8 +1505,27 @@ void launch_feature(hipStream_t s, const DevState<T>& st, const Params<T>& prm, 
     hipLaunchKernelGGL(k_feature<T>, dim3((fb.nf + 3) / 4), dim3(256), 0, s, st, prm, fb, 0, fb.nf);
 }
 template <typename T>
-void launch_gate(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const FeatBatch<T>& fb) {
+size_t gate_lds_bytes(int maxM) {
+    const size_t n4 = 4 * maxM;
+    return ((n4 * (n4 + 1) + 1) & ~(size_t)1) * sizeof(T) + (6 * n4 + 3 * n4 + 3 * n4 + 4) * sizeof(T) +
+           (maxM + 4) * sizeof(int);
+}
+
+template <typename T>
+void launch_gate(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const FeatBatch<T>& fb, int maxM) {
     if (fb.nf == 0) return;
+    size_t lds = gate_lds_bytes<T>(maxM);
+    if (lds <= 160 * 1024) {
+        static bool attr_set[2] = {false, false};
+        bool& done = attr_set[sizeof(T) == 8];
+        if (!done) {
+            (void)hipFuncSetAttribute((const void*)k_gate_lds<T>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      160 * 1024);
+            done = true;
+        }
+        hipLaunchKernelGGL(k_gate_lds<T>, dim3(fb.nf), dim3(256), lds, s, st, prm, fb, 0);
+        return;
+    }
     hipLaunchKernelGGL(k_gate<T>, dim3(fb.nf), dim3(256), 0, s, st, prm, fb, 0);
 }
 template <typename T>
@@ -1316,12 +1533,36 @@ void launch_select(hipStream_t s, const DevState<T>& st, const FeatBatch<T>& fb,
                    int row_cap) {
     hipLaunchKernelGGL(k_select<T>, dim3((st.B + 63) / 64), dim3(64), 0, s, st, fb, ws, row_cap);
 }
+template <typename T> struct RegCfg;
+template <> struct RegCfg<float> { static constexpr int CH = 64; };
+template <> struct RegCfg<double> { static constexpr int CH = 32; };
+
+static int g_compress_mode = -1;   // -1 auto, 0 global R, 1 LDS R (MSCKF_COMPRESS_R env)
+
+template <typename T, int COLS>
+void launch_compress_reg(hipStream_t s, const DevState<T>& st, const FeatBatch<T>& fb, const UpdWs<T>& ws) {
+    constexpr int CH = RegCfg<T>::CH;
+    const size_t base = (2 * CH + 8 + 4 * CH) * sizeof(T) + ((st.Nmax + 3) & ~3) * sizeof(int);
+    const size_t rl = base + (size_t)ws.Cmax * (ws.Cmax + 1) * sizeof(T);
+    if (g_compress_mode < 0) {
+        const char* e = getenv("MSCKF_COMPRESS_R");
+        g_compress_mode = e ? atoi(e) : 0;
+    }
+    if (g_compress_mode == 1 && rl <= 160 * 1024) {
+        (void)hipFuncSetAttribute((const void*)k_compress_reg<T, CH, COLS, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipLaunchKernelGGL((k_compress_reg<T, CH, COLS, true>), dim3(st.B), dim3(256), rl, s, st, fb, ws);
+    } else {
+        hipLaunchKernelGGL((k_compress_reg<T, CH, COLS, false>), dim3(st.B), dim3(256), base, s, st, fb, ws);
+    }
+}
+
 template <typename T>
 void launch_compress(hipStream_t s, const DevState<T>& st, const FeatBatch<T>& fb, const UpdWs<T>& ws) {
-    const int CH = CompressCfg<T>::CHUNK;
-    size_t lds = ((size_t)CH * ((ws.Cmax + 2) & ~1) + CH + 4) * sizeof(T) + 128 * sizeof(int);
-    hipLaunchKernelGGL(k_compress<T>, dim3(st.B), dim3(256), lds, s, st, fb, ws);
+    if (ws.Cmax + 1 <= 256) launch_compress_reg<T, 1>(s, st, fb, ws);
+    else launch_compress_reg<T, 2>(s, st, fb, ws);
 }
+
 template <typename T>
 void launch_kalman(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const UpdWs<T>& ws,
                    KernelTimer* kt) {
@@ -1355,7 +1596,7 @@ void launch_kalman(hipStream_t s, const DevState<T>& st, const Params<T>& prm, c
     template void launch_prune<T>(hipStream_t, const DevState<T>&, int, const int*, int, T*, const int*, int); \
     template void launch_triangulate<T>(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&); \
     template void launch_feature<T>(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&); \
-    template void launch_gate<T>(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&); \
+    template void launch_gate<T>(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&, int); \
     template void launch_select<T>(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const UpdWs<T>&, int); \
     template void launch_compress<T>(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const UpdWs<T>&); \
     template void launch_kalman<T>(hipStream_t, const DevState<T>&, const Params<T>&, const UpdWs<T>&, KernelTimer*);

@@ -71,7 +71,7 @@ void launch_triangulate(hipStream_t, const DevState<T>&, const Params<T>&, const
 template <typename T>
 void launch_feature(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&);
 template <typename T>
-void launch_gate(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&);
+void launch_gate(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&, int maxM);
 template <typename T>
 void launch_select(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const UpdWs<T>&, int row_cap);
 template <typename T>
