@@ -1007,9 +1007,9 @@ __global__ void __launch_bounds__(256) k_gate_lds(DevState<T> st, Params<T> prm,
         const T K = tj * tj * s_sc[0] / T(2);
         for (int a = tid; a < n4; a += blockDim.x) s_w[a] = tj * s_p[a] - K * v[a];
         __syncthreads();
-        for (int e = tid; e < n4 * n4; e += blockDim.x) {
-            int a = e / n4, c = e % n4;
-            Y[a * ld + c] -= v[a] * s_w[c] + s_w[a] * v[c];
+        for (int a = (tid >> 4); a < n4; a += 16) {
+            const T va = v[a], wa = s_w[a];
+            for (int c = (tid & 15); c < n4; c += 16) Y[a * ld + c] -= va * s_w[c] + wa * v[c];
         }
         __syncthreads();
     }
@@ -1027,12 +1027,12 @@ __global__ void __launch_bounds__(256) k_gate_lds(DevState<T> st, Params<T> prm,
         const T inv = T(1) / d;
         const T rj = r[j];
         if (tid == 0) gam += rj * rj * inv;
-        const int m = k - j - 1;
-        for (int e = tid; e < m * m; e += blockDim.x) {
-            const int i = j + 1 + e / m, l = j + 1 + e % m;
-            if (l <= i) S[i * ld + l] -= (S[i * ld + j] * inv) * S[l * ld + j];
+        // 16 x 16 thread grid over the trailing lower triangle (no divisions)
+        for (int i = j + 1 + (tid >> 4); i < k; i += 16) {
+            const T ai = S[i * ld + j] * inv;
+            for (int l = j + 1 + (tid & 15); l <= i; l += 16) S[i * ld + l] -= ai * S[l * ld + j];
+            if ((tid & 15) == 0) r[i] -= ai * rj;
         }
-        for (int i = j + 1 + tid; i < k; i += blockDim.x) r[i] -= (S[i * ld + j] * inv) * rj;
         __syncthreads();
     }
     if (tid == 0) {
@@ -1191,12 +1191,26 @@ __global__ void __launch_bounds__(256) k_compress_reg(DevState<T> st, FeatBatch<
                 }
                 continue;
             }
+            // R[j][j] of every owned column: only column j's own reflector touches
+            // it, so it is read once per chunk (no global latency per column)
+            T rdiag[COLS];
+#pragma unroll
+            for (int u = 0; u < COLS; ++u) {
+                const int j = tid + 256 * u;
+                rdiag[u] = (j >= c0 && j < C) ? Ridx(j, j) : T(0);
+            }
             // reflector of column c from (R[c][c], bv[u]) by the owner of column c
             auto reflector = [&](int c, int u, int buf) {
-                T xs = 0;
+                T p0 = 0, p1 = 0, p2 = 0, p3 = 0;
 #pragma unroll
-                for (int rr = 0; rr < CH; ++rr) xs += bv[u][rr] * bv[u][rr];
-                T alpha = Ridx(c, c);
+                for (int rr = 0; rr < CH; rr += 4) {
+                    p0 += bv[u][rr] * bv[u][rr];
+                    p1 += bv[u][rr + 1] * bv[u][rr + 1];
+                    p2 += bv[u][rr + 2] * bv[u][rr + 2];
+                    p3 += bv[u][rr + 3] * bv[u][rr + 3];
+                }
+                const T xs = (p0 + p1) + (p2 + p3);
+                const T alpha = rdiag[u];
                 T tj = 0, scale = 0, beta = alpha;
                 if (xs != T(0)) {
                     T nrm = sqrt(alpha * alpha + xs);
@@ -1207,6 +1221,7 @@ __global__ void __launch_bounds__(256) k_compress_reg(DevState<T> st, FeatBatch<
 #pragma unroll
                 for (int rr = 0; rr < CH; ++rr) s_v[buf * CH + rr] = bv[u][rr] * scale;
                 s_sc[buf] = tj;
+                rdiag[u] = beta;
                 Ridx(c, c) = beta;
             };
 #pragma unroll
@@ -1231,9 +1246,15 @@ __global__ void __launch_bounds__(256) k_compress_reg(DevState<T> st, FeatBatch<
                     const T rcur = rnext[u];
                     if (j > c + 1 && j <= C) rnext[u] = Ridx(c + 1, j);   // prefetch next row
                     if (j > c && j <= C && tj != T(0)) {
-                        T w = rcur;
+                        T q0 = rcur, q1 = 0, q2 = 0, q3 = 0;
 #pragma unroll
-                        for (int rr = 0; rr < CH; ++rr) w += v[rr] * bv[u][rr];
+                        for (int rr = 0; rr < CH; rr += 4) {
+                            q0 += v[rr] * bv[u][rr];
+                            q1 += v[rr + 1] * bv[u][rr + 1];
+                            q2 += v[rr + 2] * bv[u][rr + 2];
+                            q3 += v[rr + 3] * bv[u][rr + 3];
+                        }
+                        const T w = (q0 + q1) + (q2 + q3);
                         const T tw = tj * w;
                         Ridx(c, j) = rcur - tw;
 #pragma unroll
@@ -1533,15 +1554,11 @@ void launch_select(hipStream_t s, const DevState<T>& st, const FeatBatch<T>& fb,
                    int row_cap) {
     hipLaunchKernelGGL(k_select<T>, dim3((st.B + 63) / 64), dim3(64), 0, s, st, fb, ws, row_cap);
 }
-template <typename T> struct RegCfg;
-template <> struct RegCfg<float> { static constexpr int CH = 64; };
-template <> struct RegCfg<double> { static constexpr int CH = 32; };
 
 static int g_compress_mode = -1;   // -1 auto, 0 global R, 1 LDS R (MSCKF_COMPRESS_R env)
 
-template <typename T, int COLS>
+template <typename T, int COLS, int CH>
 void launch_compress_reg(hipStream_t s, const DevState<T>& st, const FeatBatch<T>& fb, const UpdWs<T>& ws) {
-    constexpr int CH = RegCfg<T>::CH;
     const size_t base = (2 * CH + 8 + 4 * CH) * sizeof(T) + ((st.Nmax + 3) & ~3) * sizeof(int);
     const size_t rl = base + (size_t)ws.Cmax * (ws.Cmax + 1) * sizeof(T);
     if (g_compress_mode < 0) {
@@ -1557,10 +1574,21 @@ void launch_compress_reg(hipStream_t s, const DevState<T>& st, const FeatBatch<T
     }
 }
 
+static int g_compress_ch = -1;   // rows per register chunk (MSCKF_COMPRESS_CH env: 32 | 64)
+
 template <typename T>
 void launch_compress(hipStream_t s, const DevState<T>& st, const FeatBatch<T>& fb, const UpdWs<T>& ws) {
-    if (ws.Cmax + 1 <= 256) launch_compress_reg<T, 1>(s, st, fb, ws);
-    else launch_compress_reg<T, 2>(s, st, fb, ws);
+    if (g_compress_ch < 0) {
+        const char* e = getenv("MSCKF_COMPRESS_CH");
+        g_compress_ch = e ? atoi(e) : 32;
+    }
+    const bool wide = g_compress_ch >= 64 && sizeof(T) == 4;
+    if (ws.Cmax + 1 <= 256) {
+        if (wide) launch_compress_reg<T, 1, 64>(s, st, fb, ws);
+        else launch_compress_reg<T, 1, 32>(s, st, fb, ws);
+    } else {
+        launch_compress_reg<T, 2, 32>(s, st, fb, ws);
+    }
 }
 
 template <typename T>
