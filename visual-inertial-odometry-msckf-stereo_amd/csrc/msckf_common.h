@@ -176,6 +176,12 @@ __device__ __forceinline__ void mat3_mul(const T* A, const T* B, T* C) {
             C[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
 }
 
+// Workgroup barrier that orders LDS only: outstanding global loads / stores stay
+// in flight across it (a __syncthreads() emits s_waitcnt vmcnt(0) first, which
+// would drain every prefetch).  Use only where no global data written by
+// another thread is read after the barrier.
+#define LDS_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
+
 // ------------------------------------------------------ wave reductions --
 template <typename T>
 __device__ __forceinline__ T wave_sum(T x) {

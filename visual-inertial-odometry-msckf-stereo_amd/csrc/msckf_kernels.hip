@@ -1233,7 +1233,7 @@ __global__ void __launch_bounds__(256) k_compress_reg(DevState<T> st, FeatBatch<
                 const int j = tid + 256 * u;
                 rnext[u] = (j <= C && j > c0) ? Ridx(c0, j) : T(0);
             }
-            __syncthreads();
+            LDS_BARRIER();
             for (int c = c0; c < C; ++c) {
                 const int buf = (c - c0) & 1;
                 const T tj = s_sc[buf];
@@ -1262,7 +1262,7 @@ __global__ void __launch_bounds__(256) k_compress_reg(DevState<T> st, FeatBatch<
                     }
                     if (j == c + 1 && j < C) reflector(j, u, buf ^ 1);
                 }
-                __syncthreads();
+                LDS_BARRIER();   // R prefetches / stores stay in flight
             }
         }
     }
@@ -1271,6 +1271,206 @@ __global__ void __launch_bounds__(256) k_compress_reg(DevState<T> st, FeatBatch<
         for (int e = tid; e < C * (C + 1); e += blockDim.x) {
             const int r = e / (C + 1), c = e % (C + 1);
             H[(size_t)r * ldh + (c == C ? ws.Cmax : c)] = Rm[e];
+        }
+    }
+}
+
+// Panel-blocked register merge (production path when C+1 <= 256).
+// Columns are processed in 16-wide panels aligned to 16.  The wave that owns a
+// panel factors it alone (reflector of column q formed by lane q from its
+// registers, broadcast to the wave through LDS with a wave-local wait only);
+// its lanes apply each reflector to their own columns on the spot.  One
+// workgroup barrier per panel publishes the panel's 16 reflectors; every other
+// wave then applies them to its columns from registers.  The 16 R rows of a
+// panel are prefetched one whole panel ahead (rows of panel P+1 are not
+// touched by panel P), so no global latency sits on the per-column path.
+template <typename T, int CH>
+__global__ void __launch_bounds__(256) k_compress_panel(DevState<T> st, FeatBatch<T> fb, UpdWs<T> ws) {
+    constexpr int NB = 16;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x, wave = tid >> 6;
+    const int* info = ws.info + 4 * b;
+    const int Rn = info[0], n = info[1], compress = info[2];
+    if (Rn == 0) return;
+    const int C = 6 * st.ncams[b];
+    const int ldh = ws.Cmax + 1;
+    T* H = ws.Hthin + (size_t)b * ws.Cmax * ldh;
+    T* s_Vp = reinterpret_cast<T*>(smem_raw);       // [2][NB][CH] panel reflectors
+    T* s_tp = s_Vp + 2 * NB * CH;                   // [2][NB]
+    T* s_sc = s_tp + 2 * NB;                        // tau_f[3] (+pad)
+    T* s_V = s_sc + 4;                              // [CH][4] chunk rows of V | Qr
+    int* s_obs = reinterpret_cast<int*>(s_V + 4 * CH);
+    const int j = tid;                              // the one column this thread owns
+    const bool mine = j <= C;
+    const int hcol = (j == C) ? ws.Cmax : j;
+    if (compress)
+        for (int e = tid; e < C * (C + 1); e += blockDim.x) {
+            const int r = e / (C + 1), c = e % (C + 1);
+            H[(size_t)r * ldh + (c == C ? ws.Cmax : c)] = 0;
+        }
+    else
+        for (int e = tid; e < n * ldh; e += blockDim.x) H[e] = 0;
+    for (int f = fb.feat_off[b]; f < fb.feat_off[b + 1]; ++f) {
+        if (!fb.include[f]) continue;
+        const int o0 = fb.obs_off[f], M = fb.obs_off[f + 1] - o0;
+        const T* wsf = fb.obs_ws + (size_t)o0 * OBS_WS;
+        __syncthreads();
+        for (int i = tid; i < st.Nmax; i += blockDim.x) s_obs[i] = -1;
+        if (tid < 3) s_sc[tid] = fb.tau[4 * f + tid];
+        __syncthreads();
+        int smin = 1 << 30;
+        for (int i = 0; i < M; ++i) smin = min(smin, fb.obs_cam[o0 + i]);
+        for (int i = tid; i < M; i += blockDim.x) s_obs[fb.obs_cam[o0 + i]] = i;
+        __syncthreads();
+        const T t0 = s_sc[0], t1 = s_sc[1], t2 = s_sc[2];
+        const int oi = (j < C) ? s_obs[j / 6] : -1;
+        T w0 = 0, w1 = 0, w2 = 0, hx[4] = {0, 0, 0, 0};
+        if (oi >= 0) {
+            const T* wo = wsf + (size_t)oi * OBS_WS;
+            const int c = j % 6;
+            w0 = t0 * wo[OBS_W + c];
+            w1 = t1 * wo[OBS_W + 6 + c];
+            w2 = t2 * wo[OBS_W + 12 + c];
+#pragma unroll
+            for (int a = 0; a < 4; ++a) hx[a] = wo[OBS_HX + 6 * a + c];
+        }
+        const int c0 = 6 * smin;
+        const int n4 = 4 * M;
+        for (int a0 = 3; a0 < n4; a0 += CH) {
+            const int nr = min(CH, n4 - a0);
+            __syncthreads();
+            for (int rr = tid; rr < CH; rr += blockDim.x) {
+                const int row = a0 + rr;
+                if (rr < nr) {
+                    const T* wr = wsf + (size_t)(row >> 2) * OBS_WS;
+                    s_V[4 * rr + 0] = wr[OBS_V + 3 * (row & 3) + 0];
+                    s_V[4 * rr + 1] = wr[OBS_V + 3 * (row & 3) + 1];
+                    s_V[4 * rr + 2] = wr[OBS_V + 3 * (row & 3) + 2];
+                    s_V[4 * rr + 3] = wr[OBS_QR + (row & 3)];
+                } else {
+                    s_V[4 * rr + 0] = s_V[4 * rr + 1] = s_V[4 * rr + 2] = s_V[4 * rr + 3] = 0;
+                }
+            }
+            __syncthreads();
+            T bv[CH];
+#pragma unroll
+            for (int rr = 0; rr < CH; ++rr) {
+                const int row = a0 + rr;
+                T x = 0;
+                if (j == C) {
+                    x = s_V[4 * rr + 3];
+                } else if (oi >= 0) {
+                    const T h = ((row >> 2) == oi) ? hx[row & 3] : T(0);
+                    x = h - (s_V[4 * rr] * w0 + s_V[4 * rr + 1] * w1 + s_V[4 * rr + 2] * w2);
+                    if (rr >= nr) x = 0;
+                }
+                bv[rr] = x;
+            }
+            if (!compress) {   // R <= C: the stacked rows are H_thin (msckf.py:554-556)
+                const int base = fb.row_off[f] + (a0 - 3);
+                if (mine)
+#pragma unroll
+                    for (int rr = 0; rr < CH; ++rr)
+                        if (rr < nr) H[(size_t)(base + rr) * ldh + hcol] = bv[rr];
+                continue;
+            }
+            const int P0 = c0 / NB, PL = (C - 1) / NB;
+            T rr_[NB], rn[NB];
+            {
+                const int pb = c0, pe = min(NB * (P0 + 1), C);
+#pragma unroll
+                for (int t = 0; t < NB; ++t)
+                    rn[t] = (mine && pb + t < pe && j >= pb + t) ? H[(size_t)(pb + t) * ldh + hcol] : T(0);
+            }
+            for (int P = P0; P <= PL; ++P) {
+                const int pb = max(NB * P, c0), pe = min(NB * (P + 1), C), nbp = pe - pb;
+                const int buf = (P - P0) & 1;
+                T* Vb = s_Vp + buf * NB * CH;
+                T* tb = s_tp + buf * NB;
+#pragma unroll
+                for (int t = 0; t < NB; ++t) rr_[t] = rn[t];
+                if (P < PL) {   // prefetch the next panel's R rows (untouched by this panel)
+                    const int qb = NB * (P + 1), qe = min(NB * (P + 2), C);
+#pragma unroll
+                    for (int t = 0; t < NB; ++t)
+                        rn[t] = (mine && qb + t < qe && j >= qb + t) ? H[(size_t)(qb + t) * ldh + hcol] : T(0);
+                }
+                const int owner = (NB * P) >> 6;
+                if (wave == owner) {
+#pragma unroll
+                    for (int t = 0; t < NB; ++t) {
+                        if (t < nbp) {
+                            const int q = pb + t;
+                            if (j == q) {   // reflector of column q (LAPACK dlarfg convention)
+                                T p0 = 0, p1 = 0, p2 = 0, p3 = 0;
+#pragma unroll
+                                for (int r = 0; r < CH; r += 4) {
+                                    p0 += bv[r] * bv[r];
+                                    p1 += bv[r + 1] * bv[r + 1];
+                                    p2 += bv[r + 2] * bv[r + 2];
+                                    p3 += bv[r + 3] * bv[r + 3];
+                                }
+                                const T xs = (p0 + p1) + (p2 + p3);
+                                const T alpha = rr_[t];
+                                T tj = 0, scale = 0, beta = alpha;
+                                if (xs != T(0)) {
+                                    T nrm = sqrt(alpha * alpha + xs);
+                                    beta = alpha >= 0 ? -nrm : nrm;
+                                    tj = (beta - alpha) / beta;
+                                    scale = T(1) / (alpha - beta);
+                                }
+#pragma unroll
+                                for (int r = 0; r < CH; ++r) Vb[t * CH + r] = bv[r] * scale;
+                                tb[t] = tj;
+                                rr_[t] = beta;
+                            }
+                            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // wave-local publish
+                            const T tj = tb[t];
+                            if (j > q && mine && tj != T(0)) {
+                                T q0 = rr_[t], q1 = 0, q2 = 0, q3 = 0;
+#pragma unroll
+                                for (int r = 0; r < CH; r += 4) {
+                                    q0 += Vb[t * CH + r] * bv[r];
+                                    q1 += Vb[t * CH + r + 1] * bv[r + 1];
+                                    q2 += Vb[t * CH + r + 2] * bv[r + 2];
+                                    q3 += Vb[t * CH + r + 3] * bv[r + 3];
+                                }
+                                const T tw = tj * ((q0 + q1) + (q2 + q3));
+                                rr_[t] -= tw;
+#pragma unroll
+                                for (int r = 0; r < CH; ++r) bv[r] -= Vb[t * CH + r] * tw;
+                            }
+                        }
+                    }
+                }
+                LDS_BARRIER();   // publishes the panel; R prefetches stay in flight
+                if (wave != owner && mine && j >= pe) {
+#pragma unroll
+                    for (int t = 0; t < NB; ++t) {
+                        if (t < nbp) {
+                            const T tj = tb[t];
+                            if (tj != T(0)) {
+                                T q0 = rr_[t], q1 = 0, q2 = 0, q3 = 0;
+#pragma unroll
+                                for (int r = 0; r < CH; r += 4) {
+                                    q0 += Vb[t * CH + r] * bv[r];
+                                    q1 += Vb[t * CH + r + 1] * bv[r + 1];
+                                    q2 += Vb[t * CH + r + 2] * bv[r + 2];
+                                    q3 += Vb[t * CH + r + 3] * bv[r + 3];
+                                }
+                                const T tw = tj * ((q0 + q1) + (q2 + q3));
+                                rr_[t] -= tw;
+#pragma unroll
+                                for (int r = 0; r < CH; ++r) bv[r] -= Vb[t * CH + r] * tw;
+                            }
+                        }
+                    }
+                }
+#pragma unroll
+                for (int t = 0; t < NB; ++t)
+                    if (mine && t < nbp && j >= pb + t) H[(size_t)(pb + t) * ldh + hcol] = rr_[t];
+            }
         }
     }
 }
@@ -1583,6 +1783,14 @@ void launch_compress(hipStream_t s, const DevState<T>& st, const FeatBatch<T>& f
         g_compress_ch = e ? atoi(e) : 32;
     }
     const bool wide = g_compress_ch >= 64 && sizeof(T) == 4;
+    const char* pe = getenv("MSCKF_COMPRESS_PANEL");
+    const bool panel = pe ? atoi(pe) != 0 : true;
+    if (panel && ws.Cmax + 1 <= 256) {
+        constexpr int CHP = 32;
+        const size_t lds = (2 * 16 * CHP + 2 * 16 + 4 + 4 * CHP) * sizeof(T) + ((st.Nmax + 3) & ~3) * sizeof(int);
+        hipLaunchKernelGGL((k_compress_panel<T, CHP>), dim3(st.B), dim3(256), lds, s, st, fb, ws);
+        return;
+    }
     if (ws.Cmax + 1 <= 256) {
         if (wide) launch_compress_reg<T, 1, 64>(s, st, fb, ws);
         else launch_compress_reg<T, 1, 32>(s, st, fb, ws);
