@@ -182,6 +182,18 @@ __device__ __forceinline__ void mat3_mul(const T* A, const T* B, T* C) {
 // another thread is read after the barrier.
 #define LDS_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
 
+// Broadcast lane `src` (wave-uniform) of x to the whole wave via v_readlane
+// (result lands in an SGPR: no LDS traffic).
+__device__ __forceinline__ float lane_bcast(float x, int src) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), src));
+}
+__device__ __forceinline__ double lane_bcast(double x, int src) {
+    long long u = __builtin_bit_cast(long long, x);
+    int lo = __builtin_amdgcn_readlane((int)(u & 0xffffffffLL), src);
+    int hi = __builtin_amdgcn_readlane((int)(u >> 32), src);
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
+}
+
 // ------------------------------------------------------ wave reductions --
 template <typename T>
 __device__ __forceinline__ T wave_sum(T x) {

@@ -1475,6 +1475,184 @@ __global__ void __launch_bounds__(256) k_compress_panel(DevState<T> st, FeatBatc
     }
 }
 
+// One wavefront per filter (the throughput path): no workgroup barriers at
+// all.  Lane l owns columns j = l + 64u (u < COLS) of [R | Q^T r] and the CH
+// chunk rows of those columns in registers.  Column c's reflector vector is
+// read out of the owner lane with v_readlane (SGPR broadcast); every lane
+// forms the same scalars (tau, scale) redundantly and updates its own
+// columns.  Latency is hidden by running several filters per SIMD.
+template <typename T, int CH, int COLS>
+__global__ void __launch_bounds__(64) k_compress_wave(DevState<T> st, FeatBatch<T> fb, UpdWs<T> ws) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    const int b = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int* info = ws.info + 4 * b;
+    const int Rn = info[0], n = info[1], compress = info[2];
+    if (Rn == 0) return;
+    const int C = 6 * st.ncams[b];
+    const int ldh = ws.Cmax + 1;
+    T* H = ws.Hthin + (size_t)b * ws.Cmax * ldh;
+    T* s_V = reinterpret_cast<T*>(smem_raw);        // [CH][4] chunk rows of V | Qr
+    T* s_sc = s_V + 4 * CH;                         // tau_f[3] (+pad)
+    int* s_obs = reinterpret_cast<int*>(s_sc + 4);  // [Nmax]
+    int hcol[COLS];
+#pragma unroll
+    for (int u = 0; u < COLS; ++u) {
+        const int j = lane + 64 * u;
+        hcol[u] = (j == C) ? ws.Cmax : j;
+    }
+    if (compress) {
+        for (int r = 0; r < C; ++r)
+#pragma unroll
+            for (int u = 0; u < COLS; ++u)
+                if (lane + 64 * u <= C) H[(size_t)r * ldh + hcol[u]] = 0;
+    } else {
+        for (int e = lane; e < n * ldh; e += 64) H[e] = 0;
+    }
+    for (int f = fb.feat_off[b]; f < fb.feat_off[b + 1]; ++f) {
+        if (!fb.include[f]) continue;
+        const int o0 = fb.obs_off[f], M = fb.obs_off[f + 1] - o0;
+        const T* wsf = fb.obs_ws + (size_t)o0 * OBS_WS;
+        for (int i = lane; i < st.Nmax; i += 64) s_obs[i] = -1;
+        if (lane < 3) s_sc[lane] = fb.tau[4 * f + lane];
+        int smin = 1 << 30;
+        for (int i = 0; i < M; ++i) smin = min(smin, fb.obs_cam[o0 + i]);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        for (int i = lane; i < M; i += 64) s_obs[fb.obs_cam[o0 + i]] = i;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const T t0 = s_sc[0], t1 = s_sc[1], t2 = s_sc[2];
+        int oi[COLS];
+        T w0[COLS], w1[COLS], w2[COLS], hx[COLS][4];
+#pragma unroll
+        for (int u = 0; u < COLS; ++u) {
+            const int j = lane + 64 * u;
+            oi[u] = (j < C) ? s_obs[j / 6] : -1;
+            w0[u] = w1[u] = w2[u] = 0;
+            hx[u][0] = hx[u][1] = hx[u][2] = hx[u][3] = 0;
+            if (oi[u] >= 0) {
+                const T* wo = wsf + (size_t)oi[u] * OBS_WS;
+                const int c = j % 6;
+                w0[u] = t0 * wo[OBS_W + c];
+                w1[u] = t1 * wo[OBS_W + 6 + c];
+                w2[u] = t2 * wo[OBS_W + 12 + c];
+#pragma unroll
+                for (int a = 0; a < 4; ++a) hx[u][a] = wo[OBS_HX + 6 * a + c];
+            }
+        }
+        const int c0 = 6 * smin;
+        const int n4 = 4 * M;
+        for (int a0 = 3; a0 < n4; a0 += CH) {
+            const int nr = min(CH, n4 - a0);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            for (int rr = lane; rr < CH; rr += 64) {
+                const int row = a0 + rr;
+                if (rr < nr) {
+                    const T* wr = wsf + (size_t)(row >> 2) * OBS_WS;
+                    s_V[4 * rr + 0] = wr[OBS_V + 3 * (row & 3) + 0];
+                    s_V[4 * rr + 1] = wr[OBS_V + 3 * (row & 3) + 1];
+                    s_V[4 * rr + 2] = wr[OBS_V + 3 * (row & 3) + 2];
+                    s_V[4 * rr + 3] = wr[OBS_QR + (row & 3)];
+                } else {
+                    s_V[4 * rr + 0] = s_V[4 * rr + 1] = s_V[4 * rr + 2] = s_V[4 * rr + 3] = 0;
+                }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            T bv[COLS][CH];
+#pragma unroll
+            for (int u = 0; u < COLS; ++u) {
+                const int j = lane + 64 * u;
+#pragma unroll
+                for (int rr = 0; rr < CH; ++rr) {
+                    const int row = a0 + rr;
+                    T x = 0;
+                    if (j == C) {
+                        x = s_V[4 * rr + 3];
+                    } else if (oi[u] >= 0) {
+                        const T h = ((row >> 2) == oi[u]) ? hx[u][row & 3] : T(0);
+                        x = h - (s_V[4 * rr] * w0[u] + s_V[4 * rr + 1] * w1[u] + s_V[4 * rr + 2] * w2[u]);
+                        if (rr >= nr) x = 0;
+                    }
+                    bv[u][rr] = x;
+                }
+            }
+            if (!compress) {   // R <= C: the stacked rows are H_thin (msckf.py:554-556)
+                const int base = fb.row_off[f] + (a0 - 3);
+#pragma unroll
+                for (int u = 0; u < COLS; ++u)
+                    if (lane + 64 * u <= C)
+#pragma unroll
+                        for (int rr = 0; rr < CH; ++rr)
+                            if (rr < nr) H[(size_t)(base + rr) * ldh + hcol[u]] = bv[u][rr];
+                continue;
+            }
+            T rcur[COLS];
+#pragma unroll
+            for (int u = 0; u < COLS; ++u) {
+                const int j = lane + 64 * u;
+                rcur[u] = (j >= c0 && j <= C) ? H[(size_t)c0 * ldh + hcol[u]] : T(0);
+            }
+            // the sweep is split by the owner's column slot UC (compile time) so
+            // the broadcast reflector stays in SGPRs
+#pragma unroll
+            for (int UC = 0; UC < COLS; ++UC) {
+                const int cb = max(c0, 64 * UC), ce = min(C, 64 * (UC + 1));
+                for (int c = cb; c < ce; ++c) {
+                    const int lc = c & 63;
+                    T rnext[COLS];
+#pragma unroll
+                    for (int u = 0; u < COLS; ++u) {   // prefetch row c+1 (untouched by column c)
+                        const int j = lane + 64 * u;
+                        rnext[u] = (j > c && j <= C && c + 1 < C) ? H[(size_t)(c + 1) * ldh + hcol[u]] : T(0);
+                    }
+                    T v[CH];
+#pragma unroll
+                    for (int rr = 0; rr < CH; ++rr) v[rr] = lane_bcast(bv[UC][rr], lc);
+                    const T alpha = lane_bcast(rcur[UC], lc);
+                    T p0 = 0, p1 = 0, p2 = 0, p3 = 0;
+#pragma unroll
+                    for (int rr = 0; rr < CH; rr += 4) {
+                        p0 += v[rr] * v[rr];
+                        p1 += v[rr + 1] * v[rr + 1];
+                        p2 += v[rr + 2] * v[rr + 2];
+                        p3 += v[rr + 3] * v[rr + 3];
+                    }
+                    const T xs = (p0 + p1) + (p2 + p3);
+                    T tj = 0, scale = 0, beta = alpha;
+                    if (xs != T(0)) {
+                        const T nrm = sqrt(alpha * alpha + xs);
+                        beta = alpha >= 0 ? -nrm : nrm;
+                        tj = (beta - alpha) / beta;
+                        scale = T(1) / (alpha - beta);
+                    }
+                    const T ts = tj * scale;   // w = R + scale <v_raw, b> ; b -= v_raw (scale tau w)
+#pragma unroll
+                    for (int u = UC; u < COLS; ++u) {
+                        const int j = lane + 64 * u;
+                        if (j == c) {
+                            H[(size_t)c * ldh + hcol[u]] = beta;
+                        } else if (j > c && j <= C && tj != T(0)) {
+                            T q0 = 0, q1 = 0, q2 = 0, q3 = 0;
+#pragma unroll
+                            for (int rr = 0; rr < CH; rr += 4) {
+                                q0 += v[rr] * bv[u][rr];
+                                q1 += v[rr + 1] * bv[u][rr + 1];
+                                q2 += v[rr + 2] * bv[u][rr + 2];
+                                q3 += v[rr + 3] * bv[u][rr + 3];
+                            }
+                            const T w = rcur[u] + scale * ((q0 + q1) + (q2 + q3));
+                            H[(size_t)c * ldh + hcol[u]] = rcur[u] - tj * w;
+                            const T f2 = ts * w;
+#pragma unroll
+                            for (int rr = 0; rr < CH; ++rr) bv[u][rr] -= v[rr] * f2;
+                        }
+                        rcur[u] = rnext[u];
+                    }
+                }
+            }
+        }
+    }
+}
+
 // ===========================================================================
 // Kalman update (msckf.py:559-604) on H_thin (n x C, IMU columns zero):
 //   HP = H_thin P[21:D, :]              k_hp      (n x D)
@@ -1783,9 +1961,21 @@ void launch_compress(hipStream_t s, const DevState<T>& st, const FeatBatch<T>& f
         g_compress_ch = e ? atoi(e) : 32;
     }
     const bool wide = g_compress_ch >= 64 && sizeof(T) == 4;
-    const char* pe = getenv("MSCKF_COMPRESS_PANEL");
-    const bool panel = pe ? atoi(pe) != 0 : true;
-    if (panel && ws.Cmax + 1 <= 256) {
+    const char* me = getenv("MSCKF_COMPRESS_MODE");   // wave (default) | panel | block
+    const int mode = me ? (me[0] == 'p' ? 1 : (me[0] == 'b' ? 2 : 0)) : 0;
+    if (mode == 0 && ws.Cmax + 1 <= 192) {
+        const size_t lds = (4 * 32 + 4) * sizeof(T) + ((st.Nmax + 3) & ~3) * sizeof(int);
+        if constexpr (sizeof(T) == 4) {
+            if (wide) {
+                hipLaunchKernelGGL((k_compress_wave<T, 64, 3>), dim3(st.B), dim3(64), lds + 4 * 32 * sizeof(T), s,
+                                   st, fb, ws);
+                return;
+            }
+        }
+        hipLaunchKernelGGL((k_compress_wave<T, 32, 3>), dim3(st.B), dim3(64), lds, s, st, fb, ws);
+        return;
+    }
+    if (mode <= 1 && ws.Cmax + 1 <= 256) {
         constexpr int CHP = 32;
         const size_t lds = (2 * 16 * CHP + 2 * 16 + 4 + 4 * CHP) * sizeof(T) + ((st.Nmax + 3) & ~3) * sizeof(int);
         hipLaunchKernelGGL((k_compress_panel<T, CHP>), dim3(st.B), dim3(256), lds, s, st, fb, ws);
