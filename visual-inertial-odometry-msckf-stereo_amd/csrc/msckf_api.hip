@@ -73,7 +73,8 @@ struct msckf_ctx {
     // feature batch
     int nf = 0, maxM = 0;
     std::vector<int> h_feat_off;
-    DBuf<int> feat_filter, feat_off, obs_off, obs_cam, row_off;
+    DBuf<int> feat_filter, feat_off, obs_off, obs_cam, row_off, gate_list;
+    GateClasses gc;
     DBuf<long long> ysq_off;
     DBuf<unsigned char> obs_z, chi2, p_w, obs_ws, tau, ysq, gamma;
     DBuf<uint8_t> valid, accept, include;
@@ -242,6 +243,35 @@ int load_features(msckf_ctx* c, int nf, const int32_t* feat_off, int single_filt
     HIPC(hipMemcpyAsync(c->obs_off.p, obs_off, (nf + 1) * sizeof(int), hipMemcpyHostToDevice, s));
     if (nobs) HIPC(hipMemcpyAsync(c->obs_cam.p, obs_cam, nobs * sizeof(int), hipMemcpyHostToDevice, s));
     HIPC(hipMemcpyAsync(c->ysq_off.p, ysq.data(), (nf + 1) * sizeof(long long), hipMemcpyHostToDevice, s));
+    {   // gating size classes, largest first inside the list (long blocks start early)
+        static const int lim[GateClasses::NC] = {8, 16, 24, 1 << 30};
+        std::vector<std::vector<int>> cls(GateClasses::NC);
+        GateClasses gc;
+        for (int f = 0; f < nf; ++f) {
+            const int M = obs_off[f + 1] - obs_off[f];
+            int k = 0;
+            while (M > lim[k]) ++k;
+            cls[k].push_back(f);
+            gc.maxM[k] = std::max(gc.maxM[k], M);
+        }
+        std::vector<int> flat;
+        for (int k = GateClasses::NC - 1; k >= 0; --k) {
+            gc.off[k] = 0;
+        }
+        int pos = 0;
+        for (int k = 0; k < GateClasses::NC; ++k) {
+            gc.off[k] = pos;
+            flat.insert(flat.end(), cls[k].begin(), cls[k].end());
+            pos += (int)cls[k].size();
+        }
+        gc.off[GateClasses::NC] = pos;
+        HIPC(c->gate_list.ensure(flat.size() + 1));
+        if (!flat.empty())
+            HIPC(hipMemcpyAsync(c->gate_list.p, flat.data(), flat.size() * sizeof(int), hipMemcpyHostToDevice, s));
+        gc.list = c->gate_list.p;
+        HIPC(hipStreamSynchronize(s));
+        c->gc = gc;
+    }
     HIPC(hipStreamSynchronize(s));
     HIPC(upload<T>(c, c->obs_z.p, obs_z, nobs * 4));
     if (chi2) {
@@ -279,7 +309,7 @@ int run_update_chain(msckf_ctx* c, int row_cap, bool triangulate) {
     launch_feature<T>(s, st, prm, fb);
     c->timer.end(s);
     c->timer.begin(s, "gate");
-    launch_gate<T>(s, st, prm, fb, c->maxM);
+    launch_gate<T>(s, st, prm, fb, c->gc);
     c->timer.end(s);
     c->timer.begin(s, "select");
     launch_select<T>(s, st, fb, ws, row_cap);
@@ -553,7 +583,7 @@ int msckf_destroy(msckf_ctx_t* c) {
                     &c->dx, &c->obs_z, &c->chi2, &c->p_w, &c->obs_ws, &c->tau, &c->ysq, &c->gamma, &c->scratch})
         b->release();
     for (auto* b : {&c->ncams, &c->ncams_snap, &c->info, &c->feat_filter, &c->feat_off, &c->obs_off, &c->obs_cam,
-                    &c->row_off, &c->iscratch})
+                    &c->row_off, &c->iscratch, &c->gate_list})
         b->release();
     c->ysq_off.release();
     c->valid.release();

@@ -809,8 +809,9 @@ __device__ __forceinline__ T qthx_entry(const T* ws_row_obs, const T* ws_col_obs
 // (Same value as the reference's rows-space S; ~10x fewer flops.)
 // ===========================================================================
 template <typename T>
-__global__ void __launch_bounds__(256) k_gate(DevState<T> st, Params<T> prm, FeatBatch<T> fb, int f0) {
-    const int f = f0 + blockIdx.x;
+__global__ void __launch_bounds__(256) k_gate(DevState<T> st, Params<T> prm, FeatBatch<T> fb,
+                                              const int* __restrict__ flist) {
+    const int f = flist[blockIdx.x];
     const int tid = threadIdx.x;
     if (!fb.valid[f]) {
         if (tid == 0) { fb.gamma[f] = T(NAN); fb.accept[f] = 0; }
@@ -928,9 +929,10 @@ __global__ void __launch_bounds__(256) k_gate(DevState<T> st, Params<T> prm, Fea
 // carried along as an extra column: gamma = sum_j r~_j^2 / d_j.  One barrier
 // per pivot; the column being eliminated is read-only during its step.
 template <typename T>
-__global__ void __launch_bounds__(256) k_gate_lds(DevState<T> st, Params<T> prm, FeatBatch<T> fb, int f0) {
+__global__ void __launch_bounds__(256) k_gate_lds(DevState<T> st, Params<T> prm, FeatBatch<T> fb,
+                                                  const int* __restrict__ flist) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    const int f = f0 + blockIdx.x;
+    const int f = flist[blockIdx.x];
     const int tid = threadIdx.x;
     if (!fb.valid[f]) {
         if (tid == 0) { fb.gamma[f] = T(NAN); fb.accept[f] = 0; }
@@ -1007,7 +1009,7 @@ __global__ void __launch_bounds__(256) k_gate_lds(DevState<T> st, Params<T> prm,
         const T K = tj * tj * s_sc[0] / T(2);
         for (int a = tid; a < n4; a += blockDim.x) s_w[a] = tj * s_p[a] - K * v[a];
         __syncthreads();
-        for (int a = (tid >> 4); a < n4; a += 16) {
+        for (int a = (tid >> 4); a < n4; a += (int)(blockDim.x >> 4)) {
             const T va = v[a], wa = s_w[a];
             for (int c = (tid & 15); c < n4; c += 16) Y[a * ld + c] -= va * s_w[c] + wa * v[c];
         }
@@ -1027,8 +1029,9 @@ __global__ void __launch_bounds__(256) k_gate_lds(DevState<T> st, Params<T> prm,
         const T inv = T(1) / d;
         const T rj = r[j];
         if (tid == 0) gam += rj * rj * inv;
-        // 16 x 16 thread grid over the trailing lower triangle (no divisions)
-        for (int i = j + 1 + (tid >> 4); i < k; i += 16) {
+        // (blockDim/16) x 16 thread grid over the trailing lower triangle (no divisions)
+        const int rstep = blockDim.x >> 4;
+        for (int i = j + 1 + (tid >> 4); i < k; i += rstep) {
             const T ai = S[i * ld + j] * inv;
             for (int l = j + 1 + (tid & 15); l <= i; l += 16) S[i * ld + l] -= ai * S[l * ld + j];
             if ((tid & 15) == 0) r[i] -= ai * rj;
@@ -1910,23 +1913,32 @@ size_t gate_lds_bytes(int maxM) {
            (maxM + 4) * sizeof(int);
 }
 
+// Features are launched in size classes (by M, listed on the host at load
+// time): each class gets a workgroup size and an LDS footprint that fit it, so
+// small features do not pay for the largest one.
 template <typename T>
-void launch_gate(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const FeatBatch<T>& fb, int maxM) {
+void launch_gate(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const FeatBatch<T>& fb,
+                 const GateClasses& gc) {
     if (fb.nf == 0) return;
-    size_t lds = gate_lds_bytes<T>(maxM);
-    if (lds <= 160 * 1024) {
-        static bool attr_set[2] = {false, false};
-        bool& done = attr_set[sizeof(T) == 8];
-        if (!done) {
-            (void)hipFuncSetAttribute((const void*)k_gate_lds<T>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      160 * 1024);
-            done = true;
-        }
-        hipLaunchKernelGGL(k_gate_lds<T>, dim3(fb.nf), dim3(256), lds, s, st, prm, fb, 0);
-        return;
+    static bool attr_set[2] = {false, false};
+    bool& done = attr_set[sizeof(T) == 8];
+    if (!done) {
+        (void)hipFuncSetAttribute((const void*)k_gate_lds<T>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        done = true;
     }
-    hipLaunchKernelGGL(k_gate<T>, dim3(fb.nf), dim3(256), 0, s, st, prm, fb, 0);
+    for (int c = 0; c < GateClasses::NC; ++c) {
+        const int cnt = gc.off[c + 1] - gc.off[c];
+        if (cnt == 0) continue;
+        const int maxM = gc.maxM[c];
+        const size_t lds = gate_lds_bytes<T>(maxM);
+        const int threads = maxM <= 12 ? 64 : (maxM <= 20 ? 128 : 256);
+        if (lds <= 160 * 1024)
+            hipLaunchKernelGGL(k_gate_lds<T>, dim3(cnt), dim3(threads), lds, s, st, prm, fb, gc.list + gc.off[c]);
+        else
+            hipLaunchKernelGGL(k_gate<T>, dim3(cnt), dim3(256), 0, s, st, prm, fb, gc.list + gc.off[c]);
+    }
 }
+
 template <typename T>
 void launch_select(hipStream_t s, const DevState<T>& st, const FeatBatch<T>& fb, const UpdWs<T>& ws,
                    int row_cap) {
@@ -1969,6 +1981,10 @@ void launch_compress(hipStream_t s, const DevState<T>& st, const FeatBatch<T>& f
             if (wide) {
                 hipLaunchKernelGGL((k_compress_wave<T, 64, 3>), dim3(st.B), dim3(64), lds + 4 * 32 * sizeof(T), s,
                                    st, fb, ws);
+                return;
+            }
+            if (g_compress_ch == 16) {
+                hipLaunchKernelGGL((k_compress_wave<T, 16, 3>), dim3(st.B), dim3(64), lds, s, st, fb, ws);
                 return;
             }
         }
@@ -2022,7 +2038,7 @@ void launch_kalman(hipStream_t s, const DevState<T>& st, const Params<T>& prm, c
     template void launch_prune<T>(hipStream_t, const DevState<T>&, int, const int*, int, T*, const int*, int); \
     template void launch_triangulate<T>(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&); \
     template void launch_feature<T>(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&); \
-    template void launch_gate<T>(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&, int); \
+    template void launch_gate<T>(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&, const GateClasses&); \
     template void launch_select<T>(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const UpdWs<T>&, int); \
     template void launch_compress<T>(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const UpdWs<T>&); \
     template void launch_kalman<T>(hipStream_t, const DevState<T>&, const Params<T>&, const UpdWs<T>&, KernelTimer*);

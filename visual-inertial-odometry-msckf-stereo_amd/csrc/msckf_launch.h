@@ -70,8 +70,15 @@ template <typename T>
 void launch_triangulate(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&);
 template <typename T>
 void launch_feature(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&);
+// Feature index lists per gating size class (device pointer + host offsets).
+struct GateClasses {
+    static constexpr int NC = 4;        // M <= 8, <= 16, <= 24, larger
+    const int* list = nullptr;
+    int off[NC + 1] = {0, 0, 0, 0, 0};
+    int maxM[NC] = {0, 0, 0, 0};
+};
 template <typename T>
-void launch_gate(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&, int maxM);
+void launch_gate(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&, const GateClasses&);
 template <typename T>
 void launch_select(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const UpdWs<T>&, int row_cap);
 template <typename T>
