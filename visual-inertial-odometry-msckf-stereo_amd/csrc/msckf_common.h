@@ -194,6 +194,13 @@ __device__ __forceinline__ double lane_bcast(double x, int src) {
     return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
 }
 
+// Fast reciprocal / square root for the fp32 throughput path (hardware
+// v_rcp_f32 / v_sqrt_f32, ~1 ulp); the fp64 parity path keeps IEEE ops.
+__device__ __forceinline__ float fast_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+__device__ __forceinline__ double fast_sqrt(double x) { return sqrt(x); }
+__device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ double fast_rcp(double x) { return 1.0 / x; }
+
 // ------------------------------------------------------ wave reductions --
 template <typename T>
 __device__ __forceinline__ T wave_sum(T x) {

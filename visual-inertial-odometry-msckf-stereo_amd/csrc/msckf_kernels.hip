@@ -17,6 +17,8 @@
 //   measurement_update S, K, dx, P msckf.py:559-604 (_fastSolve)    -> k_hp, k_s,
 //                                  k_chol, k_trsm, k_dx, k_pupdate, k_correct
 //   P compaction msckf.py:803-818                                   -> k_prune_*
+#include <type_traits>
+
 #include "msckf_common.h"
 #include "msckf_launch.h"
 
@@ -1656,6 +1658,192 @@ __global__ void __launch_bounds__(64) k_compress_wave(DevState<T> st, FeatBatch<
     }
 }
 
+// Lean one-wavefront-per-filter merge (default throughput path, C+1 <= 192).
+// Same algorithm as k_compress_wave with less live state: the generation
+// temporaries die before the sweep, the column loop is unrolled by two with a
+// two-rows-ahead R prefetch ring, and fp32 uses v_sqrt / v_rcp.
+template <typename T, int CH>
+__global__ void __launch_bounds__(64) k_compress_w(DevState<T> st, FeatBatch<T> fb, UpdWs<T> ws) {
+    constexpr int COLS = 3;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    const int b = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int* info = ws.info + 4 * b;
+    const int Rn = info[0], n = info[1], compress = info[2];
+    if (Rn == 0) return;
+    const int C = 6 * st.ncams[b];
+    const int ldh = ws.Cmax + 1;
+    T* H = ws.Hthin + (size_t)b * ws.Cmax * ldh;
+    T* s_V = reinterpret_cast<T*>(smem_raw);        // [CH][4] chunk rows of V | Qr
+    T* s_sc = s_V + 4 * CH;                         // tau_f[3] (+pad)
+    int* s_obs = reinterpret_cast<int*>(s_sc + 4);  // [Nmax]
+    int hcol[COLS];
+#pragma unroll
+    for (int u = 0; u < COLS; ++u) {
+        const int j = lane + 64 * u;
+        hcol[u] = (j == C) ? ws.Cmax : j;
+    }
+    if (compress) {
+        for (int r = 0; r < C; ++r)
+#pragma unroll
+            for (int u = 0; u < COLS; ++u)
+                if (lane + 64 * u <= C) H[(size_t)r * ldh + hcol[u]] = 0;
+    } else {
+        for (int e = lane; e < n * ldh; e += 64) H[e] = 0;
+    }
+    for (int f = fb.feat_off[b]; f < fb.feat_off[b + 1]; ++f) {
+        if (!fb.include[f]) continue;
+        const int o0 = fb.obs_off[f], M = fb.obs_off[f + 1] - o0;
+        const T* wsf = fb.obs_ws + (size_t)o0 * OBS_WS;
+        for (int i = lane; i < st.Nmax; i += 64) s_obs[i] = -1;
+        if (lane < 3) s_sc[lane] = fb.tau[4 * f + lane];
+        int smin = 1 << 30;
+        for (int i = 0; i < M; ++i) smin = min(smin, fb.obs_cam[o0 + i]);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        for (int i = lane; i < M; i += 64) s_obs[fb.obs_cam[o0 + i]] = i;
+        const int c0 = 6 * smin;
+        const int n4 = 4 * M;
+        for (int a0 = 3; a0 < n4; a0 += CH) {
+            const int nr = min(CH, n4 - a0);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            for (int rr = lane; rr < CH; rr += 64) {
+                const int row = a0 + rr;
+                if (rr < nr) {
+                    const T* wr = wsf + (size_t)(row >> 2) * OBS_WS;
+                    s_V[4 * rr + 0] = wr[OBS_V + 3 * (row & 3) + 0];
+                    s_V[4 * rr + 1] = wr[OBS_V + 3 * (row & 3) + 1];
+                    s_V[4 * rr + 2] = wr[OBS_V + 3 * (row & 3) + 2];
+                    s_V[4 * rr + 3] = wr[OBS_QR + (row & 3)];
+                } else {
+                    s_V[4 * rr + 0] = s_V[4 * rr + 1] = s_V[4 * rr + 2] = s_V[4 * rr + 3] = 0;
+                }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            // chunk rows as 2-wide vectors: rows (2i, 2i+1) pair up for v_pk_fma_f32
+            using V2 = T __attribute__((ext_vector_type(2)));
+            constexpr int CH2 = CH / 2;
+            V2 bv[COLS][CH2];
+#pragma unroll
+            for (int u = 0; u < COLS; ++u) {
+                const int j = lane + 64 * u;
+                const int oi = (j < C) ? s_obs[j / 6] : -1;
+                T w0 = 0, w1 = 0, w2 = 0, hx0 = 0, hx1 = 0, hx2 = 0, hx3 = 0;
+                if (oi >= 0) {
+                    const T* wo = wsf + (size_t)oi * OBS_WS;
+                    const int c = j % 6;
+                    w0 = s_sc[0] * wo[OBS_W + c];
+                    w1 = s_sc[1] * wo[OBS_W + 6 + c];
+                    w2 = s_sc[2] * wo[OBS_W + 12 + c];
+                    hx0 = wo[OBS_HX + c];
+                    hx1 = wo[OBS_HX + 6 + c];
+                    hx2 = wo[OBS_HX + 12 + c];
+                    hx3 = wo[OBS_HX + 18 + c];
+                }
+#pragma unroll
+                for (int rr = 0; rr < CH; ++rr) {
+                    const int row = a0 + rr;
+                    T x = 0;
+                    if (j == C) {
+                        x = s_V[4 * rr + 3];
+                    } else if (oi >= 0 && rr < nr) {
+                        const int ra = row & 3;
+                        T h = ra == 0 ? hx0 : (ra == 1 ? hx1 : (ra == 2 ? hx2 : hx3));
+                        h = ((row >> 2) == oi) ? h : T(0);
+                        x = h - (s_V[4 * rr] * w0 + s_V[4 * rr + 1] * w1 + s_V[4 * rr + 2] * w2);
+                    }
+                    if (rr & 1) bv[u][rr >> 1].y = x;
+                    else bv[u][rr >> 1].x = x;
+                }
+                __builtin_amdgcn_sched_barrier(0);   // keep the three columns' generation apart
+            }
+            if (!compress) {   // R <= C: the stacked rows are H_thin (msckf.py:554-556)
+                const int base = fb.row_off[f] + (a0 - 3);
+#pragma unroll
+                for (int u = 0; u < COLS; ++u)
+                    if (lane + 64 * u <= C)
+#pragma unroll
+                        for (int rr = 0; rr < CH; ++rr)
+                            if (rr < nr)
+                                H[(size_t)(base + rr) * ldh + hcol[u]] = (rr & 1) ? bv[u][rr >> 1].y : bv[u][rr >> 1].x;
+                continue;
+            }
+            auto load_row = [&](int r, int cmin, T* dst) {   // R[r][j] for own columns j >= cmin
+#pragma unroll
+                for (int u = 0; u < COLS; ++u) {
+                    const int j = lane + 64 * u;
+                    dst[u] = (r < C && j >= cmin && j <= C) ? H[(size_t)r * ldh + hcol[u]] : T(0);
+                }
+            };
+            // one column step: reflector of column c from the owner lane (slot UC)
+            auto step = [&](auto UCc, int c, const T* rrow) {
+                constexpr int UC = decltype(UCc)::value;
+                const int lc = c & 63;
+                V2 v[CH2];
+                V2 own2 = {0, 0};
+#pragma unroll
+                for (int i = 0; i < CH2; ++i) {
+                    v[i].x = lane_bcast(bv[UC][i].x, lc);
+                    v[i].y = lane_bcast(bv[UC][i].y, lc);
+                    own2 += bv[UC][i] * bv[UC][i];
+                }
+                const T xs = lane_bcast(own2.x + own2.y, lc);
+                const T alpha = lane_bcast(rrow[UC], lc);
+                T tj = 0, scale = 0, beta = alpha;
+                if (xs != T(0)) {
+                    const T nrm = fast_sqrt(alpha * alpha + xs);
+                    beta = alpha >= 0 ? -nrm : nrm;
+                    const T rb = fast_rcp(beta);
+                    tj = (beta - alpha) * rb;
+                    scale = fast_rcp(alpha - beta);
+                }
+                const T ts = tj * scale;
+#pragma unroll
+                for (int u = UC; u < COLS; ++u) {
+                    const int j = lane + 64 * u;
+                    if (j == c) {
+                        H[(size_t)c * ldh + hcol[u]] = beta;
+                    } else if (j > c && j <= C && tj != T(0)) {
+                        V2 q = {0, 0};
+#pragma unroll
+                        for (int i = 0; i < CH2; ++i) q += v[i] * bv[u][i];
+                        const T w = rrow[u] + scale * (q.x + q.y);
+                        H[(size_t)c * ldh + hcol[u]] = rrow[u] - tj * w;
+                        const T f2 = ts * w;
+                        const V2 f22 = {f2, f2};
+#pragma unroll
+                        for (int i = 0; i < CH2; ++i) bv[u][i] -= v[i] * f22;
+                    }
+                }
+            };
+            T rA[COLS], rB[COLS], rC[COLS], rD[COLS];
+            load_row(c0, c0, rA);
+            load_row(c0 + 1, c0 + 1, rB);
+            auto segment = [&](auto UCc) {
+                constexpr int UC = decltype(UCc)::value;
+                const int cb = max(c0, 64 * UC), ce = min(C, 64 * (UC + 1));
+                int c = cb;
+                for (; c + 1 < ce; c += 2) {
+                    load_row(c + 2, c + 2, rC);
+                    step(UCc, c, rA);
+                    load_row(c + 3, c + 3, rD);
+                    step(UCc, c + 1, rB);
+#pragma unroll
+                    for (int u = 0; u < COLS; ++u) { rA[u] = rC[u]; rB[u] = rD[u]; }
+                }
+                if (c < ce) {
+                    step(UCc, c, rA);
+                    load_row(c + 2, c + 2, rC);
+#pragma unroll
+                    for (int u = 0; u < COLS; ++u) { rA[u] = rB[u]; rB[u] = rC[u]; }
+                }
+            };
+            segment(std::integral_constant<int, 0>{});
+            segment(std::integral_constant<int, 1>{});
+            segment(std::integral_constant<int, 2>{});
+        }
+    }
+}
+
 // ===========================================================================
 // Kalman update (msckf.py:559-604) on H_thin (n x C, IMU columns zero):
 //   HP = H_thin P[21:D, :]              k_hp      (n x D)
@@ -1970,12 +2158,21 @@ template <typename T>
 void launch_compress(hipStream_t s, const DevState<T>& st, const FeatBatch<T>& fb, const UpdWs<T>& ws) {
     if (g_compress_ch < 0) {
         const char* e = getenv("MSCKF_COMPRESS_CH");
-        g_compress_ch = e ? atoi(e) : 32;
+        g_compress_ch = e ? atoi(e) : 16;
     }
     const bool wide = g_compress_ch >= 64 && sizeof(T) == 4;
     const char* me = getenv("MSCKF_COMPRESS_MODE");   // wave (default) | panel | block
     const int mode = me ? (me[0] == 'p' ? 1 : (me[0] == 'b' ? 2 : 0)) : 0;
     if (mode == 0 && ws.Cmax + 1 <= 192) {
+        const char* we = getenv("MSCKF_COMPRESS_W");
+        if (!we || atoi(we) != 0) {
+            const size_t lds = (4 * 32 + 4) * sizeof(T) + ((st.Nmax + 3) & ~3) * sizeof(int);
+            if (g_compress_ch == 32)
+                hipLaunchKernelGGL((k_compress_w<T, 32>), dim3(st.B), dim3(64), lds, s, st, fb, ws);
+            else
+                hipLaunchKernelGGL((k_compress_w<T, 16>), dim3(st.B), dim3(64), lds, s, st, fb, ws);
+            return;
+        }
         const size_t lds = (4 * 32 + 4) * sizeof(T) + ((st.Nmax + 3) & ~3) * sizeof(int);
         if constexpr (sizeof(T) == 4) {
             if (wide) {
