@@ -123,9 +123,9 @@ template <typename T>
 UpdWs<T> upd_ws(msckf_ctx* c) {
     UpdWs<T> w;
     w.Hthin = reinterpret_cast<T*>(c->Hthin.p);
-    w.HP = reinterpret_cast<T*>(c->HP.p);
-    w.S = reinterpret_cast<T*>(c->S.p);
-    w.dx = reinterpret_cast<T*>(c->dx.p);
+    w.HP = reinterpret_cast<KT*>(c->HP.p);
+    w.S = reinterpret_cast<KT*>(c->S.p);
+    w.dx = reinterpret_cast<KT*>(c->dx.p);
     w.info = c->info.p;
     w.Cmax = c->Cmax;
     return w;
@@ -232,7 +232,12 @@ int load_features(msckf_ctx* c, int nf, const int32_t* feat_off, int single_filt
     HIPC(c->p_w.ensure((nf * 3 + 3) * ts));
     HIPC(c->obs_ws.ensure((nobs * OBS_WS + OBS_WS) * ts));
     HIPC(c->tau.ensure((nf * 4 + 4) * ts));
-    HIPC(c->ysq.ensure((size_t)(ysq[nf] + 16) * ts));
+    {   // the (4M)^2 global gating scratch is only needed by features too large
+        // for the LDS gating path (M > ~50 in fp32, > ~35 in fp64)
+        const size_t n4 = 4 * (size_t)maxM;
+        const size_t lds = ((n4 * (n4 + 1) + 1) & ~(size_t)1) * ts + (12 * n4 + 4) * ts + (maxM + 4) * sizeof(int);
+        if (lds > 160 * 1024) HIPC(c->ysq.ensure((size_t)(ysq[nf] + 16) * ts));
+    }
     HIPC(c->gamma.ensure((nf + 1) * ts));
     HIPC(c->valid.ensure(nf + 1));
     HIPC(c->accept.ensure(nf + 1));
@@ -353,9 +358,9 @@ int do_create(msckf_ctx* c) {
     HIPC(c->cams.ensure(B * c->Nmax * CAM_STRIDE * ts));
     HIPC(c->ncams.ensure(B));
     HIPC(c->Hthin.ensure(B * c->Cmax * (c->Cmax + 1) * ts));
-    HIPC(c->HP.ensure(B * c->Cmax * c->Dmax * ts));
-    HIPC(c->S.ensure(B * c->Cmax * c->Cmax * ts));
-    HIPC(c->dx.ensure(B * c->Dmax * ts));
+    HIPC(c->HP.ensure(B * c->Cmax * c->Dmax * sizeof(KT)));
+    HIPC(c->S.ensure(B * c->Cmax * c->Cmax * sizeof(KT)));
+    HIPC(c->dx.ensure(B * (c->Dmax + c->Cmax) * sizeof(KT)));
     HIPC(c->info.ensure(4 * B));
     HIPC(hipMemset(c->P.p, 0, c->P.cap));
     HIPC(hipMemset(c->cams.p, 0, c->cams.cap));

@@ -66,13 +66,18 @@ struct FeatBatch {
     int* row_off;             // [nf] first stacked row of the feature
 };
 
-// Per-filter update workspace.
+// Per-filter update workspace.  The Kalman stage always computes in fp64
+// (KT = double): after compression the rows of H_thin carry the information of
+// ~1e4 measurements, so S = H P H^T + s2 I spans ~8 decades (s2 ~ 1e-3 vs
+// |H P H^T| ~ 1e5) -- beyond fp32 -- while the O(R C^2) QR and the per-feature
+// gating (condition ~1e3) stay in the context's scalar type T.
+using KT = double;
 template <typename T>
 struct UpdWs {
-    T* Hthin;    // [B][Cmax][Cmax+1]   (H_thin | r_thin)
-    T* HP;       // [B][Cmax][Dmax]     H_thin P, then L^-1 H_thin P
-    T* S;        // [B][Cmax][Cmax]     innovation covariance -> its Cholesky factor
-    T* dx;       // [B][Dmax]
+    T* Hthin;    // [B][Cmax][Cmax+1]   (H_thin | r_thin), scalar type T
+    KT* HP;      // [B][Cmax][Dmax]     H_thin P, then L^-1 H_thin P
+    KT* S;       // [B][Cmax][Cmax]     innovation covariance -> its Cholesky factor
+    KT* dx;      // [B][Dmax]
     int* info;   // [B][4]: rows stacked, n (rows of H_thin), compress flag, status
     int Cmax;
 };

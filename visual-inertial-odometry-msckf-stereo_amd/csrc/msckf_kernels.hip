@@ -1860,7 +1860,7 @@ constexpr int TB = 32;
 // C[i][j] (+)= sum_k A(i,k) B(k,j) with accessor lambdas; tile (ti, tj) of a
 // m x nn output, K = kk, 256 threads, 2x2 outputs per thread.
 template <typename T, typename FA, typename FB, typename FC>
-__device__ __forceinline__ void tile_gemm(int m, int nn, int kk, int ti, int tj, FA A, FB Bf, FC Cf) {
+__device__ __forceinline__ void tile_gemm(int m, int nn, int kk, int ti, int tj, FA A, FB Bf, FC Cf) {   // T = accumulation type
     __shared__ T sa[TB][TB + 1], sb[TB][TB + 1];
     const int tid = threadIdx.x;
     const int tx = tid % 16, ty = tid / 16;
@@ -1899,12 +1899,12 @@ __global__ void __launch_bounds__(256) k_hp(DevState<T> st, UpdWs<T> ws) {
     if (ti * TB >= n || tj * TB >= D) return;
     const T* H = ws.Hthin + (size_t)b * ws.Cmax * (ws.Cmax + 1);
     const T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
-    T* HP = ws.HP + (size_t)b * ws.Cmax * st.Dmax;
+    KT* HP = ws.HP + (size_t)b * ws.Cmax * st.Dmax;
     const int ldh = ws.Cmax + 1, ld = st.Dmax;
-    tile_gemm<T>(n, D, C, ti, tj,
-                 [&](int i, int k) { return H[(size_t)i * ldh + k]; },
-                 [&](int k, int j) { return P[(size_t)(21 + k) * ld + j]; },
-                 [&](int i, int j, T v) { HP[(size_t)i * ld + j] = v; });
+    tile_gemm<KT>(n, D, C, ti, tj,
+                  [&](int i, int k) { return (KT)H[(size_t)i * ldh + k]; },
+                  [&](int k, int j) { return (KT)P[(size_t)(21 + k) * ld + j]; },
+                  [&](int i, int j, KT v) { HP[(size_t)i * ld + j] = v; });
 }
 
 template <typename T>
@@ -1915,14 +1915,14 @@ __global__ void __launch_bounds__(256) k_s(DevState<T> st, Params<T> prm, UpdWs<
     const int ti = blockIdx.y, tj = blockIdx.x;
     if (ti * TB >= n || tj * TB >= n || tj > ti) return;   // lower triangle of tiles
     const T* H = ws.Hthin + (size_t)b * ws.Cmax * (ws.Cmax + 1);
-    const T* HP = ws.HP + (size_t)b * ws.Cmax * st.Dmax;
-    T* S = ws.S + (size_t)b * ws.Cmax * ws.Cmax;
+    const KT* HP = ws.HP + (size_t)b * ws.Cmax * st.Dmax;
+    KT* S = ws.S + (size_t)b * ws.Cmax * ws.Cmax;
     const int ldh = ws.Cmax + 1, ld = st.Dmax, lds = ws.Cmax;
-    const T s2 = prm.sigma2;
-    tile_gemm<T>(n, n, C, ti, tj,
-                 [&](int i, int k) { return HP[(size_t)i * ld + 21 + k]; },
-                 [&](int k, int j) { return H[(size_t)j * ldh + k]; },
-                 [&](int i, int j, T v) { S[(size_t)i * lds + j] = v + (i == j ? s2 : T(0)); });
+    const KT s2 = (KT)prm.sigma2;
+    tile_gemm<KT>(n, n, C, ti, tj,
+                  [&](int i, int k) { return HP[(size_t)i * ld + 21 + k]; },
+                  [&](int k, int j) { return (KT)H[(size_t)j * ldh + k]; },
+                  [&](int i, int j, KT v) { S[(size_t)i * lds + j] = v + (i == j ? s2 : KT(0)); });
 }
 
 // Cholesky of S (lower, in place) + y_r = L^-1 r_thin; one workgroup per filter.
@@ -1932,28 +1932,28 @@ __global__ void __launch_bounds__(256) k_chol(DevState<T> st, UpdWs<T> ws) {
     const int tid = threadIdx.x;
     const int n = ws.info[4 * b + 1];
     if (n == 0) return;
-    T* S = ws.S + (size_t)b * ws.Cmax * ws.Cmax;
+    KT* S = ws.S + (size_t)b * ws.Cmax * ws.Cmax;
     const int lds = ws.Cmax;
     const T* H = ws.Hthin + (size_t)b * ws.Cmax * (ws.Cmax + 1);
     const int ldh = ws.Cmax + 1;
-    __shared__ T s_y[512];
+    __shared__ KT s_y[512];
     __shared__ int s_fail;
     for (int i = tid; i < n; i += blockDim.x) s_y[i] = H[(size_t)i * ldh + ws.Cmax];
     if (tid == 0) s_fail = 0;
     __syncthreads();
     for (int j = 0; j < n; ++j) {
         if (tid == 0) {
-            T d = S[(size_t)j * lds + j];
-            if (!(d > 0)) { s_fail = 1; d = T(1); }
-            T l = sqrt(d);
+            KT d = S[(size_t)j * lds + j];
+            if (!(d > 0)) { s_fail = 1; d = KT(1); }
+            KT l = sqrt(d);
             S[(size_t)j * lds + j] = l;
             s_y[j] = s_y[j] / l;
         }
         __syncthreads();
-        const T ljj = S[(size_t)j * lds + j];
-        const T yj = s_y[j];
+        const KT ljj = S[(size_t)j * lds + j];
+        const KT yj = s_y[j];
         for (int i = j + 1 + tid; i < n; i += blockDim.x) {
-            T lij = S[(size_t)i * lds + j] / ljj;
+            KT lij = S[(size_t)i * lds + j] / ljj;
             S[(size_t)i * lds + j] = lij;
             s_y[i] -= lij * yj;
         }
@@ -1965,9 +1965,9 @@ __global__ void __launch_bounds__(256) k_chol(DevState<T> st, UpdWs<T> ws) {
         }
         __syncthreads();
     }
-    // store y_r in the residual column of H_thin (no longer needed as r_thin)
-    T* Hw = ws.Hthin + (size_t)b * ws.Cmax * (ws.Cmax + 1);
-    for (int i = tid; i < n; i += blockDim.x) Hw[(size_t)i * ldh + ws.Cmax] = s_y[i];
+    // y_r = L^-1 r_thin goes to the tail of the dx row (dx itself is D long)
+    KT* yr = ws.dx + (size_t)b * (st.Dmax + ws.Cmax) + st.Dmax;
+    for (int i = tid; i < n; i += blockDim.x) yr[i] = s_y[i];
     if (tid == 0 && s_fail) ws.info[4 * b + 3] = -1;
 }
 
@@ -1979,11 +1979,11 @@ __global__ void __launch_bounds__(256) k_trsm(DevState<T> st, UpdWs<T> ws) {
     const int D = 21 + 6 * st.ncams[b];
     const int col = blockIdx.x * blockDim.x + threadIdx.x;
     if (n == 0 || col >= D) return;
-    const T* L = ws.S + (size_t)b * ws.Cmax * ws.Cmax;
-    T* HP = ws.HP + (size_t)b * ws.Cmax * st.Dmax;
+    const KT* L = ws.S + (size_t)b * ws.Cmax * ws.Cmax;
+    KT* HP = ws.HP + (size_t)b * ws.Cmax * st.Dmax;
     const int lds = ws.Cmax, ld = st.Dmax;
     for (int i = 0; i < n; ++i) {
-        T s = HP[(size_t)i * ld + col];
+        KT s = HP[(size_t)i * ld + col];
         for (int j = 0; j < i; ++j) s -= L[(size_t)i * lds + j] * HP[(size_t)j * ld + col];
         HP[(size_t)i * ld + col] = s / L[(size_t)i * lds + i];
     }
@@ -1996,13 +1996,12 @@ __global__ void __launch_bounds__(256) k_dx(DevState<T> st, UpdWs<T> ws) {
     const int n = ws.info[4 * b + 1];
     const int D = 21 + 6 * st.ncams[b];
     if (n == 0) return;
-    const T* Y = ws.HP + (size_t)b * ws.Cmax * st.Dmax;
-    const T* H = ws.Hthin + (size_t)b * ws.Cmax * (ws.Cmax + 1);
-    const int ldh = ws.Cmax + 1;
-    T* dx = ws.dx + (size_t)b * st.Dmax;
+    const KT* Y = ws.HP + (size_t)b * ws.Cmax * st.Dmax;
+    KT* dx = ws.dx + (size_t)b * (st.Dmax + ws.Cmax);
+    const KT* yr = dx + st.Dmax;
     for (int col = threadIdx.x; col < D; col += blockDim.x) {
-        T s = 0;
-        for (int i = 0; i < n; ++i) s += Y[(size_t)i * st.Dmax + col] * H[(size_t)i * ldh + ws.Cmax];
+        KT s = 0;
+        for (int i = 0; i < n; ++i) s += Y[(size_t)i * st.Dmax + col] * yr[i];
         dx[col] = s;
     }
 }
@@ -2016,13 +2015,13 @@ __global__ void __launch_bounds__(256) k_pupdate(DevState<T> st, UpdWs<T> ws) {
     const int D = 21 + 6 * st.ncams[b];
     const int ti = blockIdx.y, tj = blockIdx.x;
     if (n == 0 || ti * TB >= D || tj * TB >= D) return;
-    const T* Y = ws.HP + (size_t)b * ws.Cmax * st.Dmax;
+    const KT* Y = ws.HP + (size_t)b * ws.Cmax * st.Dmax;
     T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
     const int ld = st.Dmax;
-    tile_gemm<T>(D, D, n, ti, tj,
-                 [&](int i, int k) { return Y[(size_t)k * ld + i]; },
-                 [&](int k, int j) { return Y[(size_t)k * ld + j]; },
-                 [&](int i, int j, T v) { P[(size_t)i * ld + j] -= v; });
+    tile_gemm<KT>(D, D, n, ti, tj,
+                  [&](int i, int k) { return Y[(size_t)k * ld + i]; },
+                  [&](int k, int j) { return Y[(size_t)k * ld + j]; },
+                  [&](int i, int j, KT v) { P[(size_t)i * ld + j] = (T)((KT)P[(size_t)i * ld + j] - v); });
 }
 
 // State correction (msckf.py:566-595).
@@ -2031,7 +2030,10 @@ __global__ void __launch_bounds__(64) k_correct(DevState<T> st, UpdWs<T> ws) {
     const int b = blockIdx.x;
     const int n = ws.info[4 * b + 1];
     if (n == 0) return;
-    const T* dx = ws.dx + (size_t)b * st.Dmax;
+    const KT* dxk = ws.dx + (size_t)b * (st.Dmax + ws.Cmax);
+    T dxs[21];
+    for (int i = 0; i < 21; ++i) dxs[i] = (T)dxk[i];
+    const T* dx = dxs;
     T* imu = st.imu + (size_t)b * IMU_STRIDE;
     const int nc = st.ncams[b];
     const int tid = threadIdx.x;
@@ -2055,7 +2057,8 @@ __global__ void __launch_bounds__(64) k_correct(DevState<T> st, UpdWs<T> ws) {
     }
     T* cams = st.cams + (size_t)b * st.Nmax * CAM_STRIDE;
     for (int c = tid; c < nc; c += blockDim.x) {
-        const T* d = dx + 21 + 6 * c;
+        T d[6];
+        for (int i = 0; i < 6; ++i) d[i] = (T)dxk[21 + 6 * c + i];
         T dq[4], q[4];
         small_angle_quat(d, dq);
         quat_mul(dq, cams + (size_t)c * CAM_STRIDE + C_Q, q);
