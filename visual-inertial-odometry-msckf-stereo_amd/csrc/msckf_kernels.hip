@@ -1590,6 +1590,7 @@ __global__ void __launch_bounds__(64) k_compress_wave(DevState<T> st, FeatBatch<
                             if (rr < nr) H[(size_t)(base + rr) * ldh + hcol[u]] = bv[u][rr];
                 continue;
             }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // same-address RAW on R rows
             T rcur[COLS];
 #pragma unroll
             for (int u = 0; u < COLS; ++u) {
@@ -1815,6 +1816,10 @@ __global__ void __launch_bounds__(64) k_compress_w(DevState<T> st, FeatBatch<T> 
                     }
                 }
             };
+            // R rows written by this wave's previous chunk (or the zero fill) are
+            // re-read below: drain its stores first -- a load may otherwise
+            // overtake a same-address store under heavy memory traffic
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             T rA[COLS], rB[COLS], rC[COLS], rD[COLS];
             load_row(c0, c0, rA);
             load_row(c0 + 1, c0 + 1, rB);
@@ -1971,7 +1976,9 @@ __global__ void __launch_bounds__(256) k_chol(DevState<T> st, UpdWs<T> ws) {
     if (tid == 0 && s_fail) ws.info[4 * b + 3] = -1;
 }
 
-// Y = L^-1 HP, one thread per column of HP.
+// Y = L^-1 HP, one thread per column of HP.  Rows are solved in blocks of 8
+// kept in registers; each block's stores are drained before later blocks
+// re-read them (same-address RAW through global memory).
 template <typename T>
 __global__ void __launch_bounds__(256) k_trsm(DevState<T> st, UpdWs<T> ws) {
     const int b = blockIdx.y;
@@ -1982,10 +1989,27 @@ __global__ void __launch_bounds__(256) k_trsm(DevState<T> st, UpdWs<T> ws) {
     const KT* L = ws.S + (size_t)b * ws.Cmax * ws.Cmax;
     KT* HP = ws.HP + (size_t)b * ws.Cmax * st.Dmax;
     const int lds = ws.Cmax, ld = st.Dmax;
-    for (int i = 0; i < n; ++i) {
-        KT s = HP[(size_t)i * ld + col];
-        for (int j = 0; j < i; ++j) s -= L[(size_t)i * lds + j] * HP[(size_t)j * ld + col];
-        HP[(size_t)i * ld + col] = s / L[(size_t)i * lds + i];
+    constexpr int RB = 8;
+    for (int i0 = 0; i0 < n; i0 += RB) {
+        KT y[RB];
+#pragma unroll
+        for (int t = 0; t < RB; ++t) y[t] = (i0 + t < n) ? HP[(size_t)(i0 + t) * ld + col] : KT(0);
+        for (int j = 0; j < i0; ++j) {   // earlier blocks (already final in memory)
+            const KT yj = HP[(size_t)j * ld + col];
+#pragma unroll
+            for (int t = 0; t < RB; ++t)
+                if (i0 + t < n) y[t] -= L[(size_t)(i0 + t) * lds + j] * yj;
+        }
+#pragma unroll
+        for (int t = 0; t < RB; ++t) {   // inside the block
+            if (i0 + t < n) {
+#pragma unroll
+                for (int q = 0; q < t; ++q) y[t] -= L[(size_t)(i0 + t) * lds + i0 + q] * y[q];
+                y[t] /= L[(size_t)(i0 + t) * lds + i0 + t];
+                HP[(size_t)(i0 + t) * ld + col] = y[t];
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
 }
 
