@@ -174,9 +174,9 @@ def test_update_empty_is_noop():
 
 # --------------------------------------------------- full-size batched mode --
 
-def _batched(problems, dtype, triangulate=True, row_cap=0):
+def _batched(problems, dtype, triangulate=True, row_cap=0, cap=None):
     ds = [problem_to_dict(p) for p in problems]
-    ctx = make_ctx(ds, dtype=dtype)
+    ctx = make_ctx(ds, dtype=dtype, cap=cap)
     feat_off = np.concatenate([[0], np.cumsum([p.F for p in problems])])
     obs_off, cams, zs, chi = [0], [], [], []
     for p in problems:
@@ -191,10 +191,13 @@ def _batched(problems, dtype, triangulate=True, row_cap=0):
     return ctx, ds, feat_off, acc, gam, pw, valid, rows
 
 
-@pytest.mark.parametrize("N,F,B", [(30, 200, 2), (50, 120, 1)])
-def test_batched_fp64_vs_oracle(N, F, B):
+@pytest.mark.parametrize("N,F,B,cap", [(30, 200, 2, 30), (30, 200, 1, 32), (50, 120, 1, None)])
+def test_batched_fp64_vs_oracle(N, F, B, cap):
+    """cap = cam capacity of the context: 30 (C + 1 <= 192) selects the
+    one-wave-per-filter QR kernel, 32 the 16-column panel kernel, 50+ the
+    two-column-per-thread kernel."""
     problems = [synth.make_update_problem(N, F, seed=100 + b) for b in range(B)]
-    ctx, ds, feat_off, acc, gam, pw, valid, rows = _batched(problems, np.float64)
+    ctx, ds, feat_off, acc, gam, pw, valid, rows = _batched(problems, np.float64, cap=cap)
     for b, d in enumerate(ds):
         st, acc_o, tri_p, tri_ok, gam_o = oracle_update(d)
         sl = slice(feat_off[b], feat_off[b + 1])
@@ -207,9 +210,10 @@ def test_batched_fp64_vs_oracle(N, F, B):
         np.testing.assert_allclose(unpack_imu(imu)["p"], st.imu.p, atol=1e-10)
 
 
-def test_batched_fp32_vs_oracle():
+@pytest.mark.parametrize("cap", [30, 32])
+def test_batched_fp32_vs_oracle(cap):
     problems = [synth.make_update_problem(30, 200, seed=200 + b) for b in range(3)]
-    ctx, ds, feat_off, acc, gam, pw, valid, rows = _batched(problems, np.float32)
+    ctx, ds, feat_off, acc, gam, pw, valid, rows = _batched(problems, np.float32, cap=cap)
     for b, d in enumerate(ds):
         st, acc_o, tri_p, tri_ok, gam_o = oracle_update(d)
         sl = slice(feat_off[b], feat_off[b + 1])

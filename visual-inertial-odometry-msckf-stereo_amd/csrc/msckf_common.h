@@ -199,11 +199,13 @@ __device__ __forceinline__ double lane_bcast(double x, int src) {
     return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
 }
 
-// Fast reciprocal / square root for the fp32 throughput path (hardware
-// v_rcp_f32 / v_sqrt_f32, ~1 ulp); the fp64 parity path keeps IEEE ops.
-__device__ __forceinline__ float fast_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+// Reciprocal / square root used by the Householder reflectors.  Deliberately
+// IEEE (denormal-safe): the hardware v_rcp_f32 / v_sqrt_f32 flush denormal
+// inputs, and columns in the near-null (gauge) directions of H carry tiny
+// entries with alpha ~ 0 -- the approximations turn those into inf / NaN.
+__device__ __forceinline__ float fast_sqrt(float x) { return sqrtf(x); }
 __device__ __forceinline__ double fast_sqrt(double x) { return sqrt(x); }
-__device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ float fast_rcp(float x) { return 1.0f / x; }
 __device__ __forceinline__ double fast_rcp(double x) { return 1.0 / x; }
 
 // ------------------------------------------------------ wave reductions --
