@@ -39,7 +39,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=512, help="independent filters per GPU per step")
+    ap.add_argument("--batch", type=int, default=2048, help="independent filters per GPU per step")
     ap.add_argument("--N", type=int, default=30)
     ap.add_argument("--F", type=int, default=200)
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "fp64"])
