@@ -68,7 +68,7 @@ struct msckf_ctx {
     DBuf<unsigned char> P, imu, cams, P_snap, imu_snap, cams_snap;
     DBuf<int> ncams, ncams_snap;
     // update workspace
-    DBuf<unsigned char> Hthin, HP, S, dx;
+    DBuf<unsigned char> Hthin, Hqr, HP, S, dx;
     DBuf<int> info;
     // feature batch
     int nf = 0, maxM = 0;
@@ -76,7 +76,7 @@ struct msckf_ctx {
     DBuf<int> feat_filter, feat_off, obs_off, obs_cam, row_off, gate_list;
     GateClasses gc;
     DBuf<long long> ysq_off;
-    DBuf<unsigned char> obs_z, chi2, p_w, obs_ws, tau, ysq, gamma;
+    DBuf<unsigned char> obs_z, chi2, p_w, obs_ws, obs_g, tau, ysq, gamma;
     DBuf<uint8_t> valid, accept, include;
     // misc scratch
     DBuf<unsigned char> scratch;
@@ -122,7 +122,8 @@ DevState<T> dev_state(msckf_ctx* c) {
 template <typename T>
 UpdWs<T> upd_ws(msckf_ctx* c) {
     UpdWs<T> w;
-    w.Hthin = reinterpret_cast<T*>(c->Hthin.p);
+    w.Hthin = reinterpret_cast<KT*>(c->Hthin.p);
+    w.Hqr = reinterpret_cast<T*>(c->Hqr.p);
     w.HP = reinterpret_cast<KT*>(c->HP.p);
     w.S = reinterpret_cast<KT*>(c->S.p);
     w.dx = reinterpret_cast<KT*>(c->dx.p);
@@ -145,6 +146,7 @@ FeatBatch<T> feat_batch(msckf_ctx* c) {
     f.p_w = reinterpret_cast<T*>(c->p_w.p);
     f.valid = c->valid.p;
     f.obs_ws = reinterpret_cast<T*>(c->obs_ws.p);
+    f.obs_g = reinterpret_cast<double*>(c->obs_g.p);
     f.tau = reinterpret_cast<T*>(c->tau.p);
     f.ysq = reinterpret_cast<T*>(c->ysq.p);
     f.gamma = reinterpret_cast<T*>(c->gamma.p);
@@ -213,7 +215,7 @@ int load_features(msckf_ctx* c, int nf, const int32_t* feat_off, int single_filt
         int M = obs_off[f + 1] - obs_off[f];
         maxM = std::max(maxM, M);
         int b = h_filt[f];
-        if (M < 1 || M > 128) FAIL(-1, "feature %d has %d observations (1..128 supported)", f, M);
+        if (M < 1 || M > 64) FAIL(-1, "feature %d has %d observations (1..64 supported)", f, M);
         if (M > c->h_ncams[b]) FAIL(-1, "feature %d has more observations than cam states", f);
         for (int i = obs_off[f]; i < obs_off[f + 1]; ++i)
             if (obs_cam[i] < 0 || obs_cam[i] >= c->h_ncams[b])
@@ -231,6 +233,7 @@ int load_features(msckf_ctx* c, int nf, const int32_t* feat_off, int single_filt
     HIPC(c->chi2.ensure((nf + 1) * ts));
     HIPC(c->p_w.ensure((nf * 3 + 3) * ts));
     HIPC(c->obs_ws.ensure((nobs * OBS_WS + OBS_WS) * ts));
+    HIPC(c->obs_g.ensure((nobs + 1) * OBG_STRIDE * sizeof(double)));
     HIPC(c->tau.ensure((nf * 4 + 4) * ts));
     {   // the (4M)^2 global gating scratch is only needed by features too large
         // for the LDS gating path (M > ~50 in fp32, > ~35 in fp64)
@@ -357,7 +360,11 @@ int do_create(msckf_ctx* c) {
     HIPC(c->imu.ensure(B * IMU_STRIDE * ts));
     HIPC(c->cams.ensure(B * c->Nmax * CAM_STRIDE * ts));
     HIPC(c->ncams.ensure(B));
-    HIPC(c->Hthin.ensure(B * c->Cmax * (c->Cmax + 1) * ts));
+    HIPC(c->Hthin.ensure(B * c->Cmax * (c->Cmax + 1) * sizeof(KT)));
+    {   // QR row-merge scratch only for MSCKF_COMPRESS=qr (A/B runs)
+        const char* e = getenv("MSCKF_COMPRESS");
+        if (e && e[0] == 'q') HIPC(c->Hqr.ensure(B * c->Cmax * (c->Cmax + 1) * ts));
+    }
     HIPC(c->HP.ensure(B * c->Cmax * c->Dmax * sizeof(KT)));
     HIPC(c->S.ensure(B * c->Cmax * c->Cmax * sizeof(KT)));
     HIPC(c->dx.ensure(B * (c->Dmax + c->Cmax) * sizeof(KT)));
@@ -553,7 +560,7 @@ int msckf_create(const msckf_config_t* cfg, int hip_device, int scalar_bytes, in
     if (!cfg || !out) FAIL(-1, "null argument");
     if (scalar_bytes != 4 && scalar_bytes != 8) FAIL(-1, "scalar_bytes must be 4 or 8");
     if (n_filters < 1) FAIL(-1, "n_filters must be >= 1");
-    if (n_cam_capacity < 1 || n_cam_capacity > 128) FAIL(-1, "n_cam_capacity must be in [1, 128]");
+    if (n_cam_capacity < 1 || n_cam_capacity > 64) FAIL(-1, "n_cam_capacity must be in [1, 64]");
     int ndev = 0;
     HIPC(hipGetDeviceCount(&ndev));
     if (hip_device < 0 || hip_device >= ndev) FAIL(-1, "HIP device %d not present (%d visible)", hip_device, ndev);
@@ -584,8 +591,8 @@ int msckf_destroy(msckf_ctx_t* c) {
     if (!c) return 0;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (auto* b : {&c->P, &c->imu, &c->cams, &c->P_snap, &c->imu_snap, &c->cams_snap, &c->Hthin, &c->HP, &c->S,
-                    &c->dx, &c->obs_z, &c->chi2, &c->p_w, &c->obs_ws, &c->tau, &c->ysq, &c->gamma, &c->scratch})
+    for (auto* b : {&c->P, &c->imu, &c->cams, &c->P_snap, &c->imu_snap, &c->cams_snap, &c->Hthin, &c->Hqr, &c->HP, &c->S,
+                    &c->dx, &c->obs_z, &c->chi2, &c->p_w, &c->obs_ws, &c->obs_g, &c->tau, &c->ysq, &c->gamma, &c->scratch})
         b->release();
     for (auto* b : {&c->ncams, &c->ncams_snap, &c->info, &c->feat_filter, &c->feat_off, &c->obs_off, &c->obs_cam,
                     &c->row_off, &c->iscratch, &c->gate_list})

@@ -26,6 +26,16 @@ enum CamField { C_Q = 0, C_P = 4, C_QN = 7 };
 //   Qr  4    rows of Q^T r
 constexpr int OBS_HX = 0, OBS_V = 24, OBS_W = 36, OBS_QR = 54, OBS_WS = 58;
 
+// Per-observation Gram terms written by the feature kernel (always fp64),
+// consumed by the information assembly (k_info).  With G = the top 3 rows of
+// Q^T Hx (Q = the feature's 3 Householder reflectors) and g = (Q^T r)[0:3]:
+//   G   3x6  this observation's columns of G
+//   DS  21   Hx_i^T Hx_i, lower triangle packed row-major
+//   UB  6    Hx_i^T r_i - G_i^T g
+// so that the projected block H0 = (Q^T Hx)[3:] satisfies
+//   H0^T H0 = blockdiag_i(Hx_i^T Hx_i) - G^T G,   H0^T r0 = sum_i UB_i.
+constexpr int OBG_G = 0, OBG_DS = 18, OBG_UB = 39, OBG_STRIDE = 48;
+
 template <typename T>
 struct Params {
     T sigma2;                 // observation noise variance (msckf.py:560)
@@ -58,6 +68,7 @@ struct FeatBatch {
     T* p_w;                   // [nf][3]
     uint8_t* valid;           // [nf] triangulation validity (1 if p_w given)
     T* obs_ws;                // [sum M][OBS_WS]
+    double* obs_g;            // [sum M][OBG_STRIDE] Gram terms (fp64)
     T* tau;                   // [nf][4]
     T* ysq;                   // gating scratch
     T* gamma;                 // [nf]
@@ -66,15 +77,16 @@ struct FeatBatch {
     int* row_off;             // [nf] first stacked row of the feature
 };
 
-// Per-filter update workspace.  The Kalman stage always computes in fp64
-// (KT = double): after compression the rows of H_thin carry the information of
-// ~1e4 measurements, so S = H P H^T + s2 I spans ~8 decades (s2 ~ 1e-3 vs
-// |H P H^T| ~ 1e5) -- beyond fp32 -- while the O(R C^2) QR and the per-feature
-// gating (condition ~1e3) stay in the context's scalar type T.
+// Per-filter update workspace.  The information assembly and the Kalman stage
+// always compute in fp64 (KT = double): after compression the rows of H_thin
+// carry the information of ~1e4 measurements, so S = H P H^T + s2 I spans ~8
+// decades (s2 ~ 1e-3 vs |H P H^T| ~ 1e5) -- beyond fp32 -- while the
+// per-feature gating (condition ~1e3) stays in the context's scalar type T.
 using KT = double;
 template <typename T>
 struct UpdWs {
-    T* Hthin;    // [B][Cmax][Cmax+1]   (H_thin | r_thin), scalar type T
+    KT* Hthin;   // [B][Cmax][Cmax+1]   (H_thin | r_thin): rows of the factor F, F^T F = H^T H
+    T* Hqr;      // [B][Cmax][Cmax+1]   QR row-merge output (MSCKF_COMPRESS=qr only)
     KT* HP;      // [B][Cmax][Dmax]     H_thin P, then L^-1 H_thin P
     KT* S;       // [B][Cmax][Cmax]     innovation covariance -> its Cholesky factor
     KT* dx;      // [B][Dmax]

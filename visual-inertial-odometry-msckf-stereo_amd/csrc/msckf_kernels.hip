@@ -622,54 +622,67 @@ __global__ void __launch_bounds__(256) k_triangulate(DevState<T> st, Params<T> p
 
 // ===========================================================================
 // Feature Jacobian + left-nullspace projection: one wavefront per feature,
-// lane i owns observation i (and i+64).  Computes the observability-projected
+// lane i owns observation i (M <= 64: a feature is seen at most once per cam
+// state and the cam capacity is <= 64).  Computes the observability-projected
 // 4x6 / 4x3 blocks and residual, Householder-QRs H_f (4M x 3) across the wave
-// with xor-shuffle reductions (LAPACK dlarfg sign convention), and stores the
-// compact factors of H0 = (Q^T Hx)[3:] = (Hx - V diag(tau) W^T)[3:] plus Q^T r.
+// with xor-shuffle reductions (LAPACK dlarfg sign convention), and stores
+//   * in T, for gating: the compact factors of H0 = (Q^T Hx)[3:] =
+//     (Hx - V diag(tau) W^T)[3:] plus Q^T r                       (obs_ws, tau)
+//   * in fp64, for the information assembly: G_i (the observation's columns
+//     of the top 3 rows of Q^T Hx), Hx_i^T Hx_i and Hx_i^T r_i - G_i^T g  (obs_g)
+// The whole kernel computes in fp64 (CT) whatever T is: the Gram identity
+// H0^T H0 = sum_i Hx_i^T Hx_i - G^T G cancels the feature-position directions,
+// and only an fp64 projection keeps the gauge (unobservable) directions of the
+// assembled information at rounding level.
 // The nullspace basis differs from the reference's SVD basis by an orthogonal
 // transform, to which gating and the update are invariant (quirk Q4).
 // ===========================================================================
-constexpr int FEAT_OPL = 2;   // observations per lane -> M <= 128
-
 template <typename T>
 __global__ void __launch_bounds__(256) k_feature(DevState<T> st, Params<T> prm, FeatBatch<T> fb,
                                                  int f0, int nfeat) {
+    using CT = double;
     const int lane = threadIdx.x & 63;
     const int f = f0 + blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (f >= f0 + nfeat) return;
     if (!fb.valid[f]) return;
     const int b = fb.feat_filter[f];
     const int o0 = fb.obs_off[f], M = fb.obs_off[f + 1] - o0;
+    const bool own = lane < M;
     const T* cams = st.cams + (size_t)b * st.Nmax * CAM_STRIDE;
-    const T* g = st.imu + (size_t)b * IMU_STRIDE + I_G;
-    const T pw[3] = {fb.p_w[3 * f], fb.p_w[3 * f + 1], fb.p_w[3 * f + 2]};
-    T Hx[FEAT_OPL][24], Hf[FEAT_OPL][12], r[FEAT_OPL][4];
-#pragma unroll
-    for (int s = 0; s < FEAT_OPL; ++s) {
-        const int i = lane + 64 * s;
-        for (int e = 0; e < 24; ++e) Hx[s][e] = 0;
-        for (int e = 0; e < 12; ++e) Hf[s][e] = 0;
-        for (int e = 0; e < 4; ++e) r[s][e] = 0;
-        if (i >= M) continue;
-        const T* c = cams + (size_t)fb.obs_cam[o0 + i] * CAM_STRIDE;
-        const T* z = fb.obs_z + (size_t)(o0 + i) * 4;
-        T R0[9], R1[9], t1[3], tmp[3];
-        quat_to_rot(c + C_Q, R0);
-        mat3_mul(prm.R01, R0, R1);
-        mat3T_vec(R1, prm.t01, tmp);
-        for (int k = 0; k < 3; ++k) t1[k] = c[C_P + k] - tmp[k];
-        T d0[3], d1[3], pc0[3], pc1[3];
-        for (int k = 0; k < 3; ++k) { d0[k] = pw[k] - c[C_P + k]; d1[k] = pw[k] - t1[k]; }
+    CT g[3], R01[9], t01[3];
+    for (int k = 0; k < 3; ++k) {
+        g[k] = (CT)st.imu[(size_t)b * IMU_STRIDE + I_G + k];
+        t01[k] = (CT)prm.t01[k];
+    }
+    for (int k = 0; k < 9; ++k) R01[k] = (CT)prm.R01[k];
+    const CT pw[3] = {(CT)fb.p_w[3 * f], (CT)fb.p_w[3 * f + 1], (CT)fb.p_w[3 * f + 2]};
+    CT Hx[24], Hf[12], r[4], u6[6];
+    for (int e = 0; e < 24; ++e) Hx[e] = 0;
+    for (int e = 0; e < 12; ++e) Hf[e] = 0;
+    for (int e = 0; e < 4; ++e) r[e] = 0;
+    if (own) {
+        const T* c = cams + (size_t)fb.obs_cam[o0 + lane] * CAM_STRIDE;
+        const T* z = fb.obs_z + (size_t)(o0 + lane) * 4;
+        CT q0[4], qn[4], cp[3];
+        for (int k = 0; k < 4; ++k) { q0[k] = (CT)c[C_Q + k]; qn[k] = (CT)c[C_QN + k]; }
+        for (int k = 0; k < 3; ++k) cp[k] = (CT)c[C_P + k];
+        CT R0[9], R1[9], t1[3], tmp[3];
+        quat_to_rot(q0, R0);
+        mat3_mul(R01, R0, R1);
+        mat3T_vec(R1, t01, tmp);
+        for (int k = 0; k < 3; ++k) t1[k] = cp[k] - tmp[k];
+        CT d0[3], d1[3], pc0[3], pc1[3];
+        for (int k = 0; k < 3; ++k) { d0[k] = pw[k] - cp[k]; d1[k] = pw[k] - t1[k]; }
         mat3_vec(R0, d0, pc0);
         mat3_vec(R1, d1, pc1);
         // dz/dpc (msckf.py:457-467)
-        T a00 = 1 / pc0[2], a02 = -pc0[0] / (pc0[2] * pc0[2]), a12 = -pc0[1] / (pc0[2] * pc0[2]);
-        T b00 = 1 / pc1[2], b02 = -pc1[0] / (pc1[2] * pc1[2]), b12 = -pc1[1] / (pc1[2] * pc1[2]);
+        CT a00 = 1 / pc0[2], a02 = -pc0[0] / (pc0[2] * pc0[2]), a12 = -pc0[1] / (pc0[2] * pc0[2]);
+        CT b00 = 1 / pc1[2], b02 = -pc1[0] / (pc1[2] * pc1[2]), b12 = -pc1[1] / (pc1[2] * pc1[2]);
         // dpc/dxc (msckf.py:469-475): [skew(pc0) | -R0], [R01 skew(pc0) | -R1]
-        T Sk[9], RS[9];
+        CT Sk[9], RS[9];
         skew3(pc0, Sk);
-        mat3_mul(prm.R01, Sk, RS);
-        T D0[18], D1[18];
+        mat3_mul(R01, Sk, RS);
+        CT D0[18], D1[18];
         for (int k = 0; k < 3; ++k)
             for (int l = 0; l < 3; ++l) {
                 D0[6 * k + l] = Sk[3 * k + l];
@@ -677,7 +690,7 @@ __global__ void __launch_bounds__(256) k_feature(DevState<T> st, Params<T> prm, 
                 D1[6 * k + l] = RS[3 * k + l];
                 D1[6 * k + 3 + l] = -R1[3 * k + l];
             }
-        T H[24];
+        CT H[24];
         for (int l = 0; l < 6; ++l) {
             H[l] = a00 * D0[l] + a02 * D0[12 + l];
             H[6 + l] = a00 * D0[6 + l] + a12 * D0[12 + l];
@@ -685,109 +698,113 @@ __global__ void __launch_bounds__(256) k_feature(DevState<T> st, Params<T> prm, 
             H[18 + l] = b00 * D1[6 + l] + b12 * D1[12 + l];
         }
         // observability constraint (msckf.py:484-490)
-        T u[6], Rn[9], dp[3];
-        quat_to_rot(c + C_QN, Rn);
+        CT u[6], Rn[9], dp[3];
+        quat_to_rot(qn, Rn);
         mat3_vec(Rn, g, u);
-        for (int k = 0; k < 3; ++k) dp[k] = pw[k] - c[C_P + k];
+        for (int k = 0; k < 3; ++k) dp[k] = pw[k] - cp[k];
         skew3(dp, Sk);
         mat3_vec(Sk, g, u + 3);
-        T uu = 0;
+        CT uu = 0;
         for (int k = 0; k < 6; ++k) uu += u[k] * u[k];
         for (int a = 0; a < 4; ++a) {
-            T au = 0;
+            CT au = 0;
             for (int k = 0; k < 6; ++k) au += H[6 * a + k] * u[k];
-            for (int k = 0; k < 6; ++k) Hx[s][6 * a + k] = H[6 * a + k] - au * u[k] / uu;
-            for (int k = 0; k < 3; ++k) Hf[s][3 * a + k] = -Hx[s][6 * a + 3 + k];
+            for (int k = 0; k < 6; ++k) Hx[6 * a + k] = H[6 * a + k] - au * u[k] / uu;
+            for (int k = 0; k < 3; ++k) Hf[3 * a + k] = -Hx[6 * a + 3 + k];
         }
-        r[s][0] = z[0] - pc0[0] / pc0[2];
-        r[s][1] = z[1] - pc0[1] / pc0[2];
-        r[s][2] = z[2] - pc1[0] / pc1[2];
-        r[s][3] = z[3] - pc1[1] / pc1[2];
+        r[0] = (CT)z[0] - pc0[0] / pc0[2];
+        r[1] = (CT)z[1] - pc0[1] / pc0[2];
+        r[2] = (CT)z[2] - pc1[0] / pc1[2];
+        r[3] = (CT)z[3] - pc1[1] / pc1[2];
     }
+    for (int c = 0; c < 6; ++c)   // Hx_i^T r_i, before r is reflected
+        u6[c] = Hx[c] * r[0] + Hx[6 + c] * r[1] + Hx[12 + c] * r[2] + Hx[18 + c] * r[3];
     // ---- Householder QR of H_f across the wave (rows 4i..4i+3 in lane i) ----
-    T V[FEAT_OPL][12];
-    T tau[3];
-#pragma unroll
-    for (int s = 0; s < FEAT_OPL; ++s)
-        for (int e = 0; e < 12; ++e) V[s][e] = 0;
+    CT V[12];
+    CT tau[3];
+    for (int e = 0; e < 12; ++e) V[e] = 0;
     for (int j = 0; j < 3; ++j) {
-        T alpha = __shfl(Hf[0][3 * j + j], 0, 64);   // pivot row j lives in lane 0
-        T xs = 0;
-#pragma unroll
-        for (int s = 0; s < FEAT_OPL; ++s)
-            for (int a = 0; a < 4; ++a) {
-                int row = 4 * (lane + 64 * s) + a;
-                if (row > j && lane + 64 * s < M) xs += Hf[s][3 * a + j] * Hf[s][3 * a + j];
-            }
+        CT alpha = __shfl(Hf[3 * j + j], 0, 64);   // pivot row j lives in lane 0
+        CT xs = 0;
+        for (int a = 0; a < 4; ++a) {
+            int row = 4 * lane + a;
+            if (row > j && own) xs += Hf[3 * a + j] * Hf[3 * a + j];
+        }
         xs = wave_sum(xs);
-        T tj = 0, scale = 0, beta = alpha;
-        if (xs != T(0)) {
-            T nrm = sqrt(alpha * alpha + xs);
+        CT tj = 0, scale = 0, beta = alpha;
+        if (xs != CT(0)) {
+            CT nrm = sqrt(alpha * alpha + xs);
             beta = alpha >= 0 ? -nrm : nrm;
             tj = (beta - alpha) / beta;
-            scale = T(1) / (alpha - beta);
+            scale = CT(1) / (alpha - beta);
         }
         tau[j] = tj;
         // v_j: v[j] = 1, v[row > j] = Hf[row][j] * scale, 0 above
-#pragma unroll
-        for (int s = 0; s < FEAT_OPL; ++s)
-            for (int a = 0; a < 4; ++a) {
-                int row = 4 * (lane + 64 * s) + a;
-                T v = 0;
-                if (lane + 64 * s < M) v = row == j ? T(1) : (row > j ? Hf[s][3 * a + j] * scale : T(0));
-                V[s][3 * a + j] = v;
-            }
+        for (int a = 0; a < 4; ++a) {
+            int row = 4 * lane + a;
+            CT v = 0;
+            if (own) v = row == j ? CT(1) : (row > j ? Hf[3 * a + j] * scale : CT(0));
+            V[3 * a + j] = v;
+        }
         // apply H_j to the remaining H_f columns and to r
         for (int c = j + 1; c <= 3; ++c) {
-            T w = 0;
-#pragma unroll
-            for (int s = 0; s < FEAT_OPL; ++s)
-                for (int a = 0; a < 4; ++a) w += V[s][3 * a + j] * (c < 3 ? Hf[s][3 * a + c] : r[s][a]);
+            CT w = 0;
+            for (int a = 0; a < 4; ++a) w += V[3 * a + j] * (c < 3 ? Hf[3 * a + c] : r[a]);
             w = wave_sum(w);
-#pragma unroll
-            for (int s = 0; s < FEAT_OPL; ++s)
-                for (int a = 0; a < 4; ++a) {
-                    if (c < 3) Hf[s][3 * a + c] -= tj * V[s][3 * a + j] * w;
-                    else r[s][a] -= tj * V[s][3 * a + j] * w;
-                }
+            for (int a = 0; a < 4; ++a) {
+                if (c < 3) Hf[3 * a + c] -= tj * V[3 * a + j] * w;
+                else r[a] -= tj * V[3 * a + j] * w;
+            }
         }
     }
     // ---- w_j = v_j^T X_{j-1}: 6 columns per observation, local to the lane ----
-    T d10 = 0, d20 = 0, d21 = 0;
-#pragma unroll
-    for (int s = 0; s < FEAT_OPL; ++s)
-        for (int a = 0; a < 4; ++a) {
-            d10 += V[s][3 * a + 1] * V[s][3 * a];
-            d20 += V[s][3 * a + 2] * V[s][3 * a];
-            d21 += V[s][3 * a + 2] * V[s][3 * a + 1];
-        }
+    CT d10 = 0, d20 = 0, d21 = 0;
+    for (int a = 0; a < 4; ++a) {
+        d10 += V[3 * a + 1] * V[3 * a];
+        d20 += V[3 * a + 2] * V[3 * a];
+        d21 += V[3 * a + 2] * V[3 * a + 1];
+    }
     d10 = wave_sum(d10);
     d20 = wave_sum(d20);
     d21 = wave_sum(d21);
-#pragma unroll
-    for (int s = 0; s < FEAT_OPL; ++s) {
-        const int i = lane + 64 * s;
-        if (i >= M) continue;
-        T W[18];
-        for (int c = 0; c < 6; ++c) {
-            T w0 = 0, w1 = 0, w2 = 0;
-            for (int a = 0; a < 4; ++a) {
-                w0 += V[s][3 * a] * Hx[s][6 * a + c];
-                w1 += V[s][3 * a + 1] * Hx[s][6 * a + c];
-                w2 += V[s][3 * a + 2] * Hx[s][6 * a + c];
-            }
-            w1 -= tau[0] * d10 * w0;
-            w2 -= tau[0] * d20 * w0 + tau[1] * d21 * w1;
-            W[c] = w0; W[6 + c] = w1; W[12 + c] = w2;
+    // top 3 rows of V (all in lane 0) and g = (Q^T r)[0:3], broadcast
+    CT V0[9], gr[3];
+    for (int e = 0; e < 9; ++e) V0[e] = lane_bcast(V[e], 0);
+    for (int t = 0; t < 3; ++t) gr[t] = lane_bcast(r[t], 0);
+    if (!own) return;
+    CT W[18];
+    for (int c = 0; c < 6; ++c) {
+        CT w0 = 0, w1 = 0, w2 = 0;
+        for (int a = 0; a < 4; ++a) {
+            w0 += V[3 * a] * Hx[6 * a + c];
+            w1 += V[3 * a + 1] * Hx[6 * a + c];
+            w2 += V[3 * a + 2] * Hx[6 * a + c];
         }
-        T* ws = fb.obs_ws + (size_t)(o0 + i) * OBS_WS;
-        for (int e = 0; e < 24; ++e) ws[OBS_HX + e] = Hx[s][e];
-        for (int e = 0; e < 12; ++e) ws[OBS_V + e] = V[s][e];
-        for (int e = 0; e < 18; ++e) ws[OBS_W + e] = W[e];
-        for (int e = 0; e < 4; ++e) ws[OBS_QR + e] = r[s][e];
+        w1 -= tau[0] * d10 * w0;
+        w2 -= tau[0] * d20 * w0 + tau[1] * d21 * w1;
+        W[c] = w0; W[6 + c] = w1; W[12 + c] = w2;
     }
+    T* ws = fb.obs_ws + (size_t)(o0 + lane) * OBS_WS;
+    for (int e = 0; e < 24; ++e) ws[OBS_HX + e] = (T)Hx[e];
+    for (int e = 0; e < 12; ++e) ws[OBS_V + e] = (T)V[e];
+    for (int e = 0; e < 18; ++e) ws[OBS_W + e] = (T)W[e];
+    for (int e = 0; e < 4; ++e) ws[OBS_QR + e] = (T)r[e];
     if (lane == 0)
-        for (int j = 0; j < 3; ++j) fb.tau[4 * f + j] = tau[j];
+        for (int j = 0; j < 3; ++j) fb.tau[4 * f + j] = (T)tau[j];
+    // Gram terms.  (Q^T Hx)[t][i-block] = [i == 0] Hx_0[t] - sum_j tau_j V_0[t][j] W_j(i)
+    double* og = fb.obs_g + (size_t)(o0 + lane) * OBG_STRIDE;
+    CT G[18];
+    for (int t = 0; t < 3; ++t)
+        for (int c = 0; c < 6; ++c) {
+            CT v = lane == 0 ? Hx[6 * t + c] : CT(0);
+            for (int j = 0; j < 3; ++j) v -= tau[j] * V0[3 * t + j] * W[6 * j + c];
+            G[6 * t + c] = v;
+            og[OBG_G + 6 * t + c] = v;
+        }
+    for (int x = 0, e = 0; x < 6; ++x)
+        for (int y = 0; y <= x; ++y, ++e)
+            og[OBG_DS + e] = Hx[x] * Hx[y] + Hx[6 + x] * Hx[6 + y] + Hx[12 + x] * Hx[12 + y] + Hx[18 + x] * Hx[18 + y];
+    for (int c = 0; c < 6; ++c) og[OBG_UB + c] = u6[c] - (G[c] * gr[0] + G[6 + c] * gr[1] + G[12 + c] * gr[2]);
 }
 
 // Dense row `row` (0 <= row < 4M) of Q^T Hx for observation column block i.
@@ -1078,775 +1095,226 @@ __global__ void k_select(DevState<T> st, FeatBatch<T> fb, UpdWs<T> ws, int row_c
 }
 
 // ===========================================================================
-// Stacked-H assembly / QR compression (msckf.py:549-556): one workgroup per
-// filter.  When R > C the included features' rows are merged, chunk by chunk,
-// into the running triangular factor [R | Q^T r] with one Householder
-// reflector per column (a sequential TSQR; any orthogonal row transform of
-// (H, r) leaves the update unchanged -- quirk Q4); when R <= C the stacked rows
-// are copied out as H_thin, as the reference does.
-// Register-resident merge (the production path of the QR compression).
-// Thread t owns columns j = t + 256u (u < COLS) of [R | Q^T r]; the CH rows of
-// the current chunk of the feature's projected block live in its registers
-// (b[u][0..CH)), generated directly from the compact factors (Hx, V, tau, W)
-// without an LDS tile.  Per column c one barrier: every owner of a column
-// j > c applies the reflector (v broadcast from LDS), and the owner of column
-// c+1 forms the next reflector from its registers (look-ahead).  R lives in
-// LDS when it fits, else in global memory with R[c+1][j] prefetched one step
-// ahead (row c+1 is not touched by step c).
-template <typename T, int CH, int COLS, bool R_LDS>
-__global__ void __launch_bounds__(256) k_compress_reg(DevState<T> st, FeatBatch<T> fb, UpdWs<T> ws) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    const int b = blockIdx.x;
-    const int tid = threadIdx.x;
-    const int* info = ws.info + 4 * b;
-    const int Rn = info[0], n = info[1], compress = info[2];
-    if (Rn == 0) return;
-    const int C = 6 * st.ncams[b];
-    const int ldh = ws.Cmax + 1;
-    T* H = ws.Hthin + (size_t)b * ws.Cmax * ldh;
-    const int ldr = R_LDS ? (C + 1) : ldh;
-    T* s_v = reinterpret_cast<T*>(smem_raw);                  // [2][CH]
-    T* s_sc = s_v + 2 * CH;                                   // tau[2] | tau_f[3]
-    T* s_V = s_sc + 8;                                        // [CH][4] chunk rows of V, [..][3] = Qr
-    int* s_obs = reinterpret_cast<int*>(s_V + 4 * CH);        // [Nmax] obs index of each cam slot
-    T* Rm = R_LDS ? reinterpret_cast<T*>(s_obs + ((st.Nmax + 3) & ~3)) : H;   // [C][ldr]
-    auto Ridx = [&](int r, int c) -> T& { return Rm[(size_t)r * ldr + (R_LDS ? c : (c == C ? ws.Cmax : c))]; };
-    if (compress)
-        for (int e = tid; e < C * (C + 1); e += blockDim.x) Ridx(e / (C + 1), e % (C + 1)) = 0;
-    else
-        for (int e = tid; e < n * ldh; e += blockDim.x) H[e] = 0;
-    for (int f = fb.feat_off[b]; f < fb.feat_off[b + 1]; ++f) {
-        if (!fb.include[f]) continue;
-        const int o0 = fb.obs_off[f], M = fb.obs_off[f + 1] - o0;
-        const T* wsf = fb.obs_ws + (size_t)o0 * OBS_WS;
-        __syncthreads();
-        for (int i = tid; i < st.Nmax; i += blockDim.x) s_obs[i] = -1;
-        if (tid < 3) s_sc[2 + tid] = fb.tau[4 * f + tid];
-        __syncthreads();
-        int smin = 1 << 30;
-        for (int i = 0; i < M; ++i) smin = min(smin, fb.obs_cam[o0 + i]);
-        for (int i = tid; i < M; i += blockDim.x) s_obs[fb.obs_cam[o0 + i]] = i;
-        __syncthreads();
-        const T t0 = s_sc[2], t1 = s_sc[3], t2 = s_sc[4];
-        // per owned column: its observation (if any), its W entries, its Hx rows
-        int oi[COLS];
-        T w0[COLS], w1[COLS], w2[COLS], hx[COLS][4];
-#pragma unroll
-        for (int u = 0; u < COLS; ++u) {
-            const int j = tid + 256 * u;
-            oi[u] = (j < C) ? s_obs[j / 6] : -1;
-            w0[u] = w1[u] = w2[u] = 0;
-            hx[u][0] = hx[u][1] = hx[u][2] = hx[u][3] = 0;
-            if (oi[u] >= 0) {
-                const T* wo = wsf + (size_t)oi[u] * OBS_WS;
-                const int c = j % 6;
-                w0[u] = t0 * wo[OBS_W + c];
-                w1[u] = t1 * wo[OBS_W + 6 + c];
-                w2[u] = t2 * wo[OBS_W + 12 + c];
-#pragma unroll
-                for (int a = 0; a < 4; ++a) hx[u][a] = wo[OBS_HX + 6 * a + c];
-            }
-        }
-        const int c0 = 6 * smin;
-        const int n4 = 4 * M;
-        for (int a0 = 3; a0 < n4; a0 += CH) {
-            const int nr = min(CH, n4 - a0);
-            __syncthreads();
-            for (int rr = tid; rr < CH; rr += blockDim.x) {
-                const int row = a0 + rr;
-                if (rr < nr) {
-                    const T* wr = wsf + (size_t)(row >> 2) * OBS_WS;
-                    s_V[4 * rr + 0] = wr[OBS_V + 3 * (row & 3) + 0];
-                    s_V[4 * rr + 1] = wr[OBS_V + 3 * (row & 3) + 1];
-                    s_V[4 * rr + 2] = wr[OBS_V + 3 * (row & 3) + 2];
-                    s_V[4 * rr + 3] = wr[OBS_QR + (row & 3)];
-                } else {
-                    s_V[4 * rr + 0] = s_V[4 * rr + 1] = s_V[4 * rr + 2] = s_V[4 * rr + 3] = 0;
-                }
-            }
-            __syncthreads();
-            T bv[COLS][CH];
-#pragma unroll
-            for (int u = 0; u < COLS; ++u) {
-                const int j = tid + 256 * u;
-#pragma unroll
-                for (int rr = 0; rr < CH; ++rr) {
-                    const int row = a0 + rr;
-                    T x = 0;
-                    if (j == C) {
-                        x = s_V[4 * rr + 3];
-                    } else if (oi[u] >= 0) {
-                        const T h = ((row >> 2) == oi[u]) ? hx[u][row & 3] : T(0);
-                        x = h - (s_V[4 * rr] * w0[u] + s_V[4 * rr + 1] * w1[u] + s_V[4 * rr + 2] * w2[u]);
-                        if (rr >= nr) x = 0;
-                    }
-                    bv[u][rr] = x;
-                }
-            }
-            if (!compress) {   // R <= C: the stacked rows are H_thin (msckf.py:554-556)
-                const int base = fb.row_off[f] + (a0 - 3);
-#pragma unroll
-                for (int u = 0; u < COLS; ++u) {
-                    const int j = tid + 256 * u;
-                    if (j > C) continue;
-                    const int col = (j == C) ? ws.Cmax : j;
-#pragma unroll
-                    for (int rr = 0; rr < CH; ++rr)
-                        if (rr < nr) H[(size_t)(base + rr) * ldh + col] = bv[u][rr];
-                }
-                continue;
-            }
-            // R[j][j] of every owned column: only column j's own reflector touches
-            // it, so it is read once per chunk (no global latency per column)
-            T rdiag[COLS];
-#pragma unroll
-            for (int u = 0; u < COLS; ++u) {
-                const int j = tid + 256 * u;
-                rdiag[u] = (j >= c0 && j < C) ? Ridx(j, j) : T(0);
-            }
-            // reflector of column c from (R[c][c], bv[u]) by the owner of column c
-            auto reflector = [&](int c, int u, int buf) {
-                T p0 = 0, p1 = 0, p2 = 0, p3 = 0;
-#pragma unroll
-                for (int rr = 0; rr < CH; rr += 4) {
-                    p0 += bv[u][rr] * bv[u][rr];
-                    p1 += bv[u][rr + 1] * bv[u][rr + 1];
-                    p2 += bv[u][rr + 2] * bv[u][rr + 2];
-                    p3 += bv[u][rr + 3] * bv[u][rr + 3];
-                }
-                const T xs = (p0 + p1) + (p2 + p3);
-                const T alpha = rdiag[u];
-                T tj = 0, scale = 0, beta = alpha;
-                if (xs != T(0)) {
-                    T nrm = sqrt(alpha * alpha + xs);
-                    beta = alpha >= 0 ? -nrm : nrm;
-                    tj = (beta - alpha) / beta;
-                    scale = T(1) / (alpha - beta);
-                }
-#pragma unroll
-                for (int rr = 0; rr < CH; ++rr) s_v[buf * CH + rr] = bv[u][rr] * scale;
-                s_sc[buf] = tj;
-                rdiag[u] = beta;
-                Ridx(c, c) = beta;
-            };
-#pragma unroll
-            for (int u = 0; u < COLS; ++u)
-                if (tid + 256 * u == c0) reflector(c0, u, 0);
-            T rnext[COLS];
-#pragma unroll
-            for (int u = 0; u < COLS; ++u) {
-                const int j = tid + 256 * u;
-                rnext[u] = (j <= C && j > c0) ? Ridx(c0, j) : T(0);
-            }
-            LDS_BARRIER();
-            for (int c = c0; c < C; ++c) {
-                const int buf = (c - c0) & 1;
-                const T tj = s_sc[buf];
-                T v[CH];
-#pragma unroll
-                for (int rr = 0; rr < CH; ++rr) v[rr] = s_v[buf * CH + rr];
-#pragma unroll
-                for (int u = 0; u < COLS; ++u) {
-                    const int j = tid + 256 * u;
-                    const T rcur = rnext[u];
-                    if (j > c + 1 && j <= C) rnext[u] = Ridx(c + 1, j);   // prefetch next row
-                    if (j > c && j <= C && tj != T(0)) {
-                        T q0 = rcur, q1 = 0, q2 = 0, q3 = 0;
-#pragma unroll
-                        for (int rr = 0; rr < CH; rr += 4) {
-                            q0 += v[rr] * bv[u][rr];
-                            q1 += v[rr + 1] * bv[u][rr + 1];
-                            q2 += v[rr + 2] * bv[u][rr + 2];
-                            q3 += v[rr + 3] * bv[u][rr + 3];
-                        }
-                        const T w = (q0 + q1) + (q2 + q3);
-                        const T tw = tj * w;
-                        Ridx(c, j) = rcur - tw;
-#pragma unroll
-                        for (int rr = 0; rr < CH; ++rr) bv[u][rr] -= v[rr] * tw;
-                    }
-                    if (j == c + 1 && j < C) reflector(j, u, buf ^ 1);
-                }
-                LDS_BARRIER();   // R prefetches / stores stay in flight
-            }
-        }
-    }
-    if (R_LDS && compress) {
-        __syncthreads();
-        for (int e = tid; e < C * (C + 1); e += blockDim.x) {
-            const int r = e / (C + 1), c = e % (C + 1);
-            H[(size_t)r * ldh + (c == C ? ws.Cmax : c)] = Rm[e];
-        }
-    }
-}
+// Information assembly + factorisation (replaces the QR compression of
+// msckf.py:549-556).  The update msckf.py:559-604 depends on the stacked
+// (H, r) only through A = H^T H and b = H^T r:
+//   K r = P H^T (H P H^T + s2 I)^-1 r = P (A P + s2 I)^-1 b,
+//   K H P = P (A P + s2 I)^-1 A P,
+// so any F, r_F with F^T F = A and F^T r_F = b gives the reference's update --
+// the QR's [R | Q^T r] is one such pair, the pivoted Cholesky factor of the
+// augmented Gram matrix [A b] is another.  Per feature the projected block's
+// Gram matrix is assembled from the fp64 terms of k_feature:
+//   H0^T H0 = blockdiag_i(Hx_i^T Hx_i) - G^T G,   H0^T r0 = sum_i UB_i,
+// which needs O(M^2) work per feature and never materialises the stacked
+// rows (the QR merge streamed its C x C factor through memory once per
+// 16-row chunk: ~160 GB per 2048-filter launch, profiles/r01/README.md).
+//
+// One workgroup per filter.  Thread t owns 6x6 cam-pair blocks (I >= J) of A
+// in registers (block index t + NT m, m < BPT); features are staged FB at a
+// time in LDS, indexed by cam, with a cam bitmask per feature, and each
+// thread accumulates the blocks whose two cams the feature observes.  Then an
+// outer-product Cholesky with diagonal pivoting runs on the register blocks:
+// per step the diagonal owners publish their diagonal, wave 0 picks the
+// pivot, the owners of the pivot's row publish it scaled (the row of F), and
+// every block takes the rank-1 downdate.  It stops at the numerical rank
+// (pivot <= tol_rel * max diag(A)): the 4 gauge directions that the
+// observability-constrained Jacobians leave unobservable (eigenvalues
+// ~1e-17 |A| against >= 1e-6 |A| for the observable ones on the bench
+// problems) carry no information and produce no row.
+// Output: rows 0..n-1 of [F | r_F] in H_thin (KT), n = rank in info[1].
+// ===========================================================================
+constexpr int INFO_FB = 4;    // features staged per round
+constexpr int INFO_RS = 50;   // LDS doubles per (feature, cam) record (48 + pad)
 
-// Panel-blocked register merge (production path when C+1 <= 256).
-// Columns are processed in 16-wide panels aligned to 16.  The wave that owns a
-// panel factors it alone (reflector of column q formed by lane q from its
-// registers, broadcast to the wave through LDS with a wave-local wait only);
-// its lanes apply each reflector to their own columns on the spot.  One
-// workgroup barrier per panel publishes the panel's 16 reflectors; every other
-// wave then applies them to its columns from registers.  The 16 R rows of a
-// panel are prefetched one whole panel ahead (rows of panel P+1 are not
-// touched by panel P), so no global latency sits on the per-column path.
-template <typename T, int CH>
-__global__ void __launch_bounds__(256) k_compress_panel(DevState<T> st, FeatBatch<T> fb, UpdWs<T> ws) {
-    constexpr int NB = 16;
+template <typename T, int BPT, int NT>
+__global__ void __launch_bounds__(NT) k_info(DevState<T> st, FeatBatch<T> fb, UpdWs<T> ws, double tol_rel) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int b = blockIdx.x;
-    const int tid = threadIdx.x, wave = tid >> 6;
-    const int* info = ws.info + 4 * b;
-    const int Rn = info[0], n = info[1], compress = info[2];
-    if (Rn == 0) return;
-    const int C = 6 * st.ncams[b];
-    const int ldh = ws.Cmax + 1;
-    T* H = ws.Hthin + (size_t)b * ws.Cmax * ldh;
-    T* s_Vp = reinterpret_cast<T*>(smem_raw);       // [2][NB][CH] panel reflectors
-    T* s_tp = s_Vp + 2 * NB * CH;                   // [2][NB]
-    T* s_sc = s_tp + 2 * NB;                        // tau_f[3] (+pad)
-    T* s_V = s_sc + 4;                              // [CH][4] chunk rows of V | Qr
-    int* s_obs = reinterpret_cast<int*>(s_V + 4 * CH);
-    const int j = tid;                              // the one column this thread owns
-    const bool mine = j <= C;
-    const int hcol = (j == C) ? ws.Cmax : j;
-    if (compress)
-        for (int e = tid; e < C * (C + 1); e += blockDim.x) {
-            const int r = e / (C + 1), c = e % (C + 1);
-            H[(size_t)r * ldh + (c == C ? ws.Cmax : c)] = 0;
-        }
-    else
-        for (int e = tid; e < n * ldh; e += blockDim.x) H[e] = 0;
-    for (int f = fb.feat_off[b]; f < fb.feat_off[b + 1]; ++f) {
-        if (!fb.include[f]) continue;
-        const int o0 = fb.obs_off[f], M = fb.obs_off[f + 1] - o0;
-        const T* wsf = fb.obs_ws + (size_t)o0 * OBS_WS;
-        __syncthreads();
-        for (int i = tid; i < st.Nmax; i += blockDim.x) s_obs[i] = -1;
-        if (tid < 3) s_sc[tid] = fb.tau[4 * f + tid];
-        __syncthreads();
-        int smin = 1 << 30;
-        for (int i = 0; i < M; ++i) smin = min(smin, fb.obs_cam[o0 + i]);
-        for (int i = tid; i < M; i += blockDim.x) s_obs[fb.obs_cam[o0 + i]] = i;
-        __syncthreads();
-        const T t0 = s_sc[0], t1 = s_sc[1], t2 = s_sc[2];
-        const int oi = (j < C) ? s_obs[j / 6] : -1;
-        T w0 = 0, w1 = 0, w2 = 0, hx[4] = {0, 0, 0, 0};
-        if (oi >= 0) {
-            const T* wo = wsf + (size_t)oi * OBS_WS;
-            const int c = j % 6;
-            w0 = t0 * wo[OBS_W + c];
-            w1 = t1 * wo[OBS_W + 6 + c];
-            w2 = t2 * wo[OBS_W + 12 + c];
-#pragma unroll
-            for (int a = 0; a < 4; ++a) hx[a] = wo[OBS_HX + 6 * a + c];
-        }
-        const int c0 = 6 * smin;
-        const int n4 = 4 * M;
-        for (int a0 = 3; a0 < n4; a0 += CH) {
-            const int nr = min(CH, n4 - a0);
-            __syncthreads();
-            for (int rr = tid; rr < CH; rr += blockDim.x) {
-                const int row = a0 + rr;
-                if (rr < nr) {
-                    const T* wr = wsf + (size_t)(row >> 2) * OBS_WS;
-                    s_V[4 * rr + 0] = wr[OBS_V + 3 * (row & 3) + 0];
-                    s_V[4 * rr + 1] = wr[OBS_V + 3 * (row & 3) + 1];
-                    s_V[4 * rr + 2] = wr[OBS_V + 3 * (row & 3) + 2];
-                    s_V[4 * rr + 3] = wr[OBS_QR + (row & 3)];
-                } else {
-                    s_V[4 * rr + 0] = s_V[4 * rr + 1] = s_V[4 * rr + 2] = s_V[4 * rr + 3] = 0;
-                }
-            }
-            __syncthreads();
-            T bv[CH];
-#pragma unroll
-            for (int rr = 0; rr < CH; ++rr) {
-                const int row = a0 + rr;
-                T x = 0;
-                if (j == C) {
-                    x = s_V[4 * rr + 3];
-                } else if (oi >= 0) {
-                    const T h = ((row >> 2) == oi) ? hx[row & 3] : T(0);
-                    x = h - (s_V[4 * rr] * w0 + s_V[4 * rr + 1] * w1 + s_V[4 * rr + 2] * w2);
-                    if (rr >= nr) x = 0;
-                }
-                bv[rr] = x;
-            }
-            if (!compress) {   // R <= C: the stacked rows are H_thin (msckf.py:554-556)
-                const int base = fb.row_off[f] + (a0 - 3);
-                if (mine)
-#pragma unroll
-                    for (int rr = 0; rr < CH; ++rr)
-                        if (rr < nr) H[(size_t)(base + rr) * ldh + hcol] = bv[rr];
-                continue;
-            }
-            const int P0 = c0 / NB, PL = (C - 1) / NB;
-            T rr_[NB], rn[NB];
-            {
-                const int pb = c0, pe = min(NB * (P0 + 1), C);
-#pragma unroll
-                for (int t = 0; t < NB; ++t)
-                    rn[t] = (mine && pb + t < pe && j >= pb + t) ? H[(size_t)(pb + t) * ldh + hcol] : T(0);
-            }
-            for (int P = P0; P <= PL; ++P) {
-                const int pb = max(NB * P, c0), pe = min(NB * (P + 1), C), nbp = pe - pb;
-                const int buf = (P - P0) & 1;
-                T* Vb = s_Vp + buf * NB * CH;
-                T* tb = s_tp + buf * NB;
-#pragma unroll
-                for (int t = 0; t < NB; ++t) rr_[t] = rn[t];
-                if (P < PL) {   // prefetch the next panel's R rows (untouched by this panel)
-                    const int qb = NB * (P + 1), qe = min(NB * (P + 2), C);
-#pragma unroll
-                    for (int t = 0; t < NB; ++t)
-                        rn[t] = (mine && qb + t < qe && j >= qb + t) ? H[(size_t)(qb + t) * ldh + hcol] : T(0);
-                }
-                const int owner = (NB * P) >> 6;
-                if (wave == owner) {
-#pragma unroll
-                    for (int t = 0; t < NB; ++t) {
-                        if (t < nbp) {
-                            const int q = pb + t;
-                            if (j == q) {   // reflector of column q (LAPACK dlarfg convention)
-                                T p0 = 0, p1 = 0, p2 = 0, p3 = 0;
-#pragma unroll
-                                for (int r = 0; r < CH; r += 4) {
-                                    p0 += bv[r] * bv[r];
-                                    p1 += bv[r + 1] * bv[r + 1];
-                                    p2 += bv[r + 2] * bv[r + 2];
-                                    p3 += bv[r + 3] * bv[r + 3];
-                                }
-                                const T xs = (p0 + p1) + (p2 + p3);
-                                const T alpha = rr_[t];
-                                T tj = 0, scale = 0, beta = alpha;
-                                if (xs != T(0)) {
-                                    T nrm = sqrt(alpha * alpha + xs);
-                                    beta = alpha >= 0 ? -nrm : nrm;
-                                    tj = (beta - alpha) / beta;
-                                    scale = T(1) / (alpha - beta);
-                                }
-#pragma unroll
-                                for (int r = 0; r < CH; ++r) Vb[t * CH + r] = bv[r] * scale;
-                                tb[t] = tj;
-                                rr_[t] = beta;
-                            }
-                            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // wave-local publish
-                            const T tj = tb[t];
-                            if (j > q && mine && tj != T(0)) {
-                                T q0 = rr_[t], q1 = 0, q2 = 0, q3 = 0;
-#pragma unroll
-                                for (int r = 0; r < CH; r += 4) {
-                                    q0 += Vb[t * CH + r] * bv[r];
-                                    q1 += Vb[t * CH + r + 1] * bv[r + 1];
-                                    q2 += Vb[t * CH + r + 2] * bv[r + 2];
-                                    q3 += Vb[t * CH + r + 3] * bv[r + 3];
-                                }
-                                const T tw = tj * ((q0 + q1) + (q2 + q3));
-                                rr_[t] -= tw;
-#pragma unroll
-                                for (int r = 0; r < CH; ++r) bv[r] -= Vb[t * CH + r] * tw;
-                            }
-                        }
-                    }
-                }
-                LDS_BARRIER();   // publishes the panel; R prefetches stay in flight
-                if (wave != owner && mine && j >= pe) {
-#pragma unroll
-                    for (int t = 0; t < NB; ++t) {
-                        if (t < nbp) {
-                            const T tj = tb[t];
-                            if (tj != T(0)) {
-                                T q0 = rr_[t], q1 = 0, q2 = 0, q3 = 0;
-#pragma unroll
-                                for (int r = 0; r < CH; r += 4) {
-                                    q0 += Vb[t * CH + r] * bv[r];
-                                    q1 += Vb[t * CH + r + 1] * bv[r + 1];
-                                    q2 += Vb[t * CH + r + 2] * bv[r + 2];
-                                    q3 += Vb[t * CH + r + 3] * bv[r + 3];
-                                }
-                                const T tw = tj * ((q0 + q1) + (q2 + q3));
-                                rr_[t] -= tw;
-#pragma unroll
-                                for (int r = 0; r < CH; ++r) bv[r] -= Vb[t * CH + r] * tw;
-                            }
-                        }
-                    }
-                }
-#pragma unroll
-                for (int t = 0; t < NB; ++t)
-                    if (mine && t < nbp && j >= pb + t) H[(size_t)(pb + t) * ldh + hcol] = rr_[t];
-            }
-        }
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwave = NT >> 6;
+    const int nc = st.ncams[b], C = 6 * nc, Cmax = ws.Cmax, Nmax = st.Nmax;
+    int* info = ws.info + 4 * b;
+    if (info[0] == 0) {   // nothing stacked: empty update
+        if (tid == 0) info[1] = 0;
+        return;
     }
-}
+    double* rec = reinterpret_cast<double*>(smem_raw);                      // [FB][Nmax][RS]
+    double* fvec = rec + (size_t)INFO_FB * Nmax * INFO_RS;                   // [Cmax + 1]
+    double* dval = fvec + Cmax + 1;                                          // [Cmax]
+    unsigned long long* mask = reinterpret_cast<unsigned long long*>(dval + Cmax);   // [FB]
+    int* chosen = reinterpret_cast<int*>(mask + INFO_FB);                    // [Cmax]
+    __shared__ int s_p, s_stop;
+    __shared__ double s_inv, s_d0;
 
-// One wavefront per filter (the throughput path): no workgroup barriers at
-// all.  Lane l owns columns j = l + 64u (u < COLS) of [R | Q^T r] and the CH
-// chunk rows of those columns in registers.  Column c's reflector vector is
-// read out of the owner lane with v_readlane (SGPR broadcast); every lane
-// forms the same scalars (tau, scale) redundantly and updates its own
-// columns.  Latency is hidden by running several filters per SIMD.
-template <typename T, int CH, int COLS>
-__global__ void __launch_bounds__(64) k_compress_wave(DevState<T> st, FeatBatch<T> fb, UpdWs<T> ws) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    const int b = blockIdx.x;
-    const int lane = threadIdx.x;
-    const int* info = ws.info + 4 * b;
-    const int Rn = info[0], n = info[1], compress = info[2];
-    if (Rn == 0) return;
-    const int C = 6 * st.ncams[b];
-    const int ldh = ws.Cmax + 1;
-    T* H = ws.Hthin + (size_t)b * ws.Cmax * ldh;
-    T* s_V = reinterpret_cast<T*>(smem_raw);        // [CH][4] chunk rows of V | Qr
-    T* s_sc = s_V + 4 * CH;                         // tau_f[3] (+pad)
-    int* s_obs = reinterpret_cast<int*>(s_sc + 4);  // [Nmax]
-    int hcol[COLS];
+    double a[BPT][6][6], bv[BPT][6];
+    int I[BPT], J[BPT];
+    bool act[BPT];
 #pragma unroll
-    for (int u = 0; u < COLS; ++u) {
-        const int j = lane + 64 * u;
-        hcol[u] = (j == C) ? ws.Cmax : j;
-    }
-    if (compress) {
-        for (int r = 0; r < C; ++r)
+    for (int m = 0; m < BPT; ++m) {
+        const int blk = tid + NT * m;
+        int i = (int)((sqrtf(8.0f * (float)blk + 1.0f) - 1.0f) * 0.5f);
+        while (i * (i + 1) / 2 > blk) --i;
+        while ((i + 1) * (i + 2) / 2 <= blk) ++i;
+        I[m] = i;
+        J[m] = blk - i * (i + 1) / 2;
+        act[m] = i < nc;
 #pragma unroll
-            for (int u = 0; u < COLS; ++u)
-                if (lane + 64 * u <= C) H[(size_t)r * ldh + hcol[u]] = 0;
-    } else {
-        for (int e = lane; e < n * ldh; e += 64) H[e] = 0;
-    }
-    for (int f = fb.feat_off[b]; f < fb.feat_off[b + 1]; ++f) {
-        if (!fb.include[f]) continue;
-        const int o0 = fb.obs_off[f], M = fb.obs_off[f + 1] - o0;
-        const T* wsf = fb.obs_ws + (size_t)o0 * OBS_WS;
-        for (int i = lane; i < st.Nmax; i += 64) s_obs[i] = -1;
-        if (lane < 3) s_sc[lane] = fb.tau[4 * f + lane];
-        int smin = 1 << 30;
-        for (int i = 0; i < M; ++i) smin = min(smin, fb.obs_cam[o0 + i]);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        for (int i = lane; i < M; i += 64) s_obs[fb.obs_cam[o0 + i]] = i;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        const T t0 = s_sc[0], t1 = s_sc[1], t2 = s_sc[2];
-        int oi[COLS];
-        T w0[COLS], w1[COLS], w2[COLS], hx[COLS][4];
+        for (int x = 0; x < 6; ++x) {
+            bv[m][x] = 0;
 #pragma unroll
-        for (int u = 0; u < COLS; ++u) {
-            const int j = lane + 64 * u;
-            oi[u] = (j < C) ? s_obs[j / 6] : -1;
-            w0[u] = w1[u] = w2[u] = 0;
-            hx[u][0] = hx[u][1] = hx[u][2] = hx[u][3] = 0;
-            if (oi[u] >= 0) {
-                const T* wo = wsf + (size_t)oi[u] * OBS_WS;
-                const int c = j % 6;
-                w0[u] = t0 * wo[OBS_W + c];
-                w1[u] = t1 * wo[OBS_W + 6 + c];
-                w2[u] = t2 * wo[OBS_W + 12 + c];
-#pragma unroll
-                for (int a = 0; a < 4; ++a) hx[u][a] = wo[OBS_HX + 6 * a + c];
-            }
-        }
-        const int c0 = 6 * smin;
-        const int n4 = 4 * M;
-        for (int a0 = 3; a0 < n4; a0 += CH) {
-            const int nr = min(CH, n4 - a0);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            for (int rr = lane; rr < CH; rr += 64) {
-                const int row = a0 + rr;
-                if (rr < nr) {
-                    const T* wr = wsf + (size_t)(row >> 2) * OBS_WS;
-                    s_V[4 * rr + 0] = wr[OBS_V + 3 * (row & 3) + 0];
-                    s_V[4 * rr + 1] = wr[OBS_V + 3 * (row & 3) + 1];
-                    s_V[4 * rr + 2] = wr[OBS_V + 3 * (row & 3) + 2];
-                    s_V[4 * rr + 3] = wr[OBS_QR + (row & 3)];
-                } else {
-                    s_V[4 * rr + 0] = s_V[4 * rr + 1] = s_V[4 * rr + 2] = s_V[4 * rr + 3] = 0;
-                }
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            T bv[COLS][CH];
-#pragma unroll
-            for (int u = 0; u < COLS; ++u) {
-                const int j = lane + 64 * u;
-#pragma unroll
-                for (int rr = 0; rr < CH; ++rr) {
-                    const int row = a0 + rr;
-                    T x = 0;
-                    if (j == C) {
-                        x = s_V[4 * rr + 3];
-                    } else if (oi[u] >= 0) {
-                        const T h = ((row >> 2) == oi[u]) ? hx[u][row & 3] : T(0);
-                        x = h - (s_V[4 * rr] * w0[u] + s_V[4 * rr + 1] * w1[u] + s_V[4 * rr + 2] * w2[u]);
-                        if (rr >= nr) x = 0;
-                    }
-                    bv[u][rr] = x;
-                }
-            }
-            if (!compress) {   // R <= C: the stacked rows are H_thin (msckf.py:554-556)
-                const int base = fb.row_off[f] + (a0 - 3);
-#pragma unroll
-                for (int u = 0; u < COLS; ++u)
-                    if (lane + 64 * u <= C)
-#pragma unroll
-                        for (int rr = 0; rr < CH; ++rr)
-                            if (rr < nr) H[(size_t)(base + rr) * ldh + hcol[u]] = bv[u][rr];
-                continue;
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // same-address RAW on R rows
-            T rcur[COLS];
-#pragma unroll
-            for (int u = 0; u < COLS; ++u) {
-                const int j = lane + 64 * u;
-                rcur[u] = (j >= c0 && j <= C) ? H[(size_t)c0 * ldh + hcol[u]] : T(0);
-            }
-            // the sweep is split by the owner's column slot UC (compile time) so
-            // the broadcast reflector stays in SGPRs
-#pragma unroll
-            for (int UC = 0; UC < COLS; ++UC) {
-                const int cb = max(c0, 64 * UC), ce = min(C, 64 * (UC + 1));
-                for (int c = cb; c < ce; ++c) {
-                    const int lc = c & 63;
-                    T rnext[COLS];
-#pragma unroll
-                    for (int u = 0; u < COLS; ++u) {   // prefetch row c+1 (untouched by column c)
-                        const int j = lane + 64 * u;
-                        rnext[u] = (j > c && j <= C && c + 1 < C) ? H[(size_t)(c + 1) * ldh + hcol[u]] : T(0);
-                    }
-                    T v[CH];
-#pragma unroll
-                    for (int rr = 0; rr < CH; ++rr) v[rr] = lane_bcast(bv[UC][rr], lc);
-                    const T alpha = lane_bcast(rcur[UC], lc);
-                    T p0 = 0, p1 = 0, p2 = 0, p3 = 0;
-#pragma unroll
-                    for (int rr = 0; rr < CH; rr += 4) {
-                        p0 += v[rr] * v[rr];
-                        p1 += v[rr + 1] * v[rr + 1];
-                        p2 += v[rr + 2] * v[rr + 2];
-                        p3 += v[rr + 3] * v[rr + 3];
-                    }
-                    const T xs = (p0 + p1) + (p2 + p3);
-                    T tj = 0, scale = 0, beta = alpha;
-                    if (xs != T(0)) {
-                        const T nrm = sqrt(alpha * alpha + xs);
-                        beta = alpha >= 0 ? -nrm : nrm;
-                        tj = (beta - alpha) / beta;
-                        scale = T(1) / (alpha - beta);
-                    }
-                    const T ts = tj * scale;   // w = R + scale <v_raw, b> ; b -= v_raw (scale tau w)
-#pragma unroll
-                    for (int u = UC; u < COLS; ++u) {
-                        const int j = lane + 64 * u;
-                        if (j == c) {
-                            H[(size_t)c * ldh + hcol[u]] = beta;
-                        } else if (j > c && j <= C && tj != T(0)) {
-                            T q0 = 0, q1 = 0, q2 = 0, q3 = 0;
-#pragma unroll
-                            for (int rr = 0; rr < CH; rr += 4) {
-                                q0 += v[rr] * bv[u][rr];
-                                q1 += v[rr + 1] * bv[u][rr + 1];
-                                q2 += v[rr + 2] * bv[u][rr + 2];
-                                q3 += v[rr + 3] * bv[u][rr + 3];
-                            }
-                            const T w = rcur[u] + scale * ((q0 + q1) + (q2 + q3));
-                            H[(size_t)c * ldh + hcol[u]] = rcur[u] - tj * w;
-                            const T f2 = ts * w;
-#pragma unroll
-                            for (int rr = 0; rr < CH; ++rr) bv[u][rr] -= v[rr] * f2;
-                        }
-                        rcur[u] = rnext[u];
-                    }
-                }
-            }
+            for (int y = 0; y < 6; ++y) a[m][x][y] = 0;
         }
     }
-}
+    for (int i = tid; i < Cmax; i += NT) chosen[i] = 0;
 
-// Lean one-wavefront-per-filter merge (default throughput path, C+1 <= 192).
-// Same algorithm as k_compress_wave with less live state: the generation
-// temporaries die before the sweep, the column loop is unrolled by two with a
-// two-rows-ahead R prefetch ring, and fp32 uses v_sqrt / v_rcp.
-template <typename T, int CH>
-__global__ void __launch_bounds__(64) k_compress_w(DevState<T> st, FeatBatch<T> fb, UpdWs<T> ws) {
-    constexpr int COLS = 3;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    const int b = blockIdx.x;
-    const int lane = threadIdx.x;
-    const int* info = ws.info + 4 * b;
-    const int Rn = info[0], n = info[1], compress = info[2];
-    if (Rn == 0) return;
-    const int C = 6 * st.ncams[b];
-    const int ldh = ws.Cmax + 1;
-    T* H = ws.Hthin + (size_t)b * ws.Cmax * ldh;
-    T* s_V = reinterpret_cast<T*>(smem_raw);        // [CH][4] chunk rows of V | Qr
-    T* s_sc = s_V + 4 * CH;                         // tau_f[3] (+pad)
-    int* s_obs = reinterpret_cast<int*>(s_sc + 4);  // [Nmax]
-    int hcol[COLS];
+    // ---- assembly ----
+    const int fbeg = fb.feat_off[b], fend = fb.feat_off[b + 1];
+    for (int f0 = fbeg; f0 < fend; f0 += INFO_FB) {
+        for (int s = wave; s < INFO_FB; s += nwave) {
+            const int f = f0 + s;
+            unsigned long long mk = 0;
+            if (f < fend && fb.include[f]) {
+                const int o0 = fb.obs_off[f], M = fb.obs_off[f + 1] - o0;
+                if (lane < M) mk = 1ull << fb.obs_cam[o0 + lane];
+                const double* src = fb.obs_g + (size_t)o0 * OBG_STRIDE;
+                double* dst = rec + (size_t)s * Nmax * INFO_RS;
+                for (int e = lane; e < M * OBG_STRIDE; e += 64) {
+                    const int o = e / OBG_STRIDE, k = e - o * OBG_STRIDE;
+                    if (k < OBG_UB + 6) dst[fb.obs_cam[o0 + o] * INFO_RS + k] = src[e];
+                }
+            }
+            unsigned lo = (unsigned)mk, hi = (unsigned)(mk >> 32);
 #pragma unroll
-    for (int u = 0; u < COLS; ++u) {
-        const int j = lane + 64 * u;
-        hcol[u] = (j == C) ? ws.Cmax : j;
+            for (int w = 32; w >= 1; w >>= 1) {
+                lo |= (unsigned)__shfl_xor((int)lo, w, 64);
+                hi |= (unsigned)__shfl_xor((int)hi, w, 64);
+            }
+            if (lane == 0) mask[s] = ((unsigned long long)hi << 32) | lo;
+        }
+        __syncthreads();
+        for (int s = 0; s < INFO_FB; ++s) {
+            const unsigned long long mk = mask[s];
+            const double* rs = rec + (size_t)s * Nmax * INFO_RS;
+#pragma unroll
+            for (int m = 0; m < BPT; ++m) {
+                if (!act[m] || !((mk >> I[m]) & (mk >> J[m]) & 1ull)) continue;
+                const double* gi = rs + I[m] * INFO_RS;
+                const double* gj = rs + J[m] * INFO_RS;
+#pragma unroll
+                for (int t = 0; t < 3; ++t) {
+                    double u[6], v[6];
+#pragma unroll
+                    for (int x = 0; x < 6; ++x) { u[x] = gi[OBG_G + 6 * t + x]; v[x] = gj[OBG_G + 6 * t + x]; }
+#pragma unroll
+                    for (int x = 0; x < 6; ++x)
+#pragma unroll
+                        for (int y = 0; y < 6; ++y) a[m][x][y] -= u[x] * v[y];
+                }
+                if (I[m] == J[m]) {
+#pragma unroll
+                    for (int x = 0, e = 0; x < 6; ++x)
+#pragma unroll
+                        for (int y = 0; y <= x; ++y, ++e) {
+                            const double d = gi[OBG_DS + e];
+                            a[m][x][y] += d;
+                            if (y < x) a[m][y][x] += d;
+                        }
+#pragma unroll
+                    for (int x = 0; x < 6; ++x) bv[m][x] += gi[OBG_UB + x];
+                }
+            }
+        }
+        __syncthreads();
     }
-    if (compress) {
-        for (int r = 0; r < C; ++r)
+
+    // ---- augmented outer-product Cholesky with diagonal pivoting ----
+    KT* F = ws.Hthin + (size_t)b * Cmax * (Cmax + 1);
+    const int ldf = Cmax + 1;
+    int k = 0;
+    for (; k < C; ++k) {
 #pragma unroll
-            for (int u = 0; u < COLS; ++u)
-                if (lane + 64 * u <= C) H[(size_t)r * ldh + hcol[u]] = 0;
-    } else {
-        for (int e = lane; e < n * ldh; e += 64) H[e] = 0;
-    }
-    for (int f = fb.feat_off[b]; f < fb.feat_off[b + 1]; ++f) {
-        if (!fb.include[f]) continue;
-        const int o0 = fb.obs_off[f], M = fb.obs_off[f + 1] - o0;
-        const T* wsf = fb.obs_ws + (size_t)o0 * OBS_WS;
-        for (int i = lane; i < st.Nmax; i += 64) s_obs[i] = -1;
-        if (lane < 3) s_sc[lane] = fb.tau[4 * f + lane];
-        int smin = 1 << 30;
-        for (int i = 0; i < M; ++i) smin = min(smin, fb.obs_cam[o0 + i]);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        for (int i = lane; i < M; i += 64) s_obs[fb.obs_cam[o0 + i]] = i;
-        const int c0 = 6 * smin;
-        const int n4 = 4 * M;
-        for (int a0 = 3; a0 < n4; a0 += CH) {
-            const int nr = min(CH, n4 - a0);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            for (int rr = lane; rr < CH; rr += 64) {
-                const int row = a0 + rr;
-                if (rr < nr) {
-                    const T* wr = wsf + (size_t)(row >> 2) * OBS_WS;
-                    s_V[4 * rr + 0] = wr[OBS_V + 3 * (row & 3) + 0];
-                    s_V[4 * rr + 1] = wr[OBS_V + 3 * (row & 3) + 1];
-                    s_V[4 * rr + 2] = wr[OBS_V + 3 * (row & 3) + 2];
-                    s_V[4 * rr + 3] = wr[OBS_QR + (row & 3)];
-                } else {
-                    s_V[4 * rr + 0] = s_V[4 * rr + 1] = s_V[4 * rr + 2] = s_V[4 * rr + 3] = 0;
+        for (int m = 0; m < BPT; ++m)
+            if (act[m] && I[m] == J[m])
+#pragma unroll
+                for (int x = 0; x < 6; ++x) dval[6 * I[m] + x] = chosen[6 * I[m] + x] ? -1.0 : a[m][x][x];
+        LDS_BARRIER();
+        if (wave == 0) {
+            double best = -2.0;
+            int bi = 0;
+            for (int i = lane; i < C; i += 64) {
+                const double d = dval[i];
+                if (d > best) { best = d; bi = i; }
+            }
+#pragma unroll
+            for (int w = 32; w >= 1; w >>= 1) {
+                const double ob = __shfl_xor(best, w, 64);
+                const int oi = __shfl_xor(bi, w, 64);
+                if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+            }
+            if (lane == 0) {
+                if (k == 0) s_d0 = best;
+                const bool stop = !(best > 0.0) || best <= tol_rel * s_d0;
+                s_stop = stop;
+                if (!stop) {
+                    s_p = bi;
+                    s_inv = 1.0 / sqrt(best);
+                    chosen[bi] = 1;
                 }
             }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            // chunk rows as 2-wide vectors: rows (2i, 2i+1) pair up for v_pk_fma_f32
-            using V2 = T __attribute__((ext_vector_type(2)));
-            constexpr int CH2 = CH / 2;
-            V2 bv[COLS][CH2];
+        }
+        LDS_BARRIER();
+        if (s_stop) break;
+        const int p = s_p, P = p / 6, q = p - 6 * P;
+        const double inv = s_inv;
 #pragma unroll
-            for (int u = 0; u < COLS; ++u) {
-                const int j = lane + 64 * u;
-                const int oi = (j < C) ? s_obs[j / 6] : -1;
-                T w0 = 0, w1 = 0, w2 = 0, hx0 = 0, hx1 = 0, hx2 = 0, hx3 = 0;
-                if (oi >= 0) {
-                    const T* wo = wsf + (size_t)oi * OBS_WS;
-                    const int c = j % 6;
-                    w0 = s_sc[0] * wo[OBS_W + c];
-                    w1 = s_sc[1] * wo[OBS_W + 6 + c];
-                    w2 = s_sc[2] * wo[OBS_W + 12 + c];
-                    hx0 = wo[OBS_HX + c];
-                    hx1 = wo[OBS_HX + 6 + c];
-                    hx2 = wo[OBS_HX + 12 + c];
-                    hx3 = wo[OBS_HX + 18 + c];
-                }
+        for (int m = 0; m < BPT; ++m) {
+            if (!act[m]) continue;
+            if (I[m] == P) {   // row q of block (P, J): A[p][6J + y]
 #pragma unroll
-                for (int rr = 0; rr < CH; ++rr) {
-                    const int row = a0 + rr;
-                    T x = 0;
-                    if (j == C) {
-                        x = s_V[4 * rr + 3];
-                    } else if (oi >= 0 && rr < nr) {
-                        const int ra = row & 3;
-                        T h = ra == 0 ? hx0 : (ra == 1 ? hx1 : (ra == 2 ? hx2 : hx3));
-                        h = ((row >> 2) == oi) ? h : T(0);
-                        x = h - (s_V[4 * rr] * w0 + s_V[4 * rr + 1] * w1 + s_V[4 * rr + 2] * w2);
-                    }
-                    if (rr & 1) bv[u][rr >> 1].y = x;
-                    else bv[u][rr >> 1].x = x;
+                for (int y = 0; y < 6; ++y) {
+                    double v = 0;
+#pragma unroll
+                    for (int x = 0; x < 6; ++x) v = x == q ? a[m][x][y] : v;
+                    const int c = 6 * J[m] + y;
+                    fvec[c] = (chosen[c] && c != p) ? 0.0 : v * inv;
                 }
-                __builtin_amdgcn_sched_barrier(0);   // keep the three columns' generation apart
+                if (J[m] == P) {
+                    double v = 0;
+#pragma unroll
+                    for (int x = 0; x < 6; ++x) v = x == q ? bv[m][x] : v;
+                    fvec[Cmax] = v * inv;
+                }
+            } else if (J[m] == P) {   // column q of block (I, P): A[6I + y][p]
+#pragma unroll
+                for (int y = 0; y < 6; ++y) {
+                    double v = 0;
+#pragma unroll
+                    for (int x = 0; x < 6; ++x) v = x == q ? a[m][y][x] : v;
+                    const int c = 6 * I[m] + y;
+                    fvec[c] = chosen[c] ? 0.0 : v * inv;
+                }
             }
-            if (!compress) {   // R <= C: the stacked rows are H_thin (msckf.py:554-556)
-                const int base = fb.row_off[f] + (a0 - 3);
+        }
+        LDS_BARRIER();
+        for (int c = tid; c < C; c += NT) F[(size_t)k * ldf + c] = fvec[c];
+        if (tid == 0) F[(size_t)k * ldf + Cmax] = fvec[Cmax];
 #pragma unroll
-                for (int u = 0; u < COLS; ++u)
-                    if (lane + 64 * u <= C)
+        for (int m = 0; m < BPT; ++m) {
+            if (!act[m]) continue;
+            double u[6], v[6];
 #pragma unroll
-                        for (int rr = 0; rr < CH; ++rr)
-                            if (rr < nr)
-                                H[(size_t)(base + rr) * ldh + hcol[u]] = (rr & 1) ? bv[u][rr >> 1].y : bv[u][rr >> 1].x;
-                continue;
+            for (int x = 0; x < 6; ++x) { u[x] = fvec[6 * I[m] + x]; v[x] = fvec[6 * J[m] + x]; }
+#pragma unroll
+            for (int x = 0; x < 6; ++x)
+#pragma unroll
+                for (int y = 0; y < 6; ++y) a[m][x][y] -= u[x] * v[y];
+            if (I[m] == J[m]) {
+                const double rk = fvec[Cmax];
+#pragma unroll
+                for (int x = 0; x < 6; ++x) bv[m][x] -= u[x] * rk;
             }
-            auto load_row = [&](int r, int cmin, T* dst) {   // R[r][j] for own columns j >= cmin
-#pragma unroll
-                for (int u = 0; u < COLS; ++u) {
-                    const int j = lane + 64 * u;
-                    dst[u] = (r < C && j >= cmin && j <= C) ? H[(size_t)r * ldh + hcol[u]] : T(0);
-                }
-            };
-            // one column step: reflector of column c from the owner lane (slot UC)
-            auto step = [&](auto UCc, int c, const T* rrow) {
-                constexpr int UC = decltype(UCc)::value;
-                const int lc = c & 63;
-                V2 v[CH2];
-                V2 own2 = {0, 0};
-#pragma unroll
-                for (int i = 0; i < CH2; ++i) {
-                    v[i].x = lane_bcast(bv[UC][i].x, lc);
-                    v[i].y = lane_bcast(bv[UC][i].y, lc);
-                    own2 += bv[UC][i] * bv[UC][i];
-                }
-                const T xs = lane_bcast(own2.x + own2.y, lc);
-                const T alpha = lane_bcast(rrow[UC], lc);
-                T tj = 0, scale = 0, beta = alpha;
-                if (xs != T(0)) {
-                    const T nrm = fast_sqrt(alpha * alpha + xs);
-                    beta = alpha >= 0 ? -nrm : nrm;
-                    const T rb = fast_rcp(beta);
-                    tj = (beta - alpha) * rb;
-                    scale = fast_rcp(alpha - beta);
-                }
-                const T ts = tj * scale;
-#pragma unroll
-                for (int u = UC; u < COLS; ++u) {
-                    const int j = lane + 64 * u;
-                    if (j == c) {
-                        H[(size_t)c * ldh + hcol[u]] = beta;
-                    } else if (j > c && j <= C && tj != T(0)) {
-                        V2 q = {0, 0};
-#pragma unroll
-                        for (int i = 0; i < CH2; ++i) q += v[i] * bv[u][i];
-                        const T w = rrow[u] + scale * (q.x + q.y);
-                        H[(size_t)c * ldh + hcol[u]] = rrow[u] - tj * w;
-                        const T f2 = ts * w;
-                        const V2 f22 = {f2, f2};
-#pragma unroll
-                        for (int i = 0; i < CH2; ++i) bv[u][i] -= v[i] * f22;
-                    }
-                }
-            };
-            // R rows written by this wave's previous chunk (or the zero fill) are
-            // re-read below: drain its stores first -- a load may otherwise
-            // overtake a same-address store under heavy memory traffic
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            T rA[COLS], rB[COLS], rC[COLS], rD[COLS];
-            load_row(c0, c0, rA);
-            load_row(c0 + 1, c0 + 1, rB);
-            auto segment = [&](auto UCc) {
-                constexpr int UC = decltype(UCc)::value;
-                const int cb = max(c0, 64 * UC), ce = min(C, 64 * (UC + 1));
-                int c = cb;
-                for (; c + 1 < ce; c += 2) {
-                    load_row(c + 2, c + 2, rC);
-                    step(UCc, c, rA);
-                    load_row(c + 3, c + 3, rD);
-                    step(UCc, c + 1, rB);
-#pragma unroll
-                    for (int u = 0; u < COLS; ++u) { rA[u] = rC[u]; rB[u] = rD[u]; }
-                }
-                if (c < ce) {
-                    step(UCc, c, rA);
-                    load_row(c + 2, c + 2, rC);
-#pragma unroll
-                    for (int u = 0; u < COLS; ++u) { rA[u] = rB[u]; rB[u] = rC[u]; }
-                }
-            };
-            segment(std::integral_constant<int, 0>{});
-            segment(std::integral_constant<int, 1>{});
-            segment(std::integral_constant<int, 2>{});
         }
     }
+    if (tid == 0) info[1] = k;
 }
 
 // ===========================================================================
@@ -1902,7 +1370,7 @@ __global__ void __launch_bounds__(256) k_hp(DevState<T> st, UpdWs<T> ws) {
     const int C = 6 * st.ncams[b], D = 21 + C;
     const int ti = blockIdx.y, tj = blockIdx.x;
     if (ti * TB >= n || tj * TB >= D) return;
-    const T* H = ws.Hthin + (size_t)b * ws.Cmax * (ws.Cmax + 1);
+    const KT* H = ws.Hthin + (size_t)b * ws.Cmax * (ws.Cmax + 1);
     const T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
     KT* HP = ws.HP + (size_t)b * ws.Cmax * st.Dmax;
     const int ldh = ws.Cmax + 1, ld = st.Dmax;
@@ -1919,7 +1387,7 @@ __global__ void __launch_bounds__(256) k_s(DevState<T> st, Params<T> prm, UpdWs<
     const int C = 6 * st.ncams[b];
     const int ti = blockIdx.y, tj = blockIdx.x;
     if (ti * TB >= n || tj * TB >= n || tj > ti) return;   // lower triangle of tiles
-    const T* H = ws.Hthin + (size_t)b * ws.Cmax * (ws.Cmax + 1);
+    const KT* H = ws.Hthin + (size_t)b * ws.Cmax * (ws.Cmax + 1);
     const KT* HP = ws.HP + (size_t)b * ws.Cmax * st.Dmax;
     KT* S = ws.S + (size_t)b * ws.Cmax * ws.Cmax;
     const int ldh = ws.Cmax + 1, ld = st.Dmax, lds = ws.Cmax;
@@ -1939,7 +1407,7 @@ __global__ void __launch_bounds__(256) k_chol(DevState<T> st, UpdWs<T> ws) {
     if (n == 0) return;
     KT* S = ws.S + (size_t)b * ws.Cmax * ws.Cmax;
     const int lds = ws.Cmax;
-    const T* H = ws.Hthin + (size_t)b * ws.Cmax * (ws.Cmax + 1);
+    const KT* H = ws.Hthin + (size_t)b * ws.Cmax * (ws.Cmax + 1);
     const int ldh = ws.Cmax + 1;
     __shared__ KT s_y[512];
     __shared__ int s_fail;
@@ -2160,73 +1628,40 @@ void launch_select(hipStream_t s, const DevState<T>& st, const FeatBatch<T>& fb,
     hipLaunchKernelGGL(k_select<T>, dim3((st.B + 63) / 64), dim3(64), 0, s, st, fb, ws, row_cap);
 }
 
-static int g_compress_mode = -1;   // -1 auto, 0 global R, 1 LDS R (MSCKF_COMPRESS_R env)
+// Numerical-rank threshold of the pivoted Cholesky, relative to max diag(A).
+constexpr double INFO_TOL_REL = 1e-11;
 
-template <typename T, int COLS, int CH>
-void launch_compress_reg(hipStream_t s, const DevState<T>& st, const FeatBatch<T>& fb, const UpdWs<T>& ws) {
-    const size_t base = (2 * CH + 8 + 4 * CH) * sizeof(T) + ((st.Nmax + 3) & ~3) * sizeof(int);
-    const size_t rl = base + (size_t)ws.Cmax * (ws.Cmax + 1) * sizeof(T);
-    if (g_compress_mode < 0) {
-        const char* e = getenv("MSCKF_COMPRESS_R");
-        g_compress_mode = e ? atoi(e) : 0;
+template <typename T, int BPT, int NT>
+static void launch_info_cfg(hipStream_t s, const DevState<T>& st, const FeatBatch<T>& fb, const UpdWs<T>& ws) {
+    const size_t lds = ((size_t)INFO_FB * st.Nmax * INFO_RS + 2 * (size_t)ws.Cmax + 1) * sizeof(double) +
+                       INFO_FB * sizeof(unsigned long long) + (size_t)ws.Cmax * sizeof(int);
+    static size_t attr = 64 * 1024;   // dynamic LDS granted so far (default 64 KB)
+    if (lds > attr) {
+        (void)hipFuncSetAttribute((const void*)k_info<T, BPT, NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds);
+        attr = lds;
     }
-    if (g_compress_mode == 1 && rl <= 160 * 1024) {
-        (void)hipFuncSetAttribute((const void*)k_compress_reg<T, CH, COLS, true>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        hipLaunchKernelGGL((k_compress_reg<T, CH, COLS, true>), dim3(st.B), dim3(256), rl, s, st, fb, ws);
-    } else {
-        hipLaunchKernelGGL((k_compress_reg<T, CH, COLS, false>), dim3(st.B), dim3(256), base, s, st, fb, ws);
-    }
+    hipLaunchKernelGGL((k_info<T, BPT, NT>), dim3(st.B), dim3(NT), lds, s, st, fb, ws, INFO_TOL_REL);
 }
 
-static int g_compress_ch = -1;   // rows per register chunk (MSCKF_COMPRESS_CH env: 32 | 64)
-
+// Default: information assembly + pivoted Cholesky (k_info).  MSCKF_COMPRESS=qr
+// selects the round-1 QR row-merge (msckf_qr_merge.hip) for A/B runs.
 template <typename T>
 void launch_compress(hipStream_t s, const DevState<T>& st, const FeatBatch<T>& fb, const UpdWs<T>& ws) {
-    if (g_compress_ch < 0) {
-        const char* e = getenv("MSCKF_COMPRESS_CH");
-        g_compress_ch = e ? atoi(e) : 16;
+    static int mode = -1;
+    if (mode < 0) {
+        const char* e = getenv("MSCKF_COMPRESS");
+        mode = (e && e[0] == 'q') ? 1 : 0;
     }
-    const bool wide = g_compress_ch >= 64 && sizeof(T) == 4;
-    const char* me = getenv("MSCKF_COMPRESS_MODE");   // wave (default) | panel | block
-    const int mode = me ? (me[0] == 'p' ? 1 : (me[0] == 'b' ? 2 : 0)) : 0;
-    if (mode == 0 && ws.Cmax + 1 <= 192) {
-        const char* we = getenv("MSCKF_COMPRESS_W");
-        if (!we || atoi(we) != 0) {
-            const size_t lds = (4 * 32 + 4) * sizeof(T) + ((st.Nmax + 3) & ~3) * sizeof(int);
-            if (g_compress_ch == 32)
-                hipLaunchKernelGGL((k_compress_w<T, 32>), dim3(st.B), dim3(64), lds, s, st, fb, ws);
-            else
-                hipLaunchKernelGGL((k_compress_w<T, 16>), dim3(st.B), dim3(64), lds, s, st, fb, ws);
-            return;
-        }
-        const size_t lds = (4 * 32 + 4) * sizeof(T) + ((st.Nmax + 3) & ~3) * sizeof(int);
-        if constexpr (sizeof(T) == 4) {
-            if (wide) {
-                hipLaunchKernelGGL((k_compress_wave<T, 64, 3>), dim3(st.B), dim3(64), lds + 4 * 32 * sizeof(T), s,
-                                   st, fb, ws);
-                return;
-            }
-            if (g_compress_ch == 16) {
-                hipLaunchKernelGGL((k_compress_wave<T, 16, 3>), dim3(st.B), dim3(64), lds, s, st, fb, ws);
-                return;
-            }
-        }
-        hipLaunchKernelGGL((k_compress_wave<T, 32, 3>), dim3(st.B), dim3(64), lds, s, st, fb, ws);
+    if (mode == 1) {
+        launch_compress_qr<T>(s, st, fb, ws);
         return;
     }
-    if (mode <= 1 && ws.Cmax + 1 <= 256) {
-        constexpr int CHP = 32;
-        const size_t lds = (2 * 16 * CHP + 2 * 16 + 4 + 4 * CHP) * sizeof(T) + ((st.Nmax + 3) & ~3) * sizeof(int);
-        hipLaunchKernelGGL((k_compress_panel<T, CHP>), dim3(st.B), dim3(256), lds, s, st, fb, ws);
-        return;
-    }
-    if (ws.Cmax + 1 <= 256) {
-        if (wide) launch_compress_reg<T, 1, 64>(s, st, fb, ws);
-        else launch_compress_reg<T, 1, 32>(s, st, fb, ws);
-    } else {
-        launch_compress_reg<T, 2, 32>(s, st, fb, ws);
-    }
+    const int nblk = st.Nmax * (st.Nmax + 1) / 2;   // 6x6 cam-pair blocks of A (lower triangle)
+    if (nblk <= 256) launch_info_cfg<T, 1, 256>(s, st, fb, ws);
+    else if (nblk <= 512) launch_info_cfg<T, 1, 512>(s, st, fb, ws);
+    else if (nblk <= 1024) launch_info_cfg<T, 1, 1024>(s, st, fb, ws);
+    else launch_info_cfg<T, 3, 1024>(s, st, fb, ws);   // Nmax <= 64 (3072 blocks)
 }
 
 template <typename T>

@@ -84,6 +84,8 @@ void launch_select(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const U
 template <typename T>
 void launch_compress(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const UpdWs<T>&);
 template <typename T>
+void launch_compress_qr(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const UpdWs<T>&);
+template <typename T>
 void launch_kalman(hipStream_t, const DevState<T>&, const Params<T>&, const UpdWs<T>&, KernelTimer*);
 
 }  // namespace msckf
