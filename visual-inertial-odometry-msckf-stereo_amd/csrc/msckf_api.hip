@@ -252,13 +252,12 @@ int load_features(msckf_ctx* c, int nf, const int32_t* feat_off, int single_filt
     if (nobs) HIPC(hipMemcpyAsync(c->obs_cam.p, obs_cam, nobs * sizeof(int), hipMemcpyHostToDevice, s));
     HIPC(hipMemcpyAsync(c->ysq_off.p, ysq.data(), (nf + 1) * sizeof(long long), hipMemcpyHostToDevice, s));
     {   // gating size classes, largest first inside the list (long blocks start early)
-        static const int lim[GateClasses::NC] = {8, 16, 24, 1 << 30};
         std::vector<std::vector<int>> cls(GateClasses::NC);
         GateClasses gc;
         for (int f = 0; f < nf; ++f) {
             const int M = obs_off[f + 1] - obs_off[f];
             int k = 0;
-            while (M > lim[k]) ++k;
+            while (M > GateClasses::LIM[k]) ++k;
             cls[k].push_back(f);
             gc.maxM[k] = std::max(gc.maxM[k], M);
         }

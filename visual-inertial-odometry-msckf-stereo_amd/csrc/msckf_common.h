@@ -24,7 +24,8 @@ enum CamField { C_Q = 0, C_P = 4, C_QN = 7 };
 //   V   4x3  rows of the 3 Householder vectors of H_f's QR
 //   W   3x6  this observation's 6 columns of w_j = v_j^T X_{j-1}
 //   Qr  4    rows of Q^T r
-constexpr int OBS_HX = 0, OBS_V = 24, OBS_W = 36, OBS_QR = 54, OBS_WS = 58;
+//   R   4    the observation's residual r_i (before projection)
+constexpr int OBS_HX = 0, OBS_V = 24, OBS_W = 36, OBS_QR = 54, OBS_R = 58, OBS_WS = 62;
 
 // Per-observation Gram terms written by the feature kernel (always fp64),
 // consumed by the information assembly (k_info).  With G = the top 3 rows of

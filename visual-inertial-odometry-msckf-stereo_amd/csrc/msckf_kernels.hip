@@ -719,6 +719,8 @@ __global__ void __launch_bounds__(256) k_feature(DevState<T> st, Params<T> prm, 
     }
     for (int c = 0; c < 6; ++c)   // Hx_i^T r_i, before r is reflected
         u6[c] = Hx[c] * r[0] + Hx[6 + c] * r[1] + Hx[12 + c] * r[2] + Hx[18 + c] * r[3];
+    if (own)
+        for (int e = 0; e < 4; ++e) fb.obs_ws[(size_t)(o0 + lane) * OBS_WS + OBS_R + e] = (T)r[e];
     // ---- Householder QR of H_f across the wave (rows 4i..4i+3 in lane i) ----
     CT V[12];
     CT tau[3];
@@ -1062,6 +1064,216 @@ __global__ void __launch_bounds__(256) k_gate_lds(DevState<T> st, Params<T> prm,
         fb.gamma[f] = gam;
         fb.accept[f] = (gam < fb.chi2[f]) ? 1 : 0;
     }
+}
+
+// One-wavefront gating with the matrix in registers (production path for
+// M <= 34).  With Y = Hx P Hx^T + s2 I (4M x 4M, PD) and N an orthonormal basis
+// of the left nullspace of H_f, the reference's S = N^T Y N (msckf.py:607-609
+// on H0 = N^T Hx) satisfies the oblique-projection identity
+//   N S^-1 N^T = Y^-1 - Y^-1 H_f (H_f^T Y^-1 H_f)^-1 H_f^T Y^-1,
+// so gamma = r0^T S^-1 r0 is what an LDL^T elimination of the saddle-point
+// matrix
+//     [ Y      H_f  r ]
+//     [ H_f^T  0    0 ]      (4M + 4 square, no pivoting: Y is PD and the
+//     [ r^T    0    0 ]       H_f block's Schur complement is negative definite)
+// leaves in its last pivot: -gamma.  No projection is formed at all.
+// The matrix is held as 4x4 tiles (lower triangle, column-major tile order;
+// tile t belongs to lane t % 64, slot t / 64); tile row M is [H_f^T ; r^T].
+// Blocked LDL^T, one tile column per step: the diagonal tile's owner factors
+// it, the panel tiles' owners publish W = A L_d^-T by row through LDS, and
+// every tile right of the panel takes the rank-4 update from registers; slots
+// whose tiles all lie in finished columns are skipped.  The last tile's owner
+// finishes with the three negative pivots.  No workgroup barriers:
+// 4 independent features per 256-thread workgroup.
+template <typename T>
+__host__ __device__ constexpr int gate_wave_lds_T(int Mmax) {
+    return 24 * Mmax + 8 * (4 * Mmax + 4);   // hx, panel rows (raw -> W D^-1), W^T blocks
+}
+
+template <typename T, int TPL>
+__global__ void __launch_bounds__(256) k_gate_wave(DevState<T> st, Params<T> prm, FeatBatch<T> fb,
+                                                   const int* __restrict__ flist, int nlist, int Mmax, int phases) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#ifdef GW_PHASES_CONST
+    phases = GW_PHASES_CONST;
+#endif
+    const int li = blockIdx.x * 4 + wv;
+    if (li >= nlist) return;
+    const int f = flist[li];
+    if (!fb.valid[f]) {
+        if (lane == 0) { fb.gamma[f] = T(NAN); fb.accept[f] = 0; }
+        return;
+    }
+    const int b = fb.feat_filter[f];
+    const int o0 = fb.obs_off[f], M = fb.obs_off[f + 1] - o0;
+    const int nT = M + 1, ntiles = nT * (nT + 1) / 2, L4 = 4 * Mmax + 4;
+    T* hx = reinterpret_cast<T*>(smem_raw) + (size_t)wv * gate_wave_lds_T<T>(Mmax);
+    T* wd = hx + 24 * Mmax;     // [L4][4]  panel rows: raw tile rows, then W D^-1
+    T* wt = wd + 4 * L4;        // [L4/4][4][4]  W^T per 4-row block: wt[blk][c][y] = W[4 blk + y][c]
+    int* slot = reinterpret_cast<int*>(reinterpret_cast<T*>(smem_raw) + 4 * gate_wave_lds_T<T>(Mmax)) + wv * Mmax;
+    const T* ws = fb.obs_ws + (size_t)o0 * OBS_WS;
+    for (int e = lane; e < 24 * M; e += 64) {
+        const int o = e / 24;
+        hx[e] = ws[(size_t)o * OBS_WS + OBS_HX + (e - 24 * o)];
+    }
+    for (int i = lane; i < M; i += 64) slot[i] = fb.obs_cam[o0 + i];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+
+    // tile coordinates (column-major lower triangle of the nT x nT tile grid),
+    // packed ti | tl << 16 in one register; tlmax[s] (wave-uniform) is the last
+    // tile column present in slot s
+    int crd[TPL], tlmax[TPL];
+#pragma unroll
+    for (int s = 0; s < TPL; ++s) {
+        const int t = 64 * s + lane;
+        int c = 0, rem = t < ntiles ? t : 0;
+        while (rem >= nT - c) { rem -= nT - c; ++c; }
+        crd[s] = t < ntiles ? ((c + rem) | (c << 16)) : -1;
+        int tm = 64 * s + 63 < ntiles - 1 ? 64 * s + 63 : ntiles - 1;
+        int cm = 0;
+        while (tm >= nT - cm) { tm -= nT - cm; ++cm; }
+        tlmax[s] = 64 * s < ntiles ? cm : -1;
+    }
+#define TI(s) (crd[s] & 0xffff)
+#define TL(s) (crd[s] >> 16)
+#define OK(s) (crd[s] >= 0)
+
+    // ---- Y = Hx P Hx^T tiles, r row ----
+    const T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
+    const int ldp = st.Dmax;
+    T a[TPL][4][4];
+#pragma unroll
+    for (int s = 0; s < TPL; ++s) {
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+#pragma unroll
+            for (int y = 0; y < 4; ++y) a[s][x][y] = 0;
+        if (!OK(s) || !(phases & 1)) continue;
+        const int i = TI(s), l = TL(s);
+        if (i < M) {
+            const T* Pb = P + (size_t)(21 + 6 * slot[i]) * ldp + 21 + 6 * slot[l];
+            T Pl[36];
+#pragma unroll
+            for (int k = 0; k < 6; ++k)
+#pragma unroll
+                for (int c = 0; c < 6; ++c) Pl[6 * k + c] = Pb[(size_t)k * ldp + c];
+            const T* Hi = hx + 24 * i;
+            const T* Hl = hx + 24 * l;
+#pragma unroll
+            for (int x = 0; x < 4; ++x) {
+                T t1[6];
+#pragma unroll
+                for (int c = 0; c < 6; ++c) {
+                    T acc = 0;
+#pragma unroll
+                    for (int k = 0; k < 6; ++k) acc += Hi[6 * x + k] * Pl[6 * k + c];
+                    t1[c] = acc;
+                }
+#pragma unroll
+                for (int y = 0; y < 4; ++y) {
+                    T acc = 0;
+#pragma unroll
+                    for (int k = 0; k < 6; ++k) acc += t1[k] * Hl[6 * y + k];
+                    a[s][x][y] = acc;
+                }
+            }
+            if (i == l)
+#pragma unroll
+                for (int x = 0; x < 4; ++x) a[s][x][x] += prm.sigma2;
+        } else if (l < M) {   // [H_f^T ; r^T] for observation l; H_f = -Hx[:, 3:6]
+            const T* Hl = hx + 24 * l;
+#pragma unroll
+            for (int y = 0; y < 4; ++y) {
+#pragma unroll
+                for (int x = 0; x < 3; ++x) a[s][x][y] = -Hl[6 * y + 3 + x];
+                a[s][3][y] = ws[(size_t)l * OBS_WS + OBS_R + y];
+            }
+        }
+        asm volatile("" ::: "memory");
+    }
+
+    // ---- blocked LDL^T, one 4-wide tile column per step ----
+    bool fail = false;
+    for (int tj = 0; tj < ((phases & 4) ? M : 0); ++tj) {
+        // 1. owners of the tile column dump it (raw rows 4 tj .. 4 nT - 1)
+#pragma unroll
+        for (int s = 0; s < TPL; ++s) {
+            if (!OK(s) || TL(s) != tj) continue;
+            T* dst = wd + 16 * TI(s);
+#pragma unroll
+            for (int x = 0; x < 4; ++x)
+#pragma unroll
+                for (int y = 0; y < 4; ++y) dst[4 * x + y] = a[s][x][y];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        // 2. every lane factors the diagonal tile (uniform): A_d = L_d D L_d^T
+        const T* dt = wd + 16 * tj;
+        const T d0 = dt[0];
+        const T l10 = dt[4] / d0, l20 = dt[8] / d0, l30 = dt[12] / d0;
+        const T d1 = dt[5] - l10 * l10 * d0;
+        const T l21 = (dt[9] - l20 * l10 * d0) / d1;
+        const T l31 = (dt[13] - l30 * l10 * d0) / d1;
+        const T d2 = dt[10] - l20 * l20 * d0 - l21 * l21 * d1;
+        const T l32 = (dt[14] - l30 * l20 * d0 - l31 * l21 * d1) / d2;
+        const T d3 = dt[15] - l30 * l30 * d0 - l31 * l31 * d1 - l32 * l32 * d2;
+        if (!(d0 > T(0)) || !(d1 > T(0)) || !(d2 > T(0)) || !(d3 > T(0))) { fail = true; break; }
+        const T e0 = T(1) / d0, e1 = T(1) / d1, e2 = T(1) / d2, e3 = T(1) / d3;
+        // 3. panel rows below the diagonal tile: W = A L_d^-T; store W D^-1 by
+        //    row and W transposed by 4-row block
+        for (int q = 4 * tj + 4 + lane; q < 4 * nT; q += 64) {
+            T* row = wd + 4 * q;
+            const T w0 = row[0];
+            const T w1 = row[1] - w0 * l10;
+            const T w2 = row[2] - w0 * l20 - w1 * l21;
+            const T w3 = row[3] - w0 * l30 - w1 * l31 - w2 * l32;
+            row[0] = w0 * e0; row[1] = w1 * e1; row[2] = w2 * e2; row[3] = w3 * e3;
+            T* col = wt + 16 * (q >> 2) + (q & 3);
+            col[0] = w0; col[4] = w1; col[8] = w2; col[12] = w3;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        // 4. trailing update A_il -= (W_i D^-1) W_l^T for tiles right of the panel
+#pragma unroll
+        for (int s = 0; s < TPL; ++s) {
+            if (tlmax[s] <= tj) continue;   // slot entirely in finished columns
+            if (!OK(s) || TL(s) <= tj) continue;
+            const T* ri = wd + 16 * TI(s);
+            const T* cl = wt + 16 * TL(s);
+            T u[4][4], w[4][4];
+#pragma unroll
+            for (int x = 0; x < 4; ++x)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) { u[x][c] = ri[4 * x + c]; w[c][x] = cl[4 * c + x]; }
+#pragma unroll
+            for (int x = 0; x < 4; ++x)
+#pragma unroll
+                for (int y = 0; y < 4; ++y)
+                    a[s][x][y] -= u[x][0] * w[0][y] + u[x][1] * w[1][y] + u[x][2] * w[2][y] + u[x][3] * w[3][y];
+            asm volatile("" ::: "memory");   // keep one slot's operands live at a time
+        }
+    }
+    // the last tile [[H_f^T Y^-1 H_f, .], [., r^T Y^-1 r]] (negated): three
+    // negative pivots, then -gamma
+#pragma unroll
+    for (int s = 0; s < TPL; ++s) {
+        if (64 * s + lane == ntiles - 1) {
+            const T d0 = a[s][0][0];
+            const T l10 = a[s][1][0] / d0, l20 = a[s][2][0] / d0, l30 = a[s][3][0] / d0;
+            const T d1 = a[s][1][1] - l10 * l10 * d0;
+            const T l21 = (a[s][2][1] - l20 * l10 * d0) / d1;
+            const T l31 = (a[s][3][1] - l30 * l10 * d0) / d1;
+            const T d2 = a[s][2][2] - l20 * l20 * d0 - l21 * l21 * d1;
+            const T l32 = (a[s][3][2] - l30 * l20 * d0 - l31 * l21 * d1) / d2;
+            const T d3 = a[s][3][3] - l30 * l30 * d0 - l31 * l31 * d1 - l32 * l32 * d2;
+            T gam = -d3;
+            if (fail || !(d0 < T(0)) || !(d1 < T(0)) || !(d2 < T(0)) || !(gam == gam)) gam = T(INFINITY);
+            fb.gamma[f] = gam;
+            fb.accept[f] = (gam < fb.chi2[f]) ? 1 : 0;
+        }
+    }
+#undef TI
+#undef TL
+#undef OK
 }
 
 // ===========================================================================
@@ -1596,29 +1808,66 @@ size_t gate_lds_bytes(int maxM) {
            (maxM + 4) * sizeof(int);
 }
 
+template <typename T, int TPL>
+static void launch_gate_wave(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const FeatBatch<T>& fb,
+                             const int* list, int cnt, int Mmax) {
+    const size_t lds = 4 * ((size_t)gate_wave_lds_T<T>(Mmax) * sizeof(T) + (size_t)Mmax * sizeof(int));
+    static size_t attr = 64 * 1024;
+    if (lds > attr) {
+        (void)hipFuncSetAttribute((const void*)k_gate_wave<T, TPL>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds);
+        attr = lds;
+    }
+    static int phases = -1;   // MSCKF_GATE_PHASES: profiling aid (bit0 Y tiles, bit2 elimination)
+    if (phases < 0) {
+        const char* e = getenv("MSCKF_GATE_PHASES");
+        phases = e ? atoi(e) : 7;
+    }
+    hipLaunchKernelGGL((k_gate_wave<T, TPL>), dim3((cnt + 3) / 4), dim3(256), lds, s, st, prm, fb, list, cnt, Mmax,
+                       phases);
+}
+
 // Features are launched in size classes (by M, listed on the host at load
-// time): each class gets a workgroup size and an LDS footprint that fit it, so
-// small features do not pay for the largest one.
+// time): the register-tile wave kernel sized for the class, or for the
+// largest features the workgroup LDS kernel (global-memory kernel if even
+// that does not fit).
 template <typename T>
 void launch_gate(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const FeatBatch<T>& fb,
                  const GateClasses& gc) {
     if (fb.nf == 0) return;
-    static bool attr_set[2] = {false, false};
-    bool& done = attr_set[sizeof(T) == 8];
-    if (!done) {
+    static bool attr_set = false;
+    if (!attr_set) {
         (void)hipFuncSetAttribute((const void*)k_gate_lds<T>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        done = true;
+        attr_set = true;
+    }
+    static int mode = -1;   // MSCKF_GATE=lds forces the workgroup kernel for every class (A/B runs)
+    if (mode < 0) {
+        const char* e = getenv("MSCKF_GATE");
+        mode = (e && e[0] == 'l') ? 1 : 0;
     }
     for (int c = 0; c < GateClasses::NC; ++c) {
         const int cnt = gc.off[c + 1] - gc.off[c];
         if (cnt == 0) continue;
         const int maxM = gc.maxM[c];
+        const int* list = gc.list + gc.off[c];
+        if (mode == 0 && c < GateClasses::NC - 1) {
+            switch (GateClasses::TPL[c]) {
+                case 1: launch_gate_wave<T, 1>(s, st, prm, fb, list, cnt, maxM); break;
+                case 2: launch_gate_wave<T, 2>(s, st, prm, fb, list, cnt, maxM); break;
+                case 3: launch_gate_wave<T, 3>(s, st, prm, fb, list, cnt, maxM); break;
+                case 4: launch_gate_wave<T, 4>(s, st, prm, fb, list, cnt, maxM); break;
+                case 6: launch_gate_wave<T, 6>(s, st, prm, fb, list, cnt, maxM); break;
+                case 8: launch_gate_wave<T, 8>(s, st, prm, fb, list, cnt, maxM); break;
+                default: launch_gate_wave<T, 10>(s, st, prm, fb, list, cnt, maxM); break;
+            }
+            continue;
+        }
         const size_t lds = gate_lds_bytes<T>(maxM);
         const int threads = maxM <= 12 ? 64 : (maxM <= 20 ? 128 : 256);
         if (lds <= 160 * 1024)
-            hipLaunchKernelGGL(k_gate_lds<T>, dim3(cnt), dim3(threads), lds, s, st, prm, fb, gc.list + gc.off[c]);
+            hipLaunchKernelGGL(k_gate_lds<T>, dim3(cnt), dim3(threads), lds, s, st, prm, fb, list);
         else
-            hipLaunchKernelGGL(k_gate<T>, dim3(cnt), dim3(256), 0, s, st, prm, fb, gc.list + gc.off[c]);
+            hipLaunchKernelGGL(k_gate<T>, dim3(cnt), dim3(256), 0, s, st, prm, fb, list);
     }
 }
 

@@ -71,11 +71,17 @@ void launch_triangulate(hipStream_t, const DevState<T>&, const Params<T>&, const
 template <typename T>
 void launch_feature(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&);
 // Feature index lists per gating size class (device pointer + host offsets).
+// Gating size classes by observation count M.  Class c < NC-1 runs the
+// one-wave register-tile kernel with TPL[c] 4x4 tiles per lane (enough for the
+// (M+1)(M+2)/2 tiles of the augmented 4M+1 matrix); the last class runs the
+// workgroup LDS kernel.
 struct GateClasses {
-    static constexpr int NC = 4;        // M <= 8, <= 16, <= 24, larger
+    static constexpr int NC = 8;
+    static constexpr int LIM[NC] = {9, 14, 18, 21, 26, 30, 34, 1 << 30};
+    static constexpr int TPL[NC - 1] = {1, 2, 3, 4, 6, 8, 10};
     const int* list = nullptr;
-    int off[NC + 1] = {0, 0, 0, 0, 0};
-    int maxM[NC] = {0, 0, 0, 0};
+    int off[NC + 1] = {};
+    int maxM[NC] = {};
 };
 template <typename T>
 void launch_gate(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&, const GateClasses&);
