@@ -68,7 +68,7 @@ struct msckf_ctx {
     DBuf<unsigned char> P, imu, cams, P_snap, imu_snap, cams_snap;
     DBuf<int> ncams, ncams_snap;
     // update workspace
-    DBuf<unsigned char> Hthin, Hqr, HP, S, dx;
+    DBuf<unsigned char> Hthin, Hqr, HP, S, dx, Lc, Vi, Sii, G, Tm, W;
     DBuf<int> info;
     // feature batch
     int nf = 0, maxM = 0;
@@ -129,6 +129,13 @@ UpdWs<T> upd_ws(msckf_ctx* c) {
     w.dx = reinterpret_cast<KT*>(c->dx.p);
     w.info = c->info.p;
     w.Cmax = c->Cmax;
+    w.Cp = (c->Cmax + 3) & ~3;
+    w.Lc = reinterpret_cast<KT*>(c->Lc.p);
+    w.Vi = reinterpret_cast<KT*>(c->Vi.p);
+    w.Sii = reinterpret_cast<KT*>(c->Sii.p);
+    w.G = reinterpret_cast<KT*>(c->G.p);
+    w.Tm = reinterpret_cast<KT*>(c->Tm.p);
+    w.W = reinterpret_cast<KT*>(c->W.p);
     return w;
 }
 
@@ -360,14 +367,22 @@ int do_create(msckf_ctx* c) {
     HIPC(c->cams.ensure(B * c->Nmax * CAM_STRIDE * ts));
     HIPC(c->ncams.ensure(B));
     HIPC(c->Hthin.ensure(B * c->Cmax * (c->Cmax + 1) * sizeof(KT)));
-    {   // QR row-merge scratch only for MSCKF_COMPRESS=qr (A/B runs)
-        const char* e = getenv("MSCKF_COMPRESS");
-        if (e && e[0] == 'q') HIPC(c->Hqr.ensure(B * c->Cmax * (c->Cmax + 1) * ts));
+    {   // QR row-merge scratch only for MSCKF_UPDATE=qr (A/B runs)
+        if (update_mode(c->Cmax) == UPD_QR) HIPC(c->Hqr.ensure(B * c->Cmax * (c->Cmax + 1) * ts));
     }
     HIPC(c->HP.ensure(B * c->Cmax * c->Dmax * sizeof(KT)));
     HIPC(c->S.ensure(B * c->Cmax * c->Cmax * sizeof(KT)));
     HIPC(c->dx.ensure(B * (c->Dmax + c->Cmax) * sizeof(KT)));
     HIPC(c->info.ensure(4 * B));
+    if (update_mode(c->Cmax) == UPD_CHOL) {   // Cholesky-form Kalman workspace
+        const size_t Cp = (c->Cmax + 3) & ~3, kb = sizeof(KT);
+        HIPC(c->Lc.ensure(B * Cp * Cp * kb));
+        HIPC(c->Vi.ensure(B * 24 * Cp * kb));
+        HIPC(c->Sii.ensure(B * 24 * 24 * kb));
+        HIPC(c->G.ensure(B * c->Cmax * (c->Cmax + 1) * kb));
+        HIPC(c->Tm.ensure(B * c->Cmax * (c->Cmax + 1) * kb));
+        HIPC(c->W.ensure(B * (c->Dmax + 1) * Cp * kb));
+    }
     HIPC(hipMemset(c->P.p, 0, c->P.cap));
     HIPC(hipMemset(c->cams.p, 0, c->cams.cap));
     HIPC(hipMemset(c->ncams.p, 0, B * sizeof(int)));
@@ -590,7 +605,7 @@ int msckf_destroy(msckf_ctx_t* c) {
     if (!c) return 0;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (auto* b : {&c->P, &c->imu, &c->cams, &c->P_snap, &c->imu_snap, &c->cams_snap, &c->Hthin, &c->Hqr, &c->HP, &c->S,
+    for (auto* b : {&c->P, &c->imu, &c->cams, &c->P_snap, &c->imu_snap, &c->cams_snap, &c->Hthin, &c->Hqr, &c->HP, &c->S, &c->Lc, &c->Vi, &c->Sii, &c->G, &c->Tm, &c->W,
                     &c->dx, &c->obs_z, &c->chi2, &c->p_w, &c->obs_ws, &c->obs_g, &c->tau, &c->ysq, &c->gamma, &c->scratch})
         b->release();
     for (auto* b : {&c->ncams, &c->ncams_snap, &c->info, &c->feat_filter, &c->feat_off, &c->obs_off, &c->obs_cam,

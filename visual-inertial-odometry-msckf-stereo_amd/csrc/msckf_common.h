@@ -90,9 +90,17 @@ struct UpdWs {
     T* Hqr;      // [B][Cmax][Cmax+1]   QR row-merge output (MSCKF_COMPRESS=qr only)
     KT* HP;      // [B][Cmax][Dmax]     H_thin P, then L^-1 H_thin P
     KT* S;       // [B][Cmax][Cmax]     innovation covariance -> its Cholesky factor
-    KT* dx;      // [B][Dmax]
+    KT* dx;      // [B][Dmax + Cmax]
     int* info;   // [B][4]: rows stacked, n (rows of H_thin), compress flag, status
     int Cmax;
+    // Cholesky-form Kalman stage (msckf_kalman.hip); Cp = Cmax rounded up to 4
+    KT* Lc;      // [B][Cp][Cp]          chol(P_cc), lower
+    KT* Vi;      // [B][24][Cp]          P_ic Lc^-T (21 rows used)
+    KT* Sii;     // [B][24][24]          P_ii - Vi Vi^T
+    KT* G;       // [B][Cmax][Cmax+1]    A Lc
+    KT* Tm;      // [B][Cmax][Cmax+1]    (s2 I + Lc^T A Lc | Lc^T b), lower
+    KT* W;       // [B][Dmax+1][Cp]      rows [Vi ; Lc ; c^T] L_T^-T
+    int Cp;
 };
 
 // ------------------------------------------------------------ device math --

@@ -1339,7 +1339,8 @@ constexpr int INFO_FB = 4;    // features staged per round
 constexpr int INFO_RS = 50;   // LDS doubles per (feature, cam) record (48 + pad)
 
 template <typename T, int BPT, int NT>
-__global__ void __launch_bounds__(NT) k_info(DevState<T> st, FeatBatch<T> fb, UpdWs<T> ws, double tol_rel) {
+__global__ void __launch_bounds__(NT) k_info(DevState<T> st, FeatBatch<T> fb, UpdWs<T> ws, double tol_rel,
+                                             int phases, int assemble_only) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int b = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwave = NT >> 6;
@@ -1379,7 +1380,7 @@ __global__ void __launch_bounds__(NT) k_info(DevState<T> st, FeatBatch<T> fb, Up
     for (int i = tid; i < Cmax; i += NT) chosen[i] = 0;
 
     // ---- assembly ----
-    const int fbeg = fb.feat_off[b], fend = fb.feat_off[b + 1];
+    const int fbeg = fb.feat_off[b], fend = (phases & 1) ? fb.feat_off[b + 1] : fbeg;
     for (int f0 = fbeg; f0 < fend; f0 += INFO_FB) {
         for (int s = wave; s < INFO_FB; s += nwave) {
             const int f = f0 + s;
@@ -1438,11 +1439,29 @@ __global__ void __launch_bounds__(NT) k_info(DevState<T> st, FeatBatch<T> fb, Up
         __syncthreads();
     }
 
-    // ---- augmented outer-product Cholesky with diagonal pivoting ----
     KT* F = ws.Hthin + (size_t)b * Cmax * (Cmax + 1);
     const int ldf = Cmax + 1;
+    if (assemble_only) {   // [A | b] for the Cholesky-form Kalman stage (msckf_kalman.hip)
+#pragma unroll
+        for (int m = 0; m < BPT; ++m) {
+            if (!act[m]) continue;
+#pragma unroll
+            for (int x = 0; x < 6; ++x)
+#pragma unroll
+                for (int y = 0; y < 6; ++y) {
+                    F[(size_t)(6 * I[m] + x) * ldf + 6 * J[m] + y] = a[m][x][y];
+                    F[(size_t)(6 * J[m] + y) * ldf + 6 * I[m] + x] = a[m][x][y];
+                }
+            if (I[m] == J[m])
+#pragma unroll
+                for (int x = 0; x < 6; ++x) F[(size_t)(6 * I[m] + x) * ldf + Cmax] = bv[m][x];
+        }
+        if (tid == 0) info[1] = C;
+        return;
+    }
+    // ---- augmented outer-product Cholesky with diagonal pivoting ----
     int k = 0;
-    for (; k < C; ++k) {
+    for (; k < ((phases & 2) ? C : 0); ++k) {
 #pragma unroll
         for (int m = 0; m < BPT; ++m)
             if (act[m] && I[m] == J[m])
@@ -1890,19 +1909,36 @@ static void launch_info_cfg(hipStream_t s, const DevState<T>& st, const FeatBatc
                                   (int)lds);
         attr = lds;
     }
-    hipLaunchKernelGGL((k_info<T, BPT, NT>), dim3(st.B), dim3(NT), lds, s, st, fb, ws, INFO_TOL_REL);
+    static int phases = -1;   // MSCKF_INFO_PHASES: profiling aid (bit0 assembly, bit1 factorisation)
+    if (phases < 0) {
+        const char* e = getenv("MSCKF_INFO_PHASES");
+        phases = e ? atoi(e) : 3;
+    }
+    hipLaunchKernelGGL((k_info<T, BPT, NT>), dim3(st.B), dim3(NT), lds, s, st, fb, ws, INFO_TOL_REL, phases,
+                       update_mode(ws.Cmax) == UPD_CHOL ? 1 : 0);
 }
 
-// Default: information assembly + pivoted Cholesky (k_info).  MSCKF_COMPRESS=qr
-// selects the round-1 QR row-merge (msckf_qr_merge.hip) for A/B runs.
-template <typename T>
-void launch_compress(hipStream_t s, const DevState<T>& st, const FeatBatch<T>& fb, const UpdWs<T>& ws) {
+// Update path (MSCKF_UPDATE env, for A/B runs):
+//   chol  (default) k_info assembles [A | b]; Cholesky-form Kalman stage
+//         (msckf_kalman.hip) -- when the cam capacity fits its register tiles
+//   pchol k_info assembles A and factors it by pivoted Cholesky into H_thin;
+//         Kalman stage on H_thin (k_hp ... k_pupdate)
+//   qr    round-1 QR row-merge into H_thin (msckf_qr_merge.hip); same Kalman
+int update_mode(int Cmax) {
     static int mode = -1;
     if (mode < 0) {
-        const char* e = getenv("MSCKF_COMPRESS");
-        mode = (e && e[0] == 'q') ? 1 : 0;
+        const char* e = getenv("MSCKF_UPDATE");
+        mode = UPD_CHOL;
+        if (e && e[0] == 'q') mode = UPD_QR;
+        if (e && e[0] == 'p') mode = UPD_PCHOL;
     }
-    if (mode == 1) {
+    if (mode == UPD_CHOL && !kalman_chol_supported(Cmax)) return UPD_PCHOL;
+    return mode;
+}
+
+template <typename T>
+void launch_compress(hipStream_t s, const DevState<T>& st, const FeatBatch<T>& fb, const UpdWs<T>& ws) {
+    if (update_mode(ws.Cmax) == UPD_QR) {
         launch_compress_qr<T>(s, st, fb, ws);
         return;
     }
@@ -1916,6 +1952,13 @@ void launch_compress(hipStream_t s, const DevState<T>& st, const FeatBatch<T>& f
 template <typename T>
 void launch_kalman(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const UpdWs<T>& ws,
                    KernelTimer* kt) {
+    if (update_mode(ws.Cmax) == UPD_CHOL) {
+        launch_kalman_chol<T>(s, st, prm, ws, kt);
+        kt->begin(s, "kalman_correct");
+        hipLaunchKernelGGL(k_correct<T>, dim3(st.B), dim3(64), 0, s, st, ws);
+        kt->end(s);
+        return;
+    }
     const int tc = (ws.Cmax + TB - 1) / TB, td = (st.Dmax + TB - 1) / TB;
     kt->begin(s, "kalman_hp");
     hipLaunchKernelGGL(k_hp<T>, dim3(td, tc, st.B), dim3(256), 0, s, st, ws);

@@ -91,6 +91,11 @@ template <typename T>
 void launch_compress(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const UpdWs<T>&);
 template <typename T>
 void launch_compress_qr(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const UpdWs<T>&);
+enum UpdateMode { UPD_CHOL = 0, UPD_PCHOL = 1, UPD_QR = 2 };
+int update_mode(int Cmax);
+bool kalman_chol_supported(int Cmax);
+template <typename T>
+void launch_kalman_chol(hipStream_t, const DevState<T>&, const Params<T>&, const UpdWs<T>&, KernelTimer*);
 template <typename T>
 void launch_kalman(hipStream_t, const DevState<T>&, const Params<T>&, const UpdWs<T>&, KernelTimer*);
 
