@@ -1335,8 +1335,13 @@ __global__ void k_select(DevState<T> st, FeatBatch<T> fb, UpdWs<T> ws, int row_c
 // problems) carry no information and produce no row.
 // Output: rows 0..n-1 of [F | r_F] in H_thin (KT), n = rank in info[1].
 // ===========================================================================
-constexpr int INFO_FB = 4;    // features staged per round
-constexpr int INFO_RS = 50;   // LDS doubles per (feature, cam) record (48 + pad)
+// features staged per round (one staging wave each): 4, or 2 when the
+// double-buffered slots of 4 would not fit in LDS
+__host__ __device__ constexpr int info_fb(int Nmax) { return Nmax <= 40 ? 4 : 2; }
+
+// Doubles per staging slot: a feature's M <= Nmax records copied contiguously,
+// rounded up to whole 1 KiB global_load_lds wave-instructions.
+__host__ __device__ constexpr int info_slot_doubles(int Nmax) { return (Nmax * OBG_STRIDE + 127) / 128 * 128; }
 
 template <typename T, int BPT, int NT>
 __global__ void __launch_bounds__(NT) k_info(DevState<T> st, FeatBatch<T> fb, UpdWs<T> ws, double tol_rel,
@@ -1350,11 +1355,13 @@ __global__ void __launch_bounds__(NT) k_info(DevState<T> st, FeatBatch<T> fb, Up
         if (tid == 0) info[1] = 0;
         return;
     }
-    double* rec = reinterpret_cast<double*>(smem_raw);                      // [FB][Nmax][RS]
-    double* fvec = rec + (size_t)INFO_FB * Nmax * INFO_RS;                   // [Cmax + 1]
+    const int SLOT = info_slot_doubles(Nmax), INFO_FB = info_fb(Nmax);
+    double* rec = reinterpret_cast<double*>(smem_raw);                      // [2][FB][SLOT]
+    double* fvec = rec + (size_t)2 * INFO_FB * SLOT;                         // [Cmax + 1]
     double* dval = fvec + Cmax + 1;                                          // [Cmax]
-    unsigned long long* mask = reinterpret_cast<unsigned long long*>(dval + Cmax);   // [FB]
-    int* chosen = reinterpret_cast<int*>(mask + INFO_FB);                    // [Cmax]
+    unsigned long long* mask = reinterpret_cast<unsigned long long*>(dval + Cmax);   // [2][FB]
+    int* chosen = reinterpret_cast<int*>(mask + 2 * INFO_FB);                // [Cmax]
+    int* pos = chosen + Cmax;                                                // [2][FB][Nmax] cam -> record
     __shared__ int s_p, s_stop;
     __shared__ double s_inv, s_d0;
 
@@ -1380,19 +1387,24 @@ __global__ void __launch_bounds__(NT) k_info(DevState<T> st, FeatBatch<T> fb, Up
     for (int i = tid; i < Cmax; i += NT) chosen[i] = 0;
 
     // ---- assembly ----
+    // Batches of FB features; wave s < FB stages feature f0 + s of the next
+    // batch while all waves accumulate the current one: a contiguous copy of
+    // its M records (global_load_lds, 16 B per lane), a cam -> record table
+    // and a cam bitmask.
     const int fbeg = fb.feat_off[b], fend = (phases & 1) ? fb.feat_off[b + 1] : fbeg;
-    for (int f0 = fbeg; f0 < fend; f0 += INFO_FB) {
+    auto stage = [&](int f0, int buf) {
         for (int s = wave; s < INFO_FB; s += nwave) {
             const int f = f0 + s;
+            int* ps = pos + (buf * INFO_FB + s) * Nmax;
             unsigned long long mk = 0;
+            int o0 = 0, M = 0;
             if (f < fend && fb.include[f]) {
-                const int o0 = fb.obs_off[f], M = fb.obs_off[f + 1] - o0;
-                if (lane < M) mk = 1ull << fb.obs_cam[o0 + lane];
-                const double* src = fb.obs_g + (size_t)o0 * OBG_STRIDE;
-                double* dst = rec + (size_t)s * Nmax * INFO_RS;
-                for (int e = lane; e < M * OBG_STRIDE; e += 64) {
-                    const int o = e / OBG_STRIDE, k = e - o * OBG_STRIDE;
-                    if (k < OBG_UB + 6) dst[fb.obs_cam[o0 + o] * INFO_RS + k] = src[e];
+                o0 = fb.obs_off[f];
+                M = fb.obs_off[f + 1] - o0;
+                if (lane < M) {
+                    const int cam = fb.obs_cam[o0 + lane];
+                    mk = 1ull << cam;
+                    ps[cam] = lane;
                 }
             }
             unsigned lo = (unsigned)mk, hi = (unsigned)(mk >> 32);
@@ -1401,17 +1413,33 @@ __global__ void __launch_bounds__(NT) k_info(DevState<T> st, FeatBatch<T> fb, Up
                 lo |= (unsigned)__shfl_xor((int)lo, w, 64);
                 hi |= (unsigned)__shfl_xor((int)hi, w, 64);
             }
-            if (lane == 0) mask[s] = ((unsigned long long)hi << 32) | lo;
+            if (lane == 0) mask[buf * INFO_FB + s] = ((unsigned long long)hi << 32) | lo;
+            // after every ordinary global load above: the copy below may stay in flight
+            const char* src = reinterpret_cast<const char*>(fb.obs_g + (size_t)o0 * OBG_STRIDE);
+            double* dst = rec + (size_t)(buf * INFO_FB + s) * SLOT;
+            const int nchunk = M * OBG_STRIDE / 2;   // 16-byte chunks
+            for (int c0 = 0; c0 < nchunk; c0 += 64) {
+                if (c0 + lane < nchunk)
+                    __builtin_amdgcn_global_load_lds((const void*)(src + 16 * (size_t)(c0 + lane)),
+                                                     (void*)(dst + 2 * c0), 16, 0, 0);
+            }
         }
-        __syncthreads();
+    };
+    if (fbeg < fend) stage(fbeg, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int f0 = fbeg, it = 0; f0 < fend; f0 += INFO_FB, ++it) {
+        const int buf = it & 1;
+        if (f0 + INFO_FB < fend) stage(f0 + INFO_FB, buf ^ 1);
         for (int s = 0; s < INFO_FB; ++s) {
-            const unsigned long long mk = mask[s];
-            const double* rs = rec + (size_t)s * Nmax * INFO_RS;
+            const unsigned long long mk = mask[buf * INFO_FB + s];
+            const int* ps = pos + (buf * INFO_FB + s) * Nmax;
+            const double* rs = rec + (size_t)(buf * INFO_FB + s) * SLOT;
 #pragma unroll
             for (int m = 0; m < BPT; ++m) {
                 if (!act[m] || !((mk >> I[m]) & (mk >> J[m]) & 1ull)) continue;
-                const double* gi = rs + I[m] * INFO_RS;
-                const double* gj = rs + J[m] * INFO_RS;
+                const double* gi = rs + ps[I[m]] * OBG_STRIDE;
+                const double* gj = rs + ps[J[m]] * OBG_STRIDE;
 #pragma unroll
                 for (int t = 0; t < 3; ++t) {
                     double u[6], v[6];
@@ -1436,6 +1464,7 @@ __global__ void __launch_bounds__(NT) k_info(DevState<T> st, FeatBatch<T> fb, Up
                 }
             }
         }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
 
@@ -1901,8 +1930,9 @@ constexpr double INFO_TOL_REL = 1e-11;
 
 template <typename T, int BPT, int NT>
 static void launch_info_cfg(hipStream_t s, const DevState<T>& st, const FeatBatch<T>& fb, const UpdWs<T>& ws) {
-    const size_t lds = ((size_t)INFO_FB * st.Nmax * INFO_RS + 2 * (size_t)ws.Cmax + 1) * sizeof(double) +
-                       INFO_FB * sizeof(unsigned long long) + (size_t)ws.Cmax * sizeof(int);
+    const int fbn = info_fb(st.Nmax);
+    const size_t lds = ((size_t)2 * fbn * info_slot_doubles(st.Nmax) + 2 * (size_t)ws.Cmax + 1) * sizeof(double) +
+                       2 * fbn * sizeof(unsigned long long) + ((size_t)ws.Cmax + 2 * fbn * st.Nmax) * sizeof(int);
     static size_t attr = 64 * 1024;   // dynamic LDS granted so far (default 64 KB)
     if (lds > attr) {
         (void)hipFuncSetAttribute((const void*)k_info<T, BPT, NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
