@@ -36,10 +36,15 @@ __device__ __forceinline__ int round4(int x) { return (x + 3) & ~3; }
 //      panel rows (one row per thread): W = A_panel L_d^-T -> LDS + panel()
 //   3. every tile right of the panel takes A -= W_i W_l^T from registers
 // Two barriers per step.  Tiles in columns >= nelim end as the Schur
-// complement and are handed to trail().
+// complement and are handed to trail().  In the LDS column buffer each 4-row
+// block takes RB = 18 doubles (144 B): consecutive lanes read consecutive
+// blocks with ds_read_b128, and a 144-B stride spreads a 16-lane group over
+// all 64 banks (a 128-B stride would put it on two).
 // load(i, j) must be symmetric on the square part (diagonal tiles read both
 // triangles).
 // ===========================================================================
+constexpr int RB = 18;   // doubles per 4-row block of the LDS column buffer
+
 template <int NT, int TPL, class Load, class Panel, class Trail>
 __device__ __forceinline__ bool rchol_core(int nrow, int ncol, int nelim, double* lds, Load load, Panel panel,
                                            Trail trail) {
@@ -71,18 +76,18 @@ __device__ __forceinline__ bool rchol_core(int nrow, int ncol, int nelim, double
     }
     bool fail = false;
     for (int tj = 0; tj < nelim; ++tj) {
-        double* buf = lds + (tj & 1) * 16 * nrow;   // [4 nrow][4]
+        double* buf = lds + (tj & 1) * RB * nrow;   // [nrow][RB]: rows 4 t + x at RB t + 4 x
 #pragma unroll
         for (int s = 0; s < TPL; ++s) {
             if (!ROK(s) || RTL(s) != tj) continue;
-            double* dst = buf + 16 * RTI(s);
+            double* dst = buf + RB * RTI(s);
 #pragma unroll
             for (int x = 0; x < 4; ++x)
 #pragma unroll
                 for (int y = 0; y < 4; ++y) dst[4 * x + y] = a[s][x][y];
         }
         LDS_BARRIER();
-        const double* dt = buf + 16 * tj;
+        const double* dt = buf + RB * tj;
         const double l00 = sqrt(dt[0]);
         const double i00 = 1.0 / l00;
         const double l10 = dt[4] * i00, l20 = dt[8] * i00, l30 = dt[12] * i00;
@@ -96,7 +101,7 @@ __device__ __forceinline__ bool rchol_core(int nrow, int ncol, int nelim, double
         const double i33 = 1.0 / l33;
         if (!(l00 > 0.0) || !(l11 > 0.0) || !(l22 > 0.0) || !(l33 > 0.0)) { fail = true; break; }
         for (int r = 4 * tj + 4 + tid; r < 4 * nrow; r += NT) {
-            double* row = buf + 4 * r;
+            double* row = buf + RB * (r >> 2) + 4 * (r & 3);
             const double w0 = row[0] * i00;
             const double w1 = (row[1] - w0 * l10) * i11;
             const double w2 = (row[2] - w0 * l20 - w1 * l21) * i22;
@@ -116,8 +121,8 @@ __device__ __forceinline__ bool rchol_core(int nrow, int ncol, int nelim, double
         for (int s = 0; s < TPL; ++s) {
             if (tlmax[s] <= tj) continue;   // slot entirely in finished columns
             if (!ROK(s) || RTL(s) <= tj) continue;
-            const double* ri = buf + 16 * RTI(s);
-            const double* rl = buf + 16 * RTL(s);
+            const double* ri = buf + RB * RTI(s);
+            const double* rl = buf + RB * RTL(s);
             double u[4][4], w[4][4];
 #pragma unroll
             for (int x = 0; x < 4; ++x)
@@ -148,7 +153,7 @@ __device__ __forceinline__ bool rchol_core(int nrow, int ncol, int nelim, double
     return !fail;
 }
 
-__host__ __device__ constexpr int rchol_lds_doubles(int nrow) { return 2 * 16 * nrow; }
+__host__ __device__ constexpr int rchol_lds_doubles(int nrow) { return 2 * RB * nrow; }
 
 // ---- stage A: [P_cc P_ci; P_ic P_ii] in index space [cams (Cp) | IMU (24)] ----
 template <typename T, int NT, int TPL>

@@ -1085,9 +1085,14 @@ __global__ void __launch_bounds__(256) k_gate_lds(DevState<T> st, Params<T> prm,
 // whose tiles all lie in finished columns are skipped.  The last tile's owner
 // finishes with the three negative pivots.  No workgroup barriers:
 // 4 independent features per 256-thread workgroup.
+// Panel buffers hold one 4x4 block per tile row, padded to GB floats (80 B) /
+// doubles (144 B) so that consecutive lanes' ds_read_b128 of consecutive
+// blocks hit distinct banks.
+template <typename T>
+__host__ __device__ constexpr int gate_blk() { return sizeof(T) == 8 ? 18 : 20; }
 template <typename T>
 __host__ __device__ constexpr int gate_wave_lds_T(int Mmax) {
-    return 24 * Mmax + 8 * (4 * Mmax + 4);   // hx, panel rows (raw -> W D^-1), W^T blocks
+    return 24 * Mmax + 2 * gate_blk<T>() * (Mmax + 1);   // hx, panel rows (raw -> W D^-1), W^T blocks
 }
 
 template <typename T, int TPL>
@@ -1107,10 +1112,11 @@ __global__ void __launch_bounds__(256) k_gate_wave(DevState<T> st, Params<T> prm
     }
     const int b = fb.feat_filter[f];
     const int o0 = fb.obs_off[f], M = fb.obs_off[f + 1] - o0;
-    const int nT = M + 1, ntiles = nT * (nT + 1) / 2, L4 = 4 * Mmax + 4;
+    const int nT = M + 1, ntiles = nT * (nT + 1) / 2;
     T* hx = reinterpret_cast<T*>(smem_raw) + (size_t)wv * gate_wave_lds_T<T>(Mmax);
-    T* wd = hx + 24 * Mmax;     // [L4][4]  panel rows: raw tile rows, then W D^-1
-    T* wt = wd + 4 * L4;        // [L4/4][4][4]  W^T per 4-row block: wt[blk][c][y] = W[4 blk + y][c]
+    constexpr int GB = gate_blk<T>();
+    T* wd = hx + 24 * Mmax;           // [nT][GB]  panel rows: raw tile rows, then W D^-1
+    T* wt = wd + GB * (Mmax + 1);     // [nT][GB]  W^T per 4-row block: wt[blk][4 c + y] = W[4 blk + y][c]
     int* slot = reinterpret_cast<int*>(reinterpret_cast<T*>(smem_raw) + 4 * gate_wave_lds_T<T>(Mmax)) + wv * Mmax;
     const T* ws = fb.obs_ws + (size_t)o0 * OBS_WS;
     for (int e = lane; e < 24 * M; e += 64) {
@@ -1200,7 +1206,7 @@ __global__ void __launch_bounds__(256) k_gate_wave(DevState<T> st, Params<T> prm
 #pragma unroll
         for (int s = 0; s < TPL; ++s) {
             if (!OK(s) || TL(s) != tj) continue;
-            T* dst = wd + 16 * TI(s);
+            T* dst = wd + GB * TI(s);
 #pragma unroll
             for (int x = 0; x < 4; ++x)
 #pragma unroll
@@ -1208,7 +1214,7 @@ __global__ void __launch_bounds__(256) k_gate_wave(DevState<T> st, Params<T> prm
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         // 2. every lane factors the diagonal tile (uniform): A_d = L_d D L_d^T
-        const T* dt = wd + 16 * tj;
+        const T* dt = wd + GB * tj;
         const T d0 = dt[0];
         const T l10 = dt[4] / d0, l20 = dt[8] / d0, l30 = dt[12] / d0;
         const T d1 = dt[5] - l10 * l10 * d0;
@@ -1222,13 +1228,13 @@ __global__ void __launch_bounds__(256) k_gate_wave(DevState<T> st, Params<T> prm
         // 3. panel rows below the diagonal tile: W = A L_d^-T; store W D^-1 by
         //    row and W transposed by 4-row block
         for (int q = 4 * tj + 4 + lane; q < 4 * nT; q += 64) {
-            T* row = wd + 4 * q;
+            T* row = wd + GB * (q >> 2) + 4 * (q & 3);
             const T w0 = row[0];
             const T w1 = row[1] - w0 * l10;
             const T w2 = row[2] - w0 * l20 - w1 * l21;
             const T w3 = row[3] - w0 * l30 - w1 * l31 - w2 * l32;
             row[0] = w0 * e0; row[1] = w1 * e1; row[2] = w2 * e2; row[3] = w3 * e3;
-            T* col = wt + 16 * (q >> 2) + (q & 3);
+            T* col = wt + GB * (q >> 2) + (q & 3);
             col[0] = w0; col[4] = w1; col[8] = w2; col[12] = w3;
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1237,8 +1243,8 @@ __global__ void __launch_bounds__(256) k_gate_wave(DevState<T> st, Params<T> prm
         for (int s = 0; s < TPL; ++s) {
             if (tlmax[s] <= tj) continue;   // slot entirely in finished columns
             if (!OK(s) || TL(s) <= tj) continue;
-            const T* ri = wd + 16 * TI(s);
-            const T* cl = wt + 16 * TL(s);
+            const T* ri = wd + GB * TI(s);
+            const T* cl = wt + GB * TL(s);
             T u[4][4], w[4][4];
 #pragma unroll
             for (int x = 0; x < 4; ++x)
