@@ -2,9 +2,9 @@
 
 One "step" = one batched EKF measurement update of B independent filters
 (SURVEY.md 8(d) unit of work): triangulation of every feature, per-feature
-Jacobian + nullspace projection + chi2 gating, stacking (no row cap), QR
-compression and the Kalman / covariance update -- on inputs already resident in
-HBM.  Each step first restores the filters' pristine state on the device (a
+Jacobian + nullspace projection + chi2 gating, stacking (no row cap), the
+compression of the stacked rows (information assembly) and the
+Kalman / covariance update -- on inputs already resident in HBM.  Each step first restores the filters' pristine state on the device (a
 D2D copy that is counted inside the timed region) so every step does
 identical work.
 
@@ -74,24 +74,36 @@ def build_batch(args, rank):
     return ctx, probs
 
 
-def flops_model(probs, B, accepted, feat_off):
-    """Algorithmic flops of one step, per kernel, from the realised shapes.
-    'canonical' = SURVEY.md 8(d) per-update formula (dense Householder QR on
+def flops_model(probs, B, accepted, valid, feat_off):
+    """Algorithmic flops of one step, per kernel-timer stage, from the realised
+    shapes (FMA = 2 flops; DESIGN.md 'Kernels' states each formula), plus
+    'canonical' = SURVEY.md 8(d)'s per-update formula (dense Householder QR of
     the stacked R x C matrix, rows-space gating)."""
-    tot = {"canonical": 0.0, "compress": 0.0, "gate": 0.0}
+    tot = {"canonical": 0.0, "gate": 0.0, "compress": 0.0, "kalman_a": 0.0, "kalman_b": 0.0,
+           "kalman_c": 0.0, "kalman_e": 0.0}
     for b in range(B):
         p = probs[b % len(probs)]
         C = 6 * p.N
         D = 21 + C
-        M = p.track_lengths()
-        acc = accepted[feat_off[b]:feat_off[b + 1]]
+        Cp = (C + 3) // 4 * 4
+        M = p.track_lengths().astype(float)
+        acc = accepted[feat_off[b]:feat_off[b + 1]].astype(float)
+        val = valid[feat_off[b]:feat_off[b + 1]].astype(float)
         k = 4 * M - 3
-        # gating as the kernel does it: Y blocks (480 M^2 / 2 pair flops x2), 3 two-sided reflectors, Cholesky
-        tot["gate"] += float(np.sum(480.0 * M * (M + 1) / 2 + 3 * 6 * (4 * M) ** 2 + k ** 3 / 3 + 2 * k ** 2))
-        # compress: per included feature, each of its k rows is merged column by column from its first cam
-        c0 = 6 * np.array([p.obs_cam[p.obs_off[f]:p.obs_off[f + 1]].min() for f in range(p.F)])
-        w = (C - c0).astype(float)
-        tot["compress"] += float(np.sum(acc * 2.0 * k * w * (w + 1)))
+        # gating: Y tiles (4x6 . 6x6 . 6x4 per cam pair) + blocked LDL^T of the (4M+4)^2 saddle-point matrix
+        tot["gate"] += 2 * float(np.sum(val * (240.0 * M * (M + 1) / 2 + (4 * M + 4) ** 3 / 6)))
+        # information assembly: per included feature, every observed cam pair takes G_i^T G_j (3 x 6 x 6)
+        tot["compress"] += 2 * float(np.sum(acc * (54.0 * M * (M + 1) + 27 * M)))
+        if acc.sum() > 0:
+            N = Cp + 24
+            tot["kalman_a"] += 2 * (N ** 3 - (N - Cp) ** 3) / 6
+            tot["kalman_b"] += 2 * (C ** 3 / 2 + C ** 3 / 6 + C * C / 2)
+            ER = (22 + C + 3) // 4
+            nTc = Cp // 4
+            ner_max = (2048 - nTc * (nTc + 1) // 2) // nTc
+            groups = -(-ER // ner_max)
+            tot["kalman_c"] += 2 * (groups * Cp ** 3 / 6 + (22 + C) * Cp * Cp / 2)
+            tot["kalman_e"] += 2 * (D * (D + 1) / 2 * C + D * C)
         R = float(np.sum(k * acc))
         n = min(R, C)
         F_proj = float(np.sum(48.0 * M * (6 * M + 1)))
@@ -100,6 +112,20 @@ def flops_model(probs, B, accepted, feat_off):
         F_kal = 2 * n * C * D + 2 * n * n * C + n ** 3 / 3 + 2 * n * n * D + 2 * n * D + 2 * n * D * D + D * D
         tot["canonical"] += F_proj + F_gate + F_qr + F_kal
     return tot
+
+
+def pmc_traffic(stage, dtype):
+    """HBM bytes per step of a stage's kernels from the committed rocprofv3 PMC
+    summary (tools/pmc_summary.py; FETCH_SIZE and WRITE_SIZE from separate
+    passes), or None if no summary covers them."""
+    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as fh:
+        summ = json.load(fh)
+    if summ.get("dtype") != dtype:
+        return None
+    return summ.get("stages", {}).get(stage, {}).get("bytes_per_step")
 
 
 def cpu_baseline(args, probs):
@@ -124,7 +150,7 @@ def cpu_baseline(args, probs):
     if lim is not None:
         lim.unregister() if hasattr(lim, "unregister") else None
     return {"value": done / el, "unit": "updates/s", "cores": 1, "kind": "port",
-            "sample": "%d synthetic %dx%d updates (triangulation + jacobian + gating + QR + Kalman), "
+            "sample": "%d synthetic %dx%d updates (triangulation + jacobian + gating + QR + Kalman as in the reference), "
                       "numpy/OpenBLAS 1 thread, oracle/msckf_oracle.py" % (done, args.N, args.F)}
 
 
@@ -169,34 +195,38 @@ def main():
     updates = args.batch * world * args.steps
     value = updates / el
     feat_off = np.concatenate([[0], np.cumsum([probs[b % len(probs)].F for b in range(args.batch)])])
-    fl = flops_model(probs, args.batch, acc, feat_off)
-    # dominant kernel by device time
+    fl = flops_model(probs, args.batch, acc, valid, feat_off)
+    # dominant stage by device time (HIP events on the launch stream, timed region only)
     kern = {k: v for k, v in times.items() if k != "restore"}
     dom = max(kern, key=lambda k: kern[k][0])
-    dom_ms = kern[dom][0] / max(kern[dom][1], 1)
-    dom_flops = fl.get(dom.replace("kalman_", ""), None)
-    peak = FP32_PEAK_TFLOPS if args.dtype == "fp32" else FP64_PEAK_TFLOPS
+    dom_ms = kern[dom][0] / args.steps                  # device ms of the stage per step (all its launches)
+    dom_flops = fl.get(dom)
+    # gating computes in the context's scalar type; projection, assembly and Kalman stages in fp64
+    peak = (FP32_PEAK_TFLOPS if args.dtype == "fp32" else FP64_PEAK_TFLOPS) if dom == "gate" else FP64_PEAK_TFLOPS
     roof = None
     if dom_flops:
         ach = dom_flops / (dom_ms * 1e-3) / 1e12
+        traffic = pmc_traffic(dom, args.dtype)
         roof = {"bound": "mfma", "kernel": dom, "achieved": round(ach, 3), "peak": peak, "unit": "TFLOP/s",
-                "frac": round(ach / peak, 5), "traffic": None, "avg_launch_ms": round(dom_ms, 4),
-                "flops_per_launch": dom_flops}
+                "frac": round(ach / peak, 5), "traffic": traffic, "ms_per_step": round(dom_ms, 4),
+                "flops_per_step": dom_flops,
+                "note": "vector-ALU peak of the stage's arithmetic type (fp64 vector = fp64 matrix peak on MI355X); "
+                        "traffic = PMC FETCH_SIZE+WRITE_SIZE bytes per step from profiles/pmc_summary.json"}
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "updates/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "f32" if args.dtype == "fp32" else "f64",
+        "dtype": "f32/f64" if args.dtype == "fp32" else "f64",
         "data": "synthetic (SURVEY.md 8(d) generator: %d distinct problems tiled over %d filters per GPU)"
                 % (len(probs), args.batch),
         "config": {"workload": "batched EKF measurement update, %d cam-states x %d features, %d filters/GPU, "
-                               "triangulation + jacobian + gating + QR + Kalman, no row cap" % (args.N, args.F, args.batch),
+                               "triangulation + jacobian + gating + information assembly + Kalman, no row cap"
+                               % (args.N, args.F, args.batch),
                    "cam_states": args.N, "features": args.F, "filters_per_gpu": args.batch,
                    "stacked_rows_mean": float(np.mean(rows)), "parallelism": "replicas%d" % world},
         "roofline": roof,
         "kernel_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in sorted(times.items(), key=lambda kv: -kv[1][0])},
         "canonical_gflop_per_update": round(fl["canonical"] / args.batch / 1e9, 4),
-        "canonical_tflops": round(fl["canonical"] * args.steps * world / el / 1e12, 3),
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args, probs)

@@ -1,0 +1,83 @@
+"""Summarise rocprofv3 FETCH_SIZE / WRITE_SIZE passes into profiles/pmc_summary.json.
+
+    python tools/pmc_summary.py FETCH.csv WRITE.csv --steps K --dtype fp32 [-o profiles/pmc_summary.json]
+
+FETCH.csv / WRITE.csv are the counter_collection CSVs of two separate
+`rocprofv3 --pmc FETCH_SIZE` / `--pmc WRITE_SIZE` runs of the same
+`bench.py --steps K --warmup 0` command (the two TCC counters do not fit in
+one pass on gfx950).  Counter values are KiB per dispatch.  Kernels are
+grouped into the bench's timer stages; bytes_per_step = (FETCH + WRITE) * 1024
+summed over a stage's dispatches / K.  Per MI355X_MICROARCH.md, FETCH_SIZE on
+gfx950 reads half of a 16-B-per-lane streaming read and other access widths
+are uncalibrated, so `fetch_x2_bytes_per_step` gives the upper estimate.
+"""
+import argparse
+import csv
+import json
+import re
+from collections import defaultdict
+
+STAGES = [
+    ("triangulate", r"k_triangulate"),
+    ("feature_jacobian", r"k_feature"),
+    ("gate", r"k_gate"),
+    ("select", r"k_select"),
+    ("compress", r"k_info|k_compress|k_widen"),
+    ("kalman_a", r"k_kal_a"),
+    ("kalman_b", r"k_kal_b"),
+    ("kalman_c", r"k_kal_c"),
+    ("kalman_e", r"k_kal_e"),
+    ("kalman_correct", r"k_correct"),
+]
+
+
+def stage_of(name):
+    for st, pat in STAGES:
+        if re.search(pat, name):
+            return st
+    return None
+
+
+def read(path):
+    out = defaultdict(float)
+    count = defaultdict(int)
+    for row in csv.DictReader(open(path)):
+        name = row["Kernel_Name"]
+        out[name] += float(row["Counter_Value"])
+        count[name] += 1
+    return out, count
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("fetch")
+    ap.add_argument("write")
+    ap.add_argument("--steps", type=int, required=True)
+    ap.add_argument("--dtype", default="fp32")
+    ap.add_argument("-o", "--out", default="profiles/pmc_summary.json")
+    ap.add_argument("--source", default="")
+    a = ap.parse_args()
+    fetch, nf = read(a.fetch)
+    write, nw = read(a.write)
+    stages = {}
+    for name in sorted(set(fetch) | set(write)):
+        st = stage_of(name)
+        if st is None:
+            continue
+        d = stages.setdefault(st, {"fetch_kib": 0.0, "write_kib": 0.0, "kernels": {}})
+        d["fetch_kib"] += fetch.get(name, 0.0)
+        d["write_kib"] += write.get(name, 0.0)
+        short = re.sub(r"\(.*", "", name).replace("void msckf::", "")
+        d["kernels"][short] = {"dispatches": nf.get(name, nw.get(name, 0)),
+                               "fetch_kib": fetch.get(name, 0.0), "write_kib": write.get(name, 0.0)}
+    for st, d in stages.items():
+        d["bytes_per_step"] = (d["fetch_kib"] + d["write_kib"]) * 1024 / a.steps
+        d["fetch_x2_bytes_per_step"] = (2 * d["fetch_kib"] + d["write_kib"]) * 1024 / a.steps
+    json.dump({"dtype": a.dtype, "steps": a.steps, "source": a.source, "unit": "bytes",
+               "stages": stages}, open(a.out, "w"), indent=1, sort_keys=True)
+    for st, d in sorted(stages.items(), key=lambda kv: -kv[1]["bytes_per_step"]):
+        print("%-18s %10.3f GB/step" % (st, d["bytes_per_step"] / 1e9))
+
+
+if __name__ == "__main__":
+    main()
