@@ -25,7 +25,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 import msckf_pkg  # noqa: E402,F401
-from msckf_amd import synth, FilterConfig, CHI2_05  # noqa: E402
+from msckf_amd import synth, replicas, FilterConfig, CHI2_05  # noqa: E402
 from msckf_amd._lib import Context, pack_imu, pack_cams  # noqa: E402
 
 METRIC = "EKF measurement updates/sec at 30 cam-states x 200 features; ATE RMSE vs ref"
@@ -49,12 +49,12 @@ def parse():
     return ap.parse_args()
 
 
-def build_batch(args, rank):
-    probs = [synth.make_update_problem(args.N, args.F, seed=1000 * rank + u) for u in range(min(args.unique, args.batch))]
+def build_batch(args, rank, local_rank):
+    probs = [synth.make_update_problem(args.N, args.F, seed=sd)
+             for sd in replicas.problem_seeds(rank, min(args.unique, args.batch))]
     B = args.batch
     dtype = np.float32 if args.dtype == "fp32" else np.float64
-    ctx = Context(FilterConfig(), n_filters=B, n_cam_capacity=args.N, dtype=dtype,
-                  device=int(os.environ.get("LOCAL_RANK", 0)))
+    ctx = Context(FilterConfig(), n_filters=B, n_cam_capacity=args.N, dtype=dtype, device=local_rank)
     feat_off, obs_off, cams, zs, chi = [0], [0], [], [], []
     for b in range(B):
         p = probs[b % len(probs)]
@@ -156,20 +156,10 @@ def cpu_baseline(args, probs):
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as dist
-        lr = int(os.environ.get("LOCAL_RANK", 0))
-        torch.cuda.set_device(lr)
-        dist.init_process_group("nccl")
-    ctx, probs = build_batch(args, rank)
-
-    def barrier():
-        if dist is not None:
-            dist.barrier()
+    grp = replicas.init("nccl")      # replicas only: RCCL carries the barriers and the max of the timing
+    world, rank = grp.world, grp.rank
+    ctx, probs = build_batch(args, rank, grp.local_rank)
+    barrier = grp.barrier
 
     for _ in range(args.warmup):
         ctx.restore()
@@ -187,13 +177,8 @@ def main():
     barrier()
     el = time.perf_counter() - t0
     times = ctx.kernel_times()
-    if dist is not None:
-        import torch
-        t = torch.tensor([el], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
-    updates = args.batch * world * args.steps
-    value = updates / el
+    el = grp.max_over_ranks(el)
+    value = replicas.whole_job_rate(args.batch, world, args.steps, el)
     feat_off = np.concatenate([[0], np.cumsum([probs[b % len(probs)].F for b in range(args.batch)])])
     fl = flops_model(probs, args.batch, acc, valid, feat_off)
     # dominant stage by device time (HIP events on the launch stream, timed region only)
@@ -233,8 +218,7 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     ctx.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    grp.close()
 
 
 if __name__ == "__main__":
