@@ -10,8 +10,9 @@ the IMU message buffer walk, the feature map and its observation dicts, cam-id
 keyframe selection, the online-reset decision and ``publish``.
 What runs on the GPU (through the C-ABI, libmsckf_hip.so): IMU covariance
 propagation, state augmentation, triangulation, measurement Jacobians +
-nullspace projection, gating, stacking, QR compression, the Kalman update and
-covariance compaction.  There is no CPU fallback.
+nullspace projection, gating, stacking, compression of the stacked rows
+(information assembly), the Kalman update and covariance compaction.  There is
+no CPU fallback.
 
 Differences from the reference that are deliberate:
 * the reference's IMU-buffer race between the IMU and vio threads
