@@ -75,6 +75,8 @@ struct msckf_ctx {
     std::vector<int> h_feat_off;
     DBuf<int> feat_filter, feat_off, obs_off, obs_cam, row_off, gate_list;
     GateClasses gc;
+    SegClasses sc;
+    DBuf<int> seg_list;
     DBuf<long long> ysq_off;
     DBuf<unsigned char> obs_z, chi2, p_w, obs_ws, obs_g, tau, ysq, gamma;
     DBuf<uint8_t> valid, accept, include;
@@ -154,6 +156,7 @@ FeatBatch<T> feat_batch(msckf_ctx* c) {
     f.valid = c->valid.p;
     f.obs_ws = reinterpret_cast<T*>(c->obs_ws.p);
     f.obs_g = reinterpret_cast<double*>(c->obs_g.p);
+    f.compact = feature_needs_compact(c->maxM, c->Cmax) ? 1 : 0;
     f.tau = reinterpret_cast<T*>(c->tau.p);
     f.ysq = reinterpret_cast<T*>(c->ysq.p);
     f.gamma = reinterpret_cast<T*>(c->gamma.p);
@@ -286,6 +289,24 @@ int load_features(msckf_ctx* c, int nf, const int32_t* feat_off, int single_filt
         HIPC(hipStreamSynchronize(s));
         c->gc = gc;
     }
+    {   // segment classes of the per-feature kernels (M <= S)
+        std::vector<int> flat;
+        SegClasses sc;
+        for (int k = 0; k < SegClasses::NC; ++k) {
+            sc.off[k] = (int)flat.size();
+            for (int f = 0; f < nf; ++f) {
+                const int M = obs_off[f + 1] - obs_off[f];
+                if (M <= SegClasses::S[k] && (k == 0 || M > SegClasses::S[k - 1])) flat.push_back(f);
+            }
+        }
+        sc.off[SegClasses::NC] = (int)flat.size();
+        HIPC(c->seg_list.ensure(flat.size() + 1));
+        if (!flat.empty())
+            HIPC(hipMemcpyAsync(c->seg_list.p, flat.data(), flat.size() * sizeof(int), hipMemcpyHostToDevice, s));
+        HIPC(hipStreamSynchronize(s));
+        sc.list = c->seg_list.p;
+        c->sc = sc;
+    }
     HIPC(hipStreamSynchronize(s));
     HIPC(upload<T>(c, c->obs_z.p, obs_z, nobs * 4));
     if (chi2) {
@@ -320,7 +341,7 @@ int run_update_chain(msckf_ctx* c, int row_cap, bool triangulate) {
         c->timer.end(s);
     }
     c->timer.begin(s, "feature_jacobian");
-    launch_feature<T>(s, st, prm, fb);
+    launch_feature<T>(s, st, prm, fb, c->sc);
     c->timer.end(s);
     c->timer.begin(s, "gate");
     launch_gate<T>(s, st, prm, fb, c->gc);
@@ -609,7 +630,7 @@ int msckf_destroy(msckf_ctx_t* c) {
                     &c->dx, &c->obs_z, &c->chi2, &c->p_w, &c->obs_ws, &c->obs_g, &c->tau, &c->ysq, &c->gamma, &c->scratch})
         b->release();
     for (auto* b : {&c->ncams, &c->ncams_snap, &c->info, &c->feat_filter, &c->feat_off, &c->obs_off, &c->obs_cam,
-                    &c->row_off, &c->iscratch, &c->gate_list})
+                    &c->row_off, &c->iscratch, &c->gate_list, &c->seg_list})
         b->release();
     c->ysq_off.release();
     c->valid.release();

@@ -70,6 +70,7 @@ struct FeatBatch {
     uint8_t* valid;           // [nf] triangulation validity (1 if p_w given)
     T* obs_ws;                // [sum M][OBS_WS]
     double* obs_g;            // [sum M][OBG_STRIDE] Gram terms (fp64)
+    int compact;              // write V / W / Q^T r / tau (LDS gate fallback, QR path)
     T* tau;                   // [nf][4]
     T* ysq;                   // gating scratch
     T* gamma;                 // [nf]

@@ -621,9 +621,11 @@ __global__ void __launch_bounds__(256) k_triangulate(DevState<T> st, Params<T> p
 }
 
 // ===========================================================================
-// Feature Jacobian + left-nullspace projection: one wavefront per feature,
-// lane i owns observation i (M <= 64: a feature is seen at most once per cam
-// state and the cam capacity is <= 64).  Computes the observability-projected
+// Feature Jacobian + left-nullspace projection: one S-lane segment of a
+// wavefront per feature (64/S features per wavefront, S = 8..64 by size class
+// so short tracks do not leave most lanes idle), lane i of the segment owns
+// observation i (M <= 64: a feature is seen at most once per cam state and the
+// cam capacity is <= 64).  Computes the observability-projected
 // 4x6 / 4x3 blocks and residual, Householder-QRs H_f (4M x 3) across the wave
 // with xor-shuffle reductions (LAPACK dlarfg sign convention), and stores
 //   * in T, for gating: the compact factors of H0 = (Q^T Hx)[3:] =
@@ -637,17 +639,43 @@ __global__ void __launch_bounds__(256) k_triangulate(DevState<T> st, Params<T> p
 // The nullspace basis differs from the reference's SVD basis by an orthogonal
 // transform, to which gating and the update are invariant (quirk Q4).
 // ===========================================================================
-template <typename T>
+// Sum over aligned S-lane segments of the wavefront (xor shuffles stay inside
+// a segment for offsets < S).
+template <int S, typename T>
+__device__ __forceinline__ T seg_sum(T x) {
+#pragma unroll
+    for (int m = S >> 1; m >= 1; m >>= 1) x += __shfl_xor(x, m, 64);
+    return x;
+}
+
+// Store n (even) values as 2-element vectors (8-byte float2 / 16-byte double2
+// stores; rows of obs_ws / obs_g keep that alignment).
+template <typename T, typename S>
+__device__ __forceinline__ void store_pairs(T* dst, const S* src, int n) {
+    using V2 = T __attribute__((ext_vector_type(2)));
+    V2* d = reinterpret_cast<V2*>(dst);
+    for (int e = 0; e < n; e += 2) {
+        V2 v;
+        v.x = (T)src[e];
+        v.y = (T)src[e + 1];
+        d[e >> 1] = v;
+    }
+}
+
+template <typename T, int S>
 __global__ void __launch_bounds__(256) k_feature(DevState<T> st, Params<T> prm, FeatBatch<T> fb,
-                                                 int f0, int nfeat) {
+                                                 const int* __restrict__ flist, int cnt) {
     using CT = double;
-    const int lane = threadIdx.x & 63;
-    const int f = f0 + blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    if (f >= f0 + nfeat) return;
-    if (!fb.valid[f]) return;
+    constexpr int PER = 64 / S;   // features per wavefront, one S-lane segment each
+    const int lane = threadIdx.x & 63, l = lane & (S - 1), b0 = lane & ~(S - 1);
+    const int wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (wid * PER >= cnt) return;
+    const int li = wid * PER + lane / S;
+    const int f = li < cnt ? flist[li] : 0;
+    const bool fvalid = li < cnt && fb.valid[f];
     const int b = fb.feat_filter[f];
-    const int o0 = fb.obs_off[f], M = fb.obs_off[f + 1] - o0;
-    const bool own = lane < M;
+    const int o0 = fb.obs_off[f], M = fvalid ? fb.obs_off[f + 1] - o0 : 0;
+    const bool own = l < M;
     const T* cams = st.cams + (size_t)b * st.Nmax * CAM_STRIDE;
     CT g[3], R01[9], t01[3];
     for (int k = 0; k < 3; ++k) {
@@ -661,8 +689,8 @@ __global__ void __launch_bounds__(256) k_feature(DevState<T> st, Params<T> prm, 
     for (int e = 0; e < 12; ++e) Hf[e] = 0;
     for (int e = 0; e < 4; ++e) r[e] = 0;
     if (own) {
-        const T* c = cams + (size_t)fb.obs_cam[o0 + lane] * CAM_STRIDE;
-        const T* z = fb.obs_z + (size_t)(o0 + lane) * 4;
+        const T* c = cams + (size_t)fb.obs_cam[o0 + l] * CAM_STRIDE;
+        const T* z = fb.obs_z + (size_t)(o0 + l) * 4;
         CT q0[4], qn[4], cp[3];
         for (int k = 0; k < 4; ++k) { q0[k] = (CT)c[C_Q + k]; qn[k] = (CT)c[C_QN + k]; }
         for (int k = 0; k < 3; ++k) cp[k] = (CT)c[C_P + k];
@@ -719,20 +747,19 @@ __global__ void __launch_bounds__(256) k_feature(DevState<T> st, Params<T> prm, 
     }
     for (int c = 0; c < 6; ++c)   // Hx_i^T r_i, before r is reflected
         u6[c] = Hx[c] * r[0] + Hx[6 + c] * r[1] + Hx[12 + c] * r[2] + Hx[18 + c] * r[3];
-    if (own)
-        for (int e = 0; e < 4; ++e) fb.obs_ws[(size_t)(o0 + lane) * OBS_WS + OBS_R + e] = (T)r[e];
-    // ---- Householder QR of H_f across the wave (rows 4i..4i+3 in lane i) ----
+    if (own) store_pairs(fb.obs_ws + (size_t)(o0 + l) * OBS_WS + OBS_R, r, 4);
+    // ---- Householder QR of H_f across the wave (rows 4i..4i+3 in segment lane i) ----
     CT V[12];
     CT tau[3];
     for (int e = 0; e < 12; ++e) V[e] = 0;
     for (int j = 0; j < 3; ++j) {
-        CT alpha = __shfl(Hf[3 * j + j], 0, 64);   // pivot row j lives in lane 0
+        CT alpha = __shfl(Hf[3 * j + j], b0, 64);   // pivot row j lives in the segment's first lane
         CT xs = 0;
         for (int a = 0; a < 4; ++a) {
-            int row = 4 * lane + a;
+            int row = 4 * l + a;
             if (row > j && own) xs += Hf[3 * a + j] * Hf[3 * a + j];
         }
-        xs = wave_sum(xs);
+        xs = seg_sum<S>(xs);
         CT tj = 0, scale = 0, beta = alpha;
         if (xs != CT(0)) {
             CT nrm = sqrt(alpha * alpha + xs);
@@ -743,7 +770,7 @@ __global__ void __launch_bounds__(256) k_feature(DevState<T> st, Params<T> prm, 
         tau[j] = tj;
         // v_j: v[j] = 1, v[row > j] = Hf[row][j] * scale, 0 above
         for (int a = 0; a < 4; ++a) {
-            int row = 4 * lane + a;
+            int row = 4 * l + a;
             CT v = 0;
             if (own) v = row == j ? CT(1) : (row > j ? Hf[3 * a + j] * scale : CT(0));
             V[3 * a + j] = v;
@@ -752,7 +779,7 @@ __global__ void __launch_bounds__(256) k_feature(DevState<T> st, Params<T> prm, 
         for (int c = j + 1; c <= 3; ++c) {
             CT w = 0;
             for (int a = 0; a < 4; ++a) w += V[3 * a + j] * (c < 3 ? Hf[3 * a + c] : r[a]);
-            w = wave_sum(w);
+            w = seg_sum<S>(w);
             for (int a = 0; a < 4; ++a) {
                 if (c < 3) Hf[3 * a + c] -= tj * V[3 * a + j] * w;
                 else r[a] -= tj * V[3 * a + j] * w;
@@ -766,13 +793,13 @@ __global__ void __launch_bounds__(256) k_feature(DevState<T> st, Params<T> prm, 
         d20 += V[3 * a + 2] * V[3 * a];
         d21 += V[3 * a + 2] * V[3 * a + 1];
     }
-    d10 = wave_sum(d10);
-    d20 = wave_sum(d20);
-    d21 = wave_sum(d21);
-    // top 3 rows of V (all in lane 0) and g = (Q^T r)[0:3], broadcast
+    d10 = seg_sum<S>(d10);
+    d20 = seg_sum<S>(d20);
+    d21 = seg_sum<S>(d21);
+    // top 3 rows of V (all in the segment's first lane) and g = (Q^T r)[0:3], broadcast
     CT V0[9], gr[3];
-    for (int e = 0; e < 9; ++e) V0[e] = lane_bcast(V[e], 0);
-    for (int t = 0; t < 3; ++t) gr[t] = lane_bcast(r[t], 0);
+    for (int e = 0; e < 9; ++e) V0[e] = __shfl(V[e], b0, 64);
+    for (int t = 0; t < 3; ++t) gr[t] = __shfl(r[t], b0, 64);
     if (!own) return;
     CT W[18];
     for (int c = 0; c < 6; ++c) {
@@ -786,27 +813,30 @@ __global__ void __launch_bounds__(256) k_feature(DevState<T> st, Params<T> prm, 
         w2 -= tau[0] * d20 * w0 + tau[1] * d21 * w1;
         W[c] = w0; W[6 + c] = w1; W[12 + c] = w2;
     }
-    T* ws = fb.obs_ws + (size_t)(o0 + lane) * OBS_WS;
-    for (int e = 0; e < 24; ++e) ws[OBS_HX + e] = (T)Hx[e];
-    for (int e = 0; e < 12; ++e) ws[OBS_V + e] = (T)V[e];
-    for (int e = 0; e < 18; ++e) ws[OBS_W + e] = (T)W[e];
-    for (int e = 0; e < 4; ++e) ws[OBS_QR + e] = (T)r[e];
-    if (lane == 0)
-        for (int j = 0; j < 3; ++j) fb.tau[4 * f + j] = (T)tau[j];
+    T* ws = fb.obs_ws + (size_t)(o0 + l) * OBS_WS;
+    store_pairs(ws + OBS_HX, Hx, 24);
+    if (fb.compact) {   // compact factors: only the LDS / global gate and the QR merge read them
+        store_pairs(ws + OBS_V, V, 12);
+        store_pairs(ws + OBS_W, W, 18);
+        store_pairs(ws + OBS_QR, r, 4);
+        if (l == 0)
+            for (int j = 0; j < 3; ++j) fb.tau[4 * f + j] = (T)tau[j];
+    }
     // Gram terms.  (Q^T Hx)[t][i-block] = [i == 0] Hx_0[t] - sum_j tau_j V_0[t][j] W_j(i)
-    double* og = fb.obs_g + (size_t)(o0 + lane) * OBG_STRIDE;
-    CT G[18];
+    CT rec[OBG_STRIDE];   // G | DS | UB | pad, stored as 16-byte pairs
     for (int t = 0; t < 3; ++t)
         for (int c = 0; c < 6; ++c) {
-            CT v = lane == 0 ? Hx[6 * t + c] : CT(0);
+            CT v = l == 0 ? Hx[6 * t + c] : CT(0);
             for (int j = 0; j < 3; ++j) v -= tau[j] * V0[3 * t + j] * W[6 * j + c];
-            G[6 * t + c] = v;
-            og[OBG_G + 6 * t + c] = v;
+            rec[OBG_G + 6 * t + c] = v;
         }
     for (int x = 0, e = 0; x < 6; ++x)
         for (int y = 0; y <= x; ++y, ++e)
-            og[OBG_DS + e] = Hx[x] * Hx[y] + Hx[6 + x] * Hx[6 + y] + Hx[12 + x] * Hx[12 + y] + Hx[18 + x] * Hx[18 + y];
-    for (int c = 0; c < 6; ++c) og[OBG_UB + c] = u6[c] - (G[c] * gr[0] + G[6 + c] * gr[1] + G[12 + c] * gr[2]);
+            rec[OBG_DS + e] = Hx[x] * Hx[y] + Hx[6 + x] * Hx[6 + y] + Hx[12 + x] * Hx[12 + y] + Hx[18 + x] * Hx[18 + y];
+    for (int c = 0; c < 6; ++c)
+        rec[OBG_UB + c] = u6[c] - (rec[OBG_G + c] * gr[0] + rec[OBG_G + 6 + c] * gr[1] + rec[OBG_G + 12 + c] * gr[2]);
+    for (int e = OBG_UB + 6; e < OBG_STRIDE; ++e) rec[e] = 0;
+    store_pairs(fb.obs_g + (size_t)(o0 + l) * OBG_STRIDE, rec, OBG_STRIDE);
 }
 
 // Dense row `row` (0 <= row < 4M) of Q^T Hx for observation column block i.
@@ -1851,9 +1881,21 @@ void launch_triangulate(hipStream_t s, const DevState<T>& st, const Params<T>& p
     hipLaunchKernelGGL(k_triangulate<T>, dim3((fb.nf + 3) / 4), dim3(256), 0, s, st, prm, fb, 0, fb.nf);
 }
 template <typename T>
-void launch_feature(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const FeatBatch<T>& fb) {
+void launch_feature(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const FeatBatch<T>& fb,
+                    const SegClasses& sc) {
     if (fb.nf == 0) return;
-    hipLaunchKernelGGL(k_feature<T>, dim3((fb.nf + 3) / 4), dim3(256), 0, s, st, prm, fb, 0, fb.nf);
+    for (int c = 0; c < SegClasses::NC; ++c) {
+        const int cnt = sc.off[c + 1] - sc.off[c];
+        if (cnt == 0) continue;
+        const int* list = sc.list + sc.off[c];
+        const int waves = (cnt * SegClasses::S[c] + 63) / 64, blocks = (waves + 3) / 4;
+        switch (SegClasses::S[c]) {
+            case 8: hipLaunchKernelGGL((k_feature<T, 8>), dim3(blocks), dim3(256), 0, s, st, prm, fb, list, cnt); break;
+            case 16: hipLaunchKernelGGL((k_feature<T, 16>), dim3(blocks), dim3(256), 0, s, st, prm, fb, list, cnt); break;
+            case 32: hipLaunchKernelGGL((k_feature<T, 32>), dim3(blocks), dim3(256), 0, s, st, prm, fb, list, cnt); break;
+            default: hipLaunchKernelGGL((k_feature<T, 64>), dim3(blocks), dim3(256), 0, s, st, prm, fb, list, cnt); break;
+        }
+    }
 }
 template <typename T>
 size_t gate_lds_bytes(int maxM) {
@@ -1885,6 +1927,21 @@ static void launch_gate_wave(hipStream_t s, const DevState<T>& st, const Params<
 // time): the register-tile wave kernel sized for the class, or for the
 // largest features the workgroup LDS kernel (global-memory kernel if even
 // that does not fit).
+static int gate_mode() {   // MSCKF_GATE=lds forces the workgroup kernel for every class (A/B runs)
+    static int mode = -1;
+    if (mode < 0) {
+        const char* e = getenv("MSCKF_GATE");
+        mode = (e && e[0] == 'l') ? 1 : 0;
+    }
+    return mode;
+}
+
+// The workgroup gating kernels and the QR merge read the compact factors
+// (V, W, Q^T r, tau) that k_feature otherwise skips.
+bool feature_needs_compact(int maxM, int Cmax) {
+    return gate_mode() == 1 || maxM > GateClasses::LIM[GateClasses::NC - 2] || update_mode(Cmax) == UPD_QR;
+}
+
 template <typename T>
 void launch_gate(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const FeatBatch<T>& fb,
                  const GateClasses& gc) {
@@ -1894,11 +1951,7 @@ void launch_gate(hipStream_t s, const DevState<T>& st, const Params<T>& prm, con
         (void)hipFuncSetAttribute((const void*)k_gate_lds<T>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_set = true;
     }
-    static int mode = -1;   // MSCKF_GATE=lds forces the workgroup kernel for every class (A/B runs)
-    if (mode < 0) {
-        const char* e = getenv("MSCKF_GATE");
-        mode = (e && e[0] == 'l') ? 1 : 0;
-    }
+    const int mode = gate_mode();
     for (int c = 0; c < GateClasses::NC; ++c) {
         const int cnt = gc.off[c + 1] - gc.off[c];
         if (cnt == 0) continue;
@@ -2024,7 +2077,7 @@ void launch_kalman(hipStream_t s, const DevState<T>& st, const Params<T>& prm, c
     template void launch_augment<T>(hipStream_t, const DevState<T>&, int);                               \
     template void launch_prune<T>(hipStream_t, const DevState<T>&, int, const int*, int, T*, const int*, int); \
     template void launch_triangulate<T>(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&); \
-    template void launch_feature<T>(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&); \
+    template void launch_feature<T>(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&, const SegClasses&); \
     template void launch_gate<T>(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&, const GateClasses&); \
     template void launch_select<T>(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const UpdWs<T>&, int); \
     template void launch_compress<T>(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const UpdWs<T>&); \

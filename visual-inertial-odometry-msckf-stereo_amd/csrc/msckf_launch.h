@@ -68,8 +68,16 @@ void launch_prune(hipStream_t, const DevState<T>&, int filter, const int* keep, 
                   const int* keep_cams, int nkeep);
 template <typename T>
 void launch_triangulate(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&);
+// Per-feature kernels packed S lanes per feature: features listed by class
+// (M <= S), 64/S features per wavefront.
+struct SegClasses {
+    static constexpr int NC = 4;
+    static constexpr int S[NC] = {8, 16, 32, 64};
+    const int* list = nullptr;
+    int off[NC + 1] = {};
+};
 template <typename T>
-void launch_feature(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&);
+void launch_feature(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&, const SegClasses&);
 // Feature index lists per gating size class (device pointer + host offsets).
 // Gating size classes by observation count M.  Class c < NC-1 runs the
 // one-wave register-tile kernel with TPL[c] 4x4 tiles per lane (enough for the
@@ -93,6 +101,7 @@ template <typename T>
 void launch_compress_qr(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const UpdWs<T>&);
 enum UpdateMode { UPD_CHOL = 0, UPD_PCHOL = 1, UPD_QR = 2 };
 int update_mode(int Cmax);
+bool feature_needs_compact(int maxM, int Cmax);
 bool kalman_chol_supported(int Cmax);
 template <typename T>
 void launch_kalman_chol(hipStream_t, const DevState<T>&, const Params<T>&, const UpdWs<T>&, KernelTimer*);
