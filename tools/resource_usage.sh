@@ -1,7 +1,7 @@
 #!/bin/bash
 # Print VGPR / AGPR / scratch / LDS / occupancy per kernel (hipcc resource remarks).
 SRC="${1:-visual-inertial-odometry-msckf-stereo_amd/csrc/msckf_kernels.hip}"
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -Iinclude -c "$SRC" -o /tmp/_ru.o \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -Iinclude -fno-slp-vectorize -c "$SRC" -o /tmp/_ru.o \
     -Rpass-analysis=kernel-resource-usage 2>&1 | grep remark | sed 's/.*remark: //; s/ \[-Rpass.*//' \
  | python3 -c '
 import sys, subprocess, re

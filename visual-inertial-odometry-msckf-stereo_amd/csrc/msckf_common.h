@@ -230,6 +230,18 @@ __device__ __forceinline__ double fast_sqrt(double x) { return sqrt(x); }
 __device__ __forceinline__ float fast_rcp(float x) { return 1.0f / x; }
 __device__ __forceinline__ double fast_rcp(double x) { return 1.0 / x; }
 
+// Column-major enumeration of the lower tiles (ti >= tl) of a grid with nrow
+// tile rows: column c holds nrow - c tiles and starts at c nrow - c (c - 1) / 2.
+// Returns tl for tile index t (closed form + one-step fix-up).
+__device__ __forceinline__ int colmajor_col(int t, int nrow) {
+    const float q = 2.0f * nrow + 1.0f;
+    int c = (int)((q - sqrtf(fmaxf(q * q - 8.0f * t, 0.0f))) * 0.5f);
+    if (c < 0) c = 0;
+    while (c > 0 && c * nrow - c * (c - 1) / 2 > t) --c;
+    while ((c + 1) * nrow - (c + 1) * c / 2 <= t) ++c;
+    return c;
+}
+
 // ------------------------------------------------------ wave reductions --
 template <typename T>
 __device__ __forceinline__ T wave_sum(T x) {

@@ -54,13 +54,11 @@ __device__ __forceinline__ bool rchol_core(int nrow, int ncol, int nelim, double
 #pragma unroll
     for (int s = 0; s < TPL; ++s) {
         const int t = NT * s + tid;
-        int c = 0, rem = t < ntiles ? t : 0;
-        while (rem >= nrow - c) { rem -= nrow - c; ++c; }
+        const int c = colmajor_col(t < ntiles ? t : 0, nrow);
+        const int rem = (t < ntiles ? t : 0) - (c * nrow - c * (c - 1) / 2);
         crd[s] = t < ntiles ? ((c + rem) | (c << 16)) : -1;
-        int tm = NT * s + NT - 1 < ntiles - 1 ? NT * s + NT - 1 : ntiles - 1;
-        int cm = 0;
-        while (tm >= nrow - cm) { tm -= nrow - cm; ++cm; }
-        tlmax[s] = NT * s < ntiles ? cm : -1;
+        const int tm = NT * s + NT - 1 < ntiles - 1 ? NT * s + NT - 1 : ntiles - 1;
+        tlmax[s] = NT * s < ntiles ? colmajor_col(tm, nrow) : -1;
     }
 #define RTI(s) (crd[s] & 0xffff)
 #define RTL(s) (crd[s] >> 16)

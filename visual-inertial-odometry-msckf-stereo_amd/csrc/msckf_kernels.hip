@@ -1163,13 +1163,11 @@ __global__ void __launch_bounds__(256) k_gate_wave(DevState<T> st, Params<T> prm
 #pragma unroll
     for (int s = 0; s < TPL; ++s) {
         const int t = 64 * s + lane;
-        int c = 0, rem = t < ntiles ? t : 0;
-        while (rem >= nT - c) { rem -= nT - c; ++c; }
+        const int c = colmajor_col(t < ntiles ? t : 0, nT);
+        const int rem = (t < ntiles ? t : 0) - (c * nT - c * (c - 1) / 2);
         crd[s] = t < ntiles ? ((c + rem) | (c << 16)) : -1;
-        int tm = 64 * s + 63 < ntiles - 1 ? 64 * s + 63 : ntiles - 1;
-        int cm = 0;
-        while (tm >= nT - cm) { tm -= nT - cm; ++cm; }
-        tlmax[s] = 64 * s < ntiles ? cm : -1;
+        const int tm = 64 * s + 63 < ntiles - 1 ? 64 * s + 63 : ntiles - 1;
+        tlmax[s] = 64 * s < ntiles ? colmajor_col(tm, nT) : -1;
     }
 #define TI(s) (crd[s] & 0xffff)
 #define TL(s) (crd[s] >> 16)
@@ -1275,16 +1273,38 @@ __global__ void __launch_bounds__(256) k_gate_wave(DevState<T> st, Params<T> prm
             if (!OK(s) || TL(s) <= tj) continue;
             const T* ri = wd + GB * TI(s);
             const T* cl = wt + GB * TL(s);
-            T u[4][4], w[4][4];
+            if constexpr (sizeof(T) == 4) {   // packed: column pairs (y, y+1) in one v_pk_fma_f32
+                using F2 = float __attribute__((ext_vector_type(2)));
+                const F2* c2 = reinterpret_cast<const F2*>(cl);   // c2[2 c + h] = (W^T[c][2h], W^T[c][2h+1])
+                F2 w2[4][2];
 #pragma unroll
-            for (int x = 0; x < 4; ++x)
+                for (int c = 0; c < 4; ++c) { w2[c][0] = c2[2 * c]; w2[c][1] = c2[2 * c + 1]; }
 #pragma unroll
-                for (int c = 0; c < 4; ++c) { u[x][c] = ri[4 * x + c]; w[c][x] = cl[4 * c + x]; }
+                for (int x = 0; x < 4; ++x) {
+                    T u[4];
 #pragma unroll
-            for (int x = 0; x < 4; ++x)
+                    for (int c = 0; c < 4; ++c) u[c] = ri[4 * x + c];
 #pragma unroll
-                for (int y = 0; y < 4; ++y)
-                    a[s][x][y] -= u[x][0] * w[0][y] + u[x][1] * w[1][y] + u[x][2] * w[2][y] + u[x][3] * w[3][y];
+                    for (int h = 0; h < 2; ++h) {
+                        F2 acc = {a[s][x][2 * h], a[s][x][2 * h + 1]};
+#pragma unroll
+                        for (int c = 0; c < 4; ++c) acc = __builtin_elementwise_fma(F2{-u[c], -u[c]}, w2[c][h], acc);
+                        a[s][x][2 * h] = acc.x;
+                        a[s][x][2 * h + 1] = acc.y;
+                    }
+                }
+            } else {
+                T u[4][4], w[4][4];
+#pragma unroll
+                for (int x = 0; x < 4; ++x)
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) { u[x][c] = ri[4 * x + c]; w[c][x] = cl[4 * c + x]; }
+#pragma unroll
+                for (int x = 0; x < 4; ++x)
+#pragma unroll
+                    for (int y = 0; y < 4; ++y)
+                        a[s][x][y] -= u[x][0] * w[0][y] + u[x][1] * w[1][y] + u[x][2] * w[2][y] + u[x][3] * w[3][y];
+            }
             asm volatile("" ::: "memory");   // keep one slot's operands live at a time
         }
     }
