@@ -131,7 +131,7 @@ UpdWs<T> upd_ws(msckf_ctx* c) {
     w.dx = reinterpret_cast<KT*>(c->dx.p);
     w.info = c->info.p;
     w.Cmax = c->Cmax;
-    w.Cp = (c->Cmax + 3) & ~3;
+    w.Cp = (c->Cmax + 15) & ~15;   // leading dim of Lc / Vi / W (MFMA path pads C to 16)
     w.Lc = reinterpret_cast<KT*>(c->Lc.p);
     w.Vi = reinterpret_cast<KT*>(c->Vi.p);
     w.Sii = reinterpret_cast<KT*>(c->Sii.p);
@@ -396,7 +396,7 @@ int do_create(msckf_ctx* c) {
     HIPC(c->dx.ensure(B * (c->Dmax + c->Cmax) * sizeof(KT)));
     HIPC(c->info.ensure(4 * B));
     if (update_mode(c->Cmax) == UPD_CHOL) {   // Cholesky-form Kalman workspace
-        const size_t Cp = (c->Cmax + 3) & ~3, kb = sizeof(KT);
+        const size_t Cp = (c->Cmax + 15) & ~15, kb = sizeof(KT);
         HIPC(c->Lc.ensure(B * Cp * Cp * kb));
         HIPC(c->Vi.ensure(B * 24 * Cp * kb));
         HIPC(c->Sii.ensure(B * 24 * 24 * kb));

@@ -153,6 +153,257 @@ __device__ __forceinline__ bool rchol_core(int nrow, int ncol, int nelim, double
 
 __host__ __device__ constexpr int rchol_lds_doubles(int nrow) { return 2 * RB * nrow; }
 
+typedef double v4d __attribute__((ext_vector_type(4)));
+
+// ===========================================================================
+// MFMA partial Cholesky with 16-wide steps -- EXPERIMENTAL (MSCKF_KALMAN_TILE=16),
+// slower than rchol_core today: measured per 16 pivots ~27K cycles in the
+// wave-0 diagonal factor + inverse (serial sqrt / div / LDS chain) and ~20K in
+// the update (column reads of the [R][16] panel hit 8-way bank conflicts; each
+// slot's four MFMAs form one dependent chain).  One step per tile column of
+// 16 pivots.
+//   1. owners of the tile column dump it to LDS (buf[row][16], double-buffered)
+//   2. wave 0 factors the 16 x 16 diagonal block (lane i < 16 holds row i,
+//      right-looking with shuffles) and inverts it (lane j: column j of
+//      L_d^-1 by forward substitution); both go to LDS
+//   3. owners of the panel tiles form W = A L_d^-T as four MFMAs (operands from
+//      LDS), store it over the raw rows and to panel(); the diagonal tile's
+//      rows become zero (finished)
+//   4. every tile right of the panel takes acc -= W_i W_l^T as four
+//      v_mfma_f64_16x16x4 (k-chunks of 4 panel columns), operands from LDS.
+// Three barriers per 16 pivots.
+// ===========================================================================
+template <int NW, int TPW, class Load, class Panel, class Trail>
+__device__ __forceinline__ bool mchol16_core(int nrow, int ncol, int nelim, double* lds, Load load, Panel panel,
+                                             Trail trail, int dbg = 0) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int ntiles = ncol * nrow - ncol * (ncol - 1) / 2;
+    const int R = 16 * nrow;
+    const bool prof = dbg && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0;
+    unsigned long long tph[5] = {0, 0, 0, 0, 0}, tlast = prof ? __builtin_amdgcn_s_memtime() : 0;
+#define MPROF16(k)                                                       \
+    if (prof) {                                                          \
+        const unsigned long long now = __builtin_amdgcn_s_memtime();     \
+        tph[k] += now - tlast;                                           \
+        tlast = now;                                                     \
+    }
+    int crd[TPW], tlmax[TPW];
+#pragma unroll
+    for (int s = 0; s < TPW; ++s) {
+        const int t = NW * s + wv;
+        const int c = colmajor_col(t < ntiles ? t : 0, nrow);
+        const int rem = (t < ntiles ? t : 0) - (c * nrow - c * (c - 1) / 2);
+        crd[s] = __builtin_amdgcn_readfirstlane(t < ntiles ? ((c + rem) | (c << 16)) : -1);
+        const int tm = NW * s + NW - 1 < ntiles - 1 ? NW * s + NW - 1 : ntiles - 1;
+        tlmax[s] = __builtin_amdgcn_readfirstlane(NW * s < ntiles ? colmajor_col(tm, nrow) : -1);
+    }
+#define QTI(s) (crd[s] & 0xffff)
+#define QTL(s) (crd[s] >> 16)
+#define QOK(s) (crd[s] >= 0)
+    const int lc = lane & 15, lr = lane >> 4;
+    v4d acc[TPW];
+#pragma unroll
+    for (int s = 0; s < TPW; ++s) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[s][r] = QOK(s) ? load(16 * QTI(s) + lr + 4 * r, 16 * QTL(s) + lc) : 0.0;
+        asm volatile("" ::: "memory");
+    }
+    MPROF16(0);
+    double* Ld = lds + 2 * 16 * R;   // [16][16] L_d, [16][16] L_d^-1, then a failure flag
+    double* Linv = Ld + 256;
+    double* sflag = Linv + 256;
+    bool fail = false;
+    for (int tc = 0; 16 * tc < nelim; ++tc) {
+        double* buf = lds + (tc & 1) * 16 * R;   // [R][16]
+        // opaque per step: stops the compiler from hoisting every slot's row
+        // offsets / store addresses out of the loop (that alone spilled ~200 VGPRs)
+#pragma unroll
+        for (int s = 0; s < TPW; ++s) asm volatile("" : "+s"(crd[s]));
+#pragma unroll
+        for (int s = 0; s < TPW; ++s) {
+            if (!QOK(s) || QTL(s) != tc) continue;
+            const int row0 = 16 * QTI(s) + lr;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) buf[(row0 + 4 * r) * 16 + lc] = acc[s][r];
+        }
+        LDS_BARRIER();
+        MPROF16(1);
+        const int p0 = 16 * tc;
+        if (wv == 0) {   // 16 x 16 Cholesky of the diagonal block in place in LDS, then L_d^-1
+            // lane -> entries (i = lane & 15, j = 4 (lane >> 4) .. +3) of the block
+            double* blk = buf + p0 * 16;   // [16][16], row-major
+            const int bi = lane & 15, bj0 = 4 * (lane >> 4);
+            bool bad = false;
+            for (int k = 0; k < 16; ++k) {
+                const double piv = blk[k * 16 + k];
+                bad |= !(piv > 0.0);
+                const double d = sqrt(piv > 0.0 ? piv : 1.0), inv = 1.0 / d;
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // every lane has read the pivot
+                if (bj0 == (k & ~3) && bi >= k) blk[bi * 16 + k] = bi == k ? d : blk[bi * 16 + k] * inv;
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                const double lik = blk[bi * 16 + k];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int j = bj0 + q;
+                    if (j > k && bi >= j) blk[bi * 16 + j] -= lik * blk[j * 16 + k];
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            }
+            if (lane < 16) {
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const double v = j <= lane ? blk[lane * 16 + j] : 0.0;
+                    Ld[lane * 16 + j] = v;
+                    if (j <= lane) panel(p0 + lane, p0 + j, v);   // factor rows of the diagonal block
+                }
+            }
+            if (lane == 0) sflag[0] = bad ? 1.0 : 0.0;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            // column j = lane of X = L_d^-1 by forward substitution (L_d rows broadcast from LDS)
+            double x[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                double v = (i == lane) ? 1.0 : 0.0;
+#pragma unroll
+                for (int m = 0; m < i; ++m) v -= Ld[i * 16 + m] * x[m];
+                x[i] = v / Ld[i * 16 + i];
+            }
+            if (lane < 16) {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) Linv[i * 16 + lane] = x[i];   // Linv[i][j] = (L_d^-1)[i][j]
+            }
+        }
+        LDS_BARRIER();
+        MPROF16(2);
+        if (sflag[0] != 0.0) { fail = true; break; }
+        // panel tiles (ti > tc): W = A L_d^-T as four MFMAs, B[k][n] = (L_d^-T)[k][n] = Linv[n][k];
+        // a tile's rows are read and rewritten only by its owner wave (no barrier between)
+#pragma unroll
+        for (int s = 0; s < TPW; ++s) {
+            if (!QOK(s) || QTL(s) != tc) continue;
+            const int row0 = 16 * QTI(s) + lr;
+            if (QTI(s) == tc) {   // diagonal tile: finished, enters the update as zero
+#pragma unroll
+                for (int r = 0; r < 4; ++r) buf[(row0 + 4 * r) * 16 + lc] = 0.0;
+                continue;
+            }
+            const double* ra = buf + (16 * QTI(s) + lc) * 16 + lr;
+            v4d wacc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                wacc = __builtin_amdgcn_mfma_f64_16x16x4f64(ra[4 * c], Linv[lc * 16 + 4 * c + lr], wacc, 0, 0, 0);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                buf[(row0 + 4 * r) * 16 + lc] = wacc[r];
+                panel(row0 + 4 * r, p0 + lc, wacc[r]);
+            }
+        }
+        LDS_BARRIER();
+        MPROF16(3);
+#pragma unroll
+        for (int s = 0; s < TPW; ++s) {
+            if (tlmax[s] <= tc) continue;   // slot entirely in finished tile columns
+            if (!QOK(s) || QTL(s) <= tc) continue;
+            const double* ri = buf + (16 * QTI(s) + lc) * 16 + lr;
+            const double* rl = buf + (16 * QTL(s) + lc) * 16 + lr;
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(-ri[4 * c], rl[4 * c], acc[s], 0, 0, 0);
+        }
+        MPROF16(4);
+    }
+    if (prof)
+        printf("mchol16 wg0: load %llu dump+barrier %llu diag %llu panel %llu update %llu cycles (%d steps)\n",
+               tph[0], tph[1], tph[2], tph[3], tph[4], nelim / 16);
+#undef MPROF16
+    if (!fail) {
+#pragma unroll
+        for (int s = 0; s < TPW; ++s) {
+            if (!QOK(s) || 16 * QTL(s) < nelim) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) trail(16 * QTI(s) + lr + 4 * r, 16 * QTL(s) + lc, acc[s][r]);
+        }
+    }
+#undef QTI
+#undef QTL
+#undef QOK
+    return !fail;
+}
+
+__device__ __forceinline__ int round16(int x) { return (x + 15) & ~15; }
+constexpr int KW16 = 32;   // IMU block padded to a multiple of 16 (MFMA path)
+
+// ---- stage A (MFMA): index space [cams (Cq = round16 C) | IMU (32)] ----
+template <typename T, int NW, int TPW>
+__global__ void __launch_bounds__(64 * NW) k_kal_a16(DevState<T> st, UpdWs<T> ws, int dbg) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    const int b = blockIdx.x;
+    const int* info = ws.info + 4 * b;
+    if (info[0] == 0) return;
+    const int C = 6 * st.ncams[b], Cq = round16(C);
+    const int nrow = (Cq + KW16) / 16;
+    const T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
+    const int ld = st.Dmax, Cpw = ws.Cp;
+    KT* Lc = ws.Lc + (size_t)b * Cpw * Cpw;
+    KT* Vi = ws.Vi + (size_t)b * KW * Cpw;
+    KT* Sii = ws.Sii + (size_t)b * KW * KW;
+    auto map = [&](int i) { return i < C ? 21 + i : (i < Cq ? -1 : (i < Cq + 21 ? i - Cq : -1)); };
+    auto load = [&](int i, int j) -> double {
+        const int mi = map(i), mj = map(j);
+        if (mi < 0 || mj < 0) return i == j ? 1.0 : 0.0;
+        return (double)P[(size_t)mi * ld + mj];
+    };
+    auto panel = [&](int r, int c, double v) {
+        if (r >= Cq + KW) return;
+        (r < Cq ? Lc + (size_t)r * Cpw : Vi + (size_t)(r - Cq) * Cpw)[c] = v;
+    };
+    auto trail = [&](int i, int j, double v) {
+        if (i - Cq < KW && j - Cq < KW) Sii[(i - Cq) * KW + (j - Cq)] = v;
+    };
+    const bool ok = mchol16_core<NW, TPW>(nrow, nrow, Cq, reinterpret_cast<double*>(smem_raw), load, panel, trail, dbg);
+    if (!ok && threadIdx.x == 0) ws.info[4 * b + 3] = -1;
+}
+
+// ---- stage C (MFMA): T (Cq) with extra rows [Vc_i (21); Lc (C); c^T], 16-row tiles ----
+template <typename T, int NW, int TPW>
+__global__ void __launch_bounds__(64 * NW) k_kal_c16(DevState<T> st, UpdWs<T> ws, int ner, int dbg) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    const int b = blockIdx.y, g = blockIdx.x;
+    const int* info = ws.info + 4 * b;
+    if (info[0] == 0) return;
+    const int C = 6 * st.ncams[b], Cq = round16(C), nTc = Cq / 16;
+    const int E = 21 + C + 1, ER = (E + 15) / 16;
+    const int e0 = g * ner;
+    if (e0 >= ER) return;
+    const int nr = ER - e0 < ner ? ER - e0 : ner;
+    const int Cpw = ws.Cp, ldt = ws.Cmax + 1;
+    const KT* Tm = ws.Tm + (size_t)b * ws.Cmax * ldt;
+    const KT* Lc = ws.Lc + (size_t)b * Cpw * Cpw;
+    const KT* Vi = ws.Vi + (size_t)b * KW * Cpw;
+    KT* W = ws.W + (size_t)b * (st.Dmax + 1) * Cpw;
+    auto load = [&](int i, int j) -> double {
+        if (i < Cq) {
+            if (i >= C || j >= C) return i == j ? 1.0 : 0.0;
+            return i >= j ? Tm[(size_t)i * ldt + j] : Tm[(size_t)j * ldt + i];
+        }
+        const int e = i - Cq + 16 * e0;
+        if (j >= C) return 0.0;
+        if (e < 21) return Vi[(size_t)e * Cpw + j];
+        if (e < 21 + C) return j <= e - 21 ? Lc[(size_t)(e - 21) * Cpw + j] : 0.0;
+        if (e == 21 + C) return Tm[(size_t)j * ldt + C];
+        return 0.0;
+    };
+    auto panel = [&](int r, int c, double v) {
+        if (r < Cq) return;
+        const int e = r - Cq + 16 * e0;
+        if (e < E) W[(size_t)e * Cpw + c] = v;
+    };
+    auto trail = [](int, int, double) {};
+    const bool ok = mchol16_core<NW, TPW>(nTc + nr, nTc, Cq, reinterpret_cast<double*>(smem_raw), load, panel, trail, dbg);
+    if (!ok && threadIdx.x == 0) ws.info[4 * b + 3] = -1;
+}
+
 // ---- stage A: [P_cc P_ci; P_ic P_ii] in index space [cams (Cp) | IMU (24)] ----
 template <typename T, int NT, int TPL>
 __global__ void __launch_bounds__(NT) k_kal_a(DevState<T> st, UpdWs<T> ws) {
@@ -379,7 +630,32 @@ static void launch_c_cfg(hipStream_t s, const DevState<T>& st, const UpdWs<T>& w
     hipLaunchKernelGGL((k_kal_c<T, NT, TPL>), dim3(groups, st.B), dim3(NT), lds, s, st, ws, ner);
 }
 
+
+// MFMA path configurations (waves, tiles per wave) that compile without
+// spills: 14 accumulator tiles (112 VGPRs) in a 256-register budget at 8
+// waves, 8 tiles (64 VGPRs) in a 128-register budget at 16 waves.
+struct MfmaCfg { int nw, tpw; };
+static bool pick_mfma(int tiles, MfmaCfg& c) {
+    if (tiles <= 8 * 14) { c = {8, 14}; return true; }
+    if (tiles <= 16 * 8) { c = {16, 8}; return true; }
+    return false;
+}
+
+static bool mfma_kalman(int Cmax) {
+    static int mode = -1;   // MSCKF_KALMAN_TILE=16 selects the experimental MFMA tiles (A/B runs)
+    if (mode < 0) {
+        const char* e = getenv("MSCKF_KALMAN_TILE");
+        mode = (e && atoi(e) == 16) ? 1 : 0;
+    }
+    if (!mode) return false;
+    const int Cq = (Cmax + 15) & ~15;
+    const int nrowA = (Cq + 32) / 16, nTc = Cq / 16;
+    MfmaCfg c;
+    return pick_mfma(nrowA * (nrowA + 1) / 2, c) && pick_mfma(nTc * (nTc + 1) / 2 + nTc, c);
+}
+
 bool kalman_chol_supported(int Cmax) {
+    if (mfma_kalman(Cmax)) return true;
     const int Cp = (Cmax + 3) & ~3;
     const int nrowA = (Cp + KW) / 4;
     RcholCfg c;
@@ -388,12 +664,45 @@ bool kalman_chol_supported(int Cmax) {
     return pick_rchol(nTc * (nTc + 1) / 2 + nTc, c);
 }
 
+template <typename T, int NW, int TPW>
+static void launch_a16(hipStream_t s, const DevState<T>& st, const UpdWs<T>& ws, size_t lds) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_kal_a16<T, NW, TPW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        attr = true;
+    }
+    static const int dbg = getenv("MSCKF_DBG_KAL") ? 1 : 0;
+    hipLaunchKernelGGL((k_kal_a16<T, NW, TPW>), dim3(st.B), dim3(64 * NW), lds, s, st, ws, dbg);
+}
+template <typename T, int NW, int TPW>
+static void launch_c16(hipStream_t s, const DevState<T>& st, const UpdWs<T>& ws, int groups, int ner, size_t lds) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_kal_c16<T, NW, TPW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        attr = true;
+    }
+    static const int dbg = getenv("MSCKF_DBG_KAL") ? 1 : 0;
+    hipLaunchKernelGGL((k_kal_c16<T, NW, TPW>), dim3(groups, st.B), dim3(64 * NW), lds, s, st, ws, ner, dbg);
+}
+
 template <typename T>
 void launch_kalman_chol(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const UpdWs<T>& ws,
                         KernelTimer* kt) {
-    const int Cp = ws.Cp, Cmax = ws.Cmax;
-    // stage A
-    {
+    const int Cp = (ws.Cmax + 3) & ~3, Cmax = ws.Cmax;
+    const bool mf = mfma_kalman(Cmax);
+    const int Cq = (Cmax + 15) & ~15;
+    if (mf) {   // stage A, MFMA tiles
+        const int nrow = (Cq + 32) / 16;
+        MfmaCfg c;
+        pick_mfma(nrow * (nrow + 1) / 2, c);
+        const size_t lds = (2 * 16 * 16 * (size_t)nrow + 512 + 8) * sizeof(double);
+        kt->begin(s, "kalman_a");
+        if (c.nw == 8) launch_a16<T, 8, 14>(s, st, ws, lds);
+        else launch_a16<T, 16, 8>(s, st, ws, lds);
+        kt->end(s);
+    } else {   // stage A, 4x4 VALU tiles
         const int nrow = (Cp + KW) / 4;
         RcholCfg c;
         pick_rchol(nrow * (nrow + 1) / 2, c);
@@ -408,8 +717,21 @@ void launch_kalman_chol(hipStream_t s, const DevState<T>& st, const Params<T>& p
     hipLaunchKernelGGL(k_kal_b1<T>, dim3(tiles, tiles, st.B), dim3(256), 0, s, st, ws);
     hipLaunchKernelGGL(k_kal_b2<T>, dim3((Cmax + 1 + GT - 1) / GT, tiles, st.B), dim3(256), 0, s, st, prm, ws);
     kt->end(s);
-    // stage C: T tiles + as many extra-row tiles as fit, the rest in more groups
-    {
+    if (mf) {   // stage C, MFMA tiles: T + as many extra-row tiles as fit, the rest in more groups
+        const int nTc = Cq / 16, Tt = nTc * (nTc + 1) / 2;
+        const int ER = (21 + Cmax + 1 + 15) / 16;
+        MfmaCfg c{16, 8};
+        if (Tt + ER * nTc <= 8 * 14) c = {8, 14};
+        if (const char* e = getenv("MSCKF_KAL_C_CFG")) c = atoi(e) == 8 ? MfmaCfg{8, 14} : MfmaCfg{16, 8};
+        const int ner_max = (c.nw * c.tpw - Tt) / nTc;
+        const int groups = (ER + ner_max - 1) / ner_max;
+        const int ner = (ER + groups - 1) / groups;
+        const size_t lds = (2 * 16 * 16 * (size_t)(nTc + ner) + 512 + 8) * sizeof(double);
+        kt->begin(s, "kalman_c");
+        if (c.nw == 8) launch_c16<T, 8, 14>(s, st, ws, groups, ner, lds);
+        else launch_c16<T, 16, 8>(s, st, ws, groups, ner, lds);
+        kt->end(s);
+    } else {   // stage C, 4x4 VALU tiles: T tiles + as many extra-row tiles as fit
         const int nTc = Cp / 4, Tt = nTc * (nTc + 1) / 2;
         const int ER = (21 + Cmax + 1 + 3) / 4;
         RcholCfg c{512, 4};
