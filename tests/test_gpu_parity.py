@@ -191,11 +191,17 @@ def _batched(problems, dtype, triangulate=True, row_cap=0, cap=None):
     return ctx, ds, feat_off, acc, gam, pw, valid, rows
 
 
-@pytest.mark.parametrize("N,F,B,cap", [(30, 200, 2, 30), (30, 200, 1, 32), (50, 120, 1, None)])
+@pytest.mark.parametrize("N,F,B,cap", [(30, 200, 2, 30), (30, 200, 1, 32), (50, 120, 1, None),
+                                       (80, 40, 1, None), (100, 20, 1, None)])
 def test_batched_fp64_vs_oracle(N, F, B, cap):
-    """cap = cam capacity of the context: 30 (C + 1 <= 192) selects the
-    one-wave-per-filter QR kernel, 32 the 16-column panel kernel, 50+ the
-    two-column-per-thread kernel."""
+    """cap = cam capacity of the context (default N).  Paths exercised:
+    30 -- register-tile Kalman stages, one-workgroup information assembly,
+    one-wave gating for every size class; 32 -- 1024-thread assembly;
+    50 -- multi-workgroup assembly, global-memory Kalman stages A / C,
+    global-memory gating (fp64 LDS too small); 80 -- tracks longer
+    than 64 observations (two per lane in k_feature, cam masks beyond bit 63);
+    100 -- the longest tracks the reference chi2 table (dof <= 99,
+    msckf.py:121-123) can gate."""
     problems = [synth.make_update_problem(N, F, seed=100 + b) for b in range(B)]
     ctx, ds, feat_off, acc, gam, pw, valid, rows = _batched(problems, np.float64, cap=cap)
     for b, d in enumerate(ds):

@@ -68,7 +68,7 @@ struct msckf_ctx {
     DBuf<unsigned char> P, imu, cams, P_snap, imu_snap, cams_snap;
     DBuf<int> ncams, ncams_snap;
     // update workspace
-    DBuf<unsigned char> Hthin, Hqr, HP, S, dx, Lc, Vi, Sii, G, Tm, W;
+    DBuf<unsigned char> Hthin, Hqr, HP, S, dx, Lc, Vi, Sii, G, Tm, W, Wk;
     DBuf<int> info;
     // feature batch
     int nf = 0, maxM = 0;
@@ -138,6 +138,8 @@ UpdWs<T> upd_ws(msckf_ctx* c) {
     w.G = reinterpret_cast<KT*>(c->G.p);
     w.Tm = reinterpret_cast<KT*>(c->Tm.p);
     w.W = reinterpret_cast<KT*>(c->W.p);
+    w.Wk = reinterpret_cast<KT*>(c->Wk.p);
+    w.wk_stride = kalman_global_ws_doubles(c->Cmax);
     return w;
 }
 
@@ -225,7 +227,7 @@ int load_features(msckf_ctx* c, int nf, const int32_t* feat_off, int single_filt
         int M = obs_off[f + 1] - obs_off[f];
         maxM = std::max(maxM, M);
         int b = h_filt[f];
-        if (M < 1 || M > 64) FAIL(-1, "feature %d has %d observations (1..64 supported)", f, M);
+        if (M < 1 || M > 128) FAIL(-1, "feature %d has %d observations (1..128 supported)", f, M);
         if (M > c->h_ncams[b]) FAIL(-1, "feature %d has more observations than cam states", f);
         for (int i = obs_off[f]; i < obs_off[f + 1]; ++i)
             if (obs_cam[i] < 0 || obs_cam[i] >= c->h_ncams[b])
@@ -403,6 +405,8 @@ int do_create(msckf_ctx* c) {
         HIPC(c->G.ensure(B * c->Cmax * (c->Cmax + 1) * kb));
         HIPC(c->Tm.ensure(B * c->Cmax * (c->Cmax + 1) * kb));
         HIPC(c->W.ensure(B * (c->Dmax + 1) * Cp * kb));
+        const size_t wk = kalman_global_ws_doubles(c->Cmax);   // large windows only
+        if (wk) HIPC(c->Wk.ensure(B * wk * kb));
     }
     HIPC(hipMemset(c->P.p, 0, c->P.cap));
     HIPC(hipMemset(c->cams.p, 0, c->cams.cap));
@@ -595,7 +599,7 @@ int msckf_create(const msckf_config_t* cfg, int hip_device, int scalar_bytes, in
     if (!cfg || !out) FAIL(-1, "null argument");
     if (scalar_bytes != 4 && scalar_bytes != 8) FAIL(-1, "scalar_bytes must be 4 or 8");
     if (n_filters < 1) FAIL(-1, "n_filters must be >= 1");
-    if (n_cam_capacity < 1 || n_cam_capacity > 64) FAIL(-1, "n_cam_capacity must be in [1, 64]");
+    if (n_cam_capacity < 1 || n_cam_capacity > 128) FAIL(-1, "n_cam_capacity must be in [1, 128]");
     int ndev = 0;
     HIPC(hipGetDeviceCount(&ndev));
     if (hip_device < 0 || hip_device >= ndev) FAIL(-1, "HIP device %d not present (%d visible)", hip_device, ndev);
@@ -626,7 +630,7 @@ int msckf_destroy(msckf_ctx_t* c) {
     if (!c) return 0;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (auto* b : {&c->P, &c->imu, &c->cams, &c->P_snap, &c->imu_snap, &c->cams_snap, &c->Hthin, &c->Hqr, &c->HP, &c->S, &c->Lc, &c->Vi, &c->Sii, &c->G, &c->Tm, &c->W,
+    for (auto* b : {&c->P, &c->imu, &c->cams, &c->P_snap, &c->imu_snap, &c->cams_snap, &c->Hthin, &c->Hqr, &c->HP, &c->S, &c->Lc, &c->Vi, &c->Sii, &c->G, &c->Tm, &c->W, &c->Wk,
                     &c->dx, &c->obs_z, &c->chi2, &c->p_w, &c->obs_ws, &c->obs_g, &c->tau, &c->ysq, &c->gamma, &c->scratch})
         b->release();
     for (auto* b : {&c->ncams, &c->ncams_snap, &c->info, &c->feat_filter, &c->feat_off, &c->obs_off, &c->obs_cam,

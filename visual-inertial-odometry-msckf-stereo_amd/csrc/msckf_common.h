@@ -101,6 +101,8 @@ struct UpdWs {
     KT* G;       // [B][Cmax][Cmax+1]    A Lc
     KT* Tm;      // [B][Cmax][Cmax+1]    (s2 I + Lc^T A Lc | Lc^T b), lower
     KT* W;       // [B][Dmax+1][Cp]      rows [Vi ; Lc ; c^T] L_T^-T
+    KT* Wk;      // [B][wk_stride]       global-memory factorisation workspace (large windows only)
+    size_t wk_stride;
     int Cp;
 };
 

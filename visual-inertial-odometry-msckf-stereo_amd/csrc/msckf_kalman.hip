@@ -476,6 +476,116 @@ __global__ void __launch_bounds__(NT) k_kal_c(DevState<T> st, UpdWs<T> ws, int n
 }
 
 // ===========================================================================
+// Global-memory fallback of stages A and C for windows whose tiles do not fit
+// in one workgroup's registers (Nmax > 36): the same partial Cholesky, in place
+// on a row-major workspace, one column per step (k_chol's scheme).  Rows
+// < ncol form the square (lower) part; rows >= ncol are extra rows with ncol
+// columns.  Correct at any size, not fast.
+// ===========================================================================
+__device__ bool gchol_core(KT* A, int ld, int nrow, int ncol, int nelim) {
+    const int tid = threadIdx.x, nt = blockDim.x;
+    __shared__ int s_bad;
+    if (tid == 0) s_bad = 0;
+    __syncthreads();
+    for (int j = 0; j < nelim; ++j) {
+        if (tid == 0) {
+            const KT d = A[(size_t)j * ld + j];
+            if (!(d > 0)) s_bad = 1;
+            A[(size_t)j * ld + j] = sqrt(d > 0 ? d : KT(1));
+        }
+        __syncthreads();
+        if (s_bad) return false;
+        const KT inv = KT(1) / A[(size_t)j * ld + j];
+        for (int i = j + 1 + tid; i < nrow; i += nt) A[(size_t)i * ld + j] *= inv;
+        __syncthreads();
+        // trailing update: rows i > j, columns l in (j, min(i, ncol - 1)]; thread grid 16 columns wide
+        const int lw = ncol - j - 1;
+        if (lw > 0) {
+            for (int i = j + 1 + tid / 16; i < nrow; i += nt / 16) {
+                const KT aij = A[(size_t)i * ld + j];
+                const int lmax = i < ncol ? i : ncol - 1;
+                for (int l = j + 1 + (tid & 15); l <= lmax; l += 16) A[(size_t)i * ld + l] -= aij * A[(size_t)l * ld + j];
+            }
+        }
+        __syncthreads();
+    }
+    return true;
+}
+
+// stage A: workspace [C + 21][C + 21], index space [cams (C) | IMU (21)]
+template <typename T>
+__global__ void __launch_bounds__(256) k_kal_ga(DevState<T> st, UpdWs<T> ws) {
+    const int b = blockIdx.x;
+    if (ws.info[4 * b] == 0) return;
+    const int C = 6 * st.ncams[b], N = C + 21, Cpw = ws.Cp;
+    KT* A = ws.Wk + (size_t)b * ws.wk_stride;
+    const T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
+    const int ld = st.Dmax;
+    auto map = [&](int i) { return i < C ? 21 + i : i - C; };
+    for (int e = threadIdx.x; e < N * N; e += blockDim.x) {
+        const int i = e / N, j = e - i * N;
+        if (j <= i) A[(size_t)i * N + j] = (KT)P[(size_t)map(i) * ld + map(j)];
+    }
+    __syncthreads();
+    if (!gchol_core(A, N, N, N, C)) {
+        if (threadIdx.x == 0) ws.info[4 * b + 3] = -1;
+        return;
+    }
+    KT* Lc = ws.Lc + (size_t)b * Cpw * Cpw;
+    KT* Vi = ws.Vi + (size_t)b * KW * Cpw;
+    KT* Sii = ws.Sii + (size_t)b * KW * KW;
+    for (int e = threadIdx.x; e < N * N; e += blockDim.x) {
+        const int i = e / N, j = e - i * N;
+        if (j > i) continue;
+        const KT v = A[(size_t)i * N + j];
+        if (i < C) Lc[(size_t)i * Cpw + j] = v;
+        else if (j < C) Vi[(size_t)(i - C) * Cpw + j] = v;
+        else Sii[(i - C) * KW + (j - C)] = v;
+    }
+}
+
+// stage C: workspace [C + E][C]: T (lower) then the extra rows [Vc_i (21); Lc (C); c^T]
+template <typename T>
+__global__ void __launch_bounds__(256) k_kal_gc(DevState<T> st, UpdWs<T> ws) {
+    const int b = blockIdx.x;
+    if (ws.info[4 * b] == 0 || ws.info[4 * b + 3] < 0) return;
+    const int C = 6 * st.ncams[b], E = 21 + C + 1, Cpw = ws.Cp, ldt = ws.Cmax + 1;
+    KT* A = ws.Wk + (size_t)b * ws.wk_stride;
+    const KT* Tm = ws.Tm + (size_t)b * ws.Cmax * ldt;
+    const KT* Lc = ws.Lc + (size_t)b * Cpw * Cpw;
+    const KT* Vi = ws.Vi + (size_t)b * KW * Cpw;
+    for (int e = threadIdx.x; e < (C + E) * C; e += blockDim.x) {
+        const int i = e / C, j = e - i * C;
+        KT v = 0;
+        if (i < C) v = j <= i ? Tm[(size_t)i * ldt + j] : KT(0);
+        else {
+            const int x = i - C;
+            if (x < 21) v = Vi[(size_t)x * Cpw + j];
+            else if (x < 21 + C) v = j <= x - 21 ? Lc[(size_t)(x - 21) * Cpw + j] : KT(0);
+            else v = Tm[(size_t)j * ldt + C];
+        }
+        A[(size_t)i * C + j] = v;
+    }
+    __syncthreads();
+    if (!gchol_core(A, C, C + E, C, C)) {
+        if (threadIdx.x == 0) ws.info[4 * b + 3] = -1;
+        return;
+    }
+    KT* W = ws.W + (size_t)b * (st.Dmax + 1) * Cpw;
+    for (int e = threadIdx.x; e < E * C; e += blockDim.x) {
+        const int x = e / C, j = e - x * C;
+        W[(size_t)x * Cpw + j] = A[(size_t)(C + x) * C + j];
+    }
+}
+
+size_t kalman_global_ws_doubles(int Cmax) {   // per filter, 0 when the register-tile stages fit
+    if (kalman_chol_supported(Cmax)) return 0;
+    const size_t C = Cmax, N = C + 21, E = 21 + C + 1;
+    const size_t a = N * N, c = (C + E) * C;
+    return a > c ? a : c;
+}
+
+// ===========================================================================
 // 64 x 64 output tile, 256 threads (4 x 4 each), K in steps of 16 through LDS.
 // A(i, k) and B(k, j) are accessors; *_KFAST says whether consecutive k are
 // contiguous in memory for that operand (selects the coalesced load mapping).
@@ -692,8 +802,13 @@ void launch_kalman_chol(hipStream_t s, const DevState<T>& st, const Params<T>& p
                         KernelTimer* kt) {
     const int Cp = (ws.Cmax + 3) & ~3, Cmax = ws.Cmax;
     const bool mf = mfma_kalman(Cmax);
+    const bool glob = !kalman_chol_supported(Cmax);   // large window: global-memory stages A and C
     const int Cq = (Cmax + 15) & ~15;
-    if (mf) {   // stage A, MFMA tiles
+    if (glob) {
+        kt->begin(s, "kalman_a");
+        hipLaunchKernelGGL(k_kal_ga<T>, dim3(st.B), dim3(256), 0, s, st, ws);
+        kt->end(s);
+    } else if (mf) {   // stage A, MFMA tiles
         const int nrow = (Cq + 32) / 16;
         MfmaCfg c;
         pick_mfma(nrow * (nrow + 1) / 2, c);
@@ -717,7 +832,11 @@ void launch_kalman_chol(hipStream_t s, const DevState<T>& st, const Params<T>& p
     hipLaunchKernelGGL(k_kal_b1<T>, dim3(tiles, tiles, st.B), dim3(256), 0, s, st, ws);
     hipLaunchKernelGGL(k_kal_b2<T>, dim3((Cmax + 1 + GT - 1) / GT, tiles, st.B), dim3(256), 0, s, st, prm, ws);
     kt->end(s);
-    if (mf) {   // stage C, MFMA tiles: T + as many extra-row tiles as fit, the rest in more groups
+    if (glob) {
+        kt->begin(s, "kalman_c");
+        hipLaunchKernelGGL(k_kal_gc<T>, dim3(st.B), dim3(256), 0, s, st, ws);
+        kt->end(s);
+    } else if (mf) {   // stage C, MFMA tiles: T + as many extra-row tiles as fit, the rest in more groups
         const int nTc = Cq / 16, Tt = nTc * (nTc + 1) / 2;
         const int ER = (21 + Cmax + 1 + 15) / 16;
         MfmaCfg c{16, 8};

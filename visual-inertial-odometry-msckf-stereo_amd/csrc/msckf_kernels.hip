@@ -623,9 +623,9 @@ __global__ void __launch_bounds__(256) k_triangulate(DevState<T> st, Params<T> p
 // ===========================================================================
 // Feature Jacobian + left-nullspace projection: one S-lane segment of a
 // wavefront per feature (64/S features per wavefront, S = 8..64 by size class
-// so short tracks do not leave most lanes idle), lane i of the segment owns
-// observation i (M <= 64: a feature is seen at most once per cam state and the
-// cam capacity is <= 64).  Computes the observability-projected
+// so short tracks do not leave most lanes idle); lane l of the segment owns
+// observations l and, for 64 < M <= 128, l + 64 (a feature is seen at most
+// once per cam state; the cam capacity is <= 128).  Computes the observability-projected
 // 4x6 / 4x3 blocks and residual, Householder-QRs H_f (4M x 3) across the wave
 // with xor-shuffle reductions (LAPACK dlarfg sign convention), and stores
 //   * in T, for gating: the compact factors of H0 = (Q^T Hx)[3:] =
@@ -662,7 +662,7 @@ __device__ __forceinline__ void store_pairs(T* dst, const S* src, int n) {
     }
 }
 
-template <typename T, int S>
+template <typename T, int S, int OPL>
 __global__ void __launch_bounds__(256) k_feature(DevState<T> st, Params<T> prm, FeatBatch<T> fb,
                                                  const int* __restrict__ flist, int cnt) {
     using CT = double;
@@ -675,7 +675,6 @@ __global__ void __launch_bounds__(256) k_feature(DevState<T> st, Params<T> prm, 
     const bool fvalid = li < cnt && fb.valid[f];
     const int b = fb.feat_filter[f];
     const int o0 = fb.obs_off[f], M = fvalid ? fb.obs_off[f + 1] - o0 : 0;
-    const bool own = l < M;
     const T* cams = st.cams + (size_t)b * st.Nmax * CAM_STRIDE;
     CT g[3], R01[9], t01[3];
     for (int k = 0; k < 3; ++k) {
@@ -684,81 +683,91 @@ __global__ void __launch_bounds__(256) k_feature(DevState<T> st, Params<T> prm, 
     }
     for (int k = 0; k < 9; ++k) R01[k] = (CT)prm.R01[k];
     const CT pw[3] = {(CT)fb.p_w[3 * f], (CT)fb.p_w[3 * f + 1], (CT)fb.p_w[3 * f + 2]};
-    CT Hx[24], Hf[12], r[4], u6[6];
-    for (int e = 0; e < 24; ++e) Hx[e] = 0;
-    for (int e = 0; e < 12; ++e) Hf[e] = 0;
-    for (int e = 0; e < 4; ++e) r[e] = 0;
-    if (own) {
-        const T* c = cams + (size_t)fb.obs_cam[o0 + l] * CAM_STRIDE;
-        const T* z = fb.obs_z + (size_t)(o0 + l) * 4;
-        CT q0[4], qn[4], cp[3];
-        for (int k = 0; k < 4; ++k) { q0[k] = (CT)c[C_Q + k]; qn[k] = (CT)c[C_QN + k]; }
-        for (int k = 0; k < 3; ++k) cp[k] = (CT)c[C_P + k];
-        CT R0[9], R1[9], t1[3], tmp[3];
-        quat_to_rot(q0, R0);
-        mat3_mul(R01, R0, R1);
-        mat3T_vec(R1, t01, tmp);
-        for (int k = 0; k < 3; ++k) t1[k] = cp[k] - tmp[k];
-        CT d0[3], d1[3], pc0[3], pc1[3];
-        for (int k = 0; k < 3; ++k) { d0[k] = pw[k] - cp[k]; d1[k] = pw[k] - t1[k]; }
-        mat3_vec(R0, d0, pc0);
-        mat3_vec(R1, d1, pc1);
-        // dz/dpc (msckf.py:457-467)
-        CT a00 = 1 / pc0[2], a02 = -pc0[0] / (pc0[2] * pc0[2]), a12 = -pc0[1] / (pc0[2] * pc0[2]);
-        CT b00 = 1 / pc1[2], b02 = -pc1[0] / (pc1[2] * pc1[2]), b12 = -pc1[1] / (pc1[2] * pc1[2]);
-        // dpc/dxc (msckf.py:469-475): [skew(pc0) | -R0], [R01 skew(pc0) | -R1]
-        CT Sk[9], RS[9];
-        skew3(pc0, Sk);
-        mat3_mul(R01, Sk, RS);
-        CT D0[18], D1[18];
-        for (int k = 0; k < 3; ++k)
-            for (int l = 0; l < 3; ++l) {
-                D0[6 * k + l] = Sk[3 * k + l];
-                D0[6 * k + 3 + l] = -R0[3 * k + l];
-                D1[6 * k + l] = RS[3 * k + l];
-                D1[6 * k + 3 + l] = -R1[3 * k + l];
+    // observation i = l + S s of the feature lives in slot s of segment lane l
+    CT Hx[OPL][24], Hf[OPL][12], r[OPL][4], u6[OPL][6];
+#pragma unroll
+    for (int s = 0; s < OPL; ++s) {
+        const int i = l + S * s;
+        const bool own = i < M;
+        for (int e = 0; e < 24; ++e) Hx[s][e] = 0;
+        for (int e = 0; e < 12; ++e) Hf[s][e] = 0;
+        for (int e = 0; e < 4; ++e) r[s][e] = 0;
+        if (own) {
+            const T* c = cams + (size_t)fb.obs_cam[o0 + i] * CAM_STRIDE;
+            const T* z = fb.obs_z + (size_t)(o0 + i) * 4;
+            CT q0[4], qn[4], cp[3];
+            for (int k = 0; k < 4; ++k) { q0[k] = (CT)c[C_Q + k]; qn[k] = (CT)c[C_QN + k]; }
+            for (int k = 0; k < 3; ++k) cp[k] = (CT)c[C_P + k];
+            CT R0[9], R1[9], t1[3], tmp[3];
+            quat_to_rot(q0, R0);
+            mat3_mul(R01, R0, R1);
+            mat3T_vec(R1, t01, tmp);
+            for (int k = 0; k < 3; ++k) t1[k] = cp[k] - tmp[k];
+            CT d0[3], d1[3], pc0[3], pc1[3];
+            for (int k = 0; k < 3; ++k) { d0[k] = pw[k] - cp[k]; d1[k] = pw[k] - t1[k]; }
+            mat3_vec(R0, d0, pc0);
+            mat3_vec(R1, d1, pc1);
+            // dz/dpc (msckf.py:457-467)
+            CT a00 = 1 / pc0[2], a02 = -pc0[0] / (pc0[2] * pc0[2]), a12 = -pc0[1] / (pc0[2] * pc0[2]);
+            CT b00 = 1 / pc1[2], b02 = -pc1[0] / (pc1[2] * pc1[2]), b12 = -pc1[1] / (pc1[2] * pc1[2]);
+            // dpc/dxc (msckf.py:469-475): [skew(pc0) | -R0], [R01 skew(pc0) | -R1]
+            CT Sk[9], RS[9];
+            skew3(pc0, Sk);
+            mat3_mul(R01, Sk, RS);
+            CT D0[18], D1[18];
+            for (int k = 0; k < 3; ++k)
+                for (int m = 0; m < 3; ++m) {
+                    D0[6 * k + m] = Sk[3 * k + m];
+                    D0[6 * k + 3 + m] = -R0[3 * k + m];
+                    D1[6 * k + m] = RS[3 * k + m];
+                    D1[6 * k + 3 + m] = -R1[3 * k + m];
+                }
+            CT H[24];
+            for (int m = 0; m < 6; ++m) {
+                H[m] = a00 * D0[m] + a02 * D0[12 + m];
+                H[6 + m] = a00 * D0[6 + m] + a12 * D0[12 + m];
+                H[12 + m] = b00 * D1[m] + b02 * D1[12 + m];
+                H[18 + m] = b00 * D1[6 + m] + b12 * D1[12 + m];
             }
-        CT H[24];
-        for (int l = 0; l < 6; ++l) {
-            H[l] = a00 * D0[l] + a02 * D0[12 + l];
-            H[6 + l] = a00 * D0[6 + l] + a12 * D0[12 + l];
-            H[12 + l] = b00 * D1[l] + b02 * D1[12 + l];
-            H[18 + l] = b00 * D1[6 + l] + b12 * D1[12 + l];
+            // observability constraint (msckf.py:484-490)
+            CT u[6], Rn[9], dp[3];
+            quat_to_rot(qn, Rn);
+            mat3_vec(Rn, g, u);
+            for (int k = 0; k < 3; ++k) dp[k] = pw[k] - cp[k];
+            skew3(dp, Sk);
+            mat3_vec(Sk, g, u + 3);
+            CT uu = 0;
+            for (int k = 0; k < 6; ++k) uu += u[k] * u[k];
+            for (int a = 0; a < 4; ++a) {
+                CT au = 0;
+                for (int k = 0; k < 6; ++k) au += H[6 * a + k] * u[k];
+                for (int k = 0; k < 6; ++k) Hx[s][6 * a + k] = H[6 * a + k] - au * u[k] / uu;
+                for (int k = 0; k < 3; ++k) Hf[s][3 * a + k] = -Hx[s][6 * a + 3 + k];
+            }
+            r[s][0] = (CT)z[0] - pc0[0] / pc0[2];
+            r[s][1] = (CT)z[1] - pc0[1] / pc0[2];
+            r[s][2] = (CT)z[2] - pc1[0] / pc1[2];
+            r[s][3] = (CT)z[3] - pc1[1] / pc1[2];
         }
-        // observability constraint (msckf.py:484-490)
-        CT u[6], Rn[9], dp[3];
-        quat_to_rot(qn, Rn);
-        mat3_vec(Rn, g, u);
-        for (int k = 0; k < 3; ++k) dp[k] = pw[k] - cp[k];
-        skew3(dp, Sk);
-        mat3_vec(Sk, g, u + 3);
-        CT uu = 0;
-        for (int k = 0; k < 6; ++k) uu += u[k] * u[k];
-        for (int a = 0; a < 4; ++a) {
-            CT au = 0;
-            for (int k = 0; k < 6; ++k) au += H[6 * a + k] * u[k];
-            for (int k = 0; k < 6; ++k) Hx[6 * a + k] = H[6 * a + k] - au * u[k] / uu;
-            for (int k = 0; k < 3; ++k) Hf[3 * a + k] = -Hx[6 * a + 3 + k];
-        }
-        r[0] = (CT)z[0] - pc0[0] / pc0[2];
-        r[1] = (CT)z[1] - pc0[1] / pc0[2];
-        r[2] = (CT)z[2] - pc1[0] / pc1[2];
-        r[3] = (CT)z[3] - pc1[1] / pc1[2];
+        for (int c = 0; c < 6; ++c)   // Hx_i^T r_i, before r is reflected
+            u6[s][c] = Hx[s][c] * r[s][0] + Hx[s][6 + c] * r[s][1] + Hx[s][12 + c] * r[s][2] + Hx[s][18 + c] * r[s][3];
+        if (own) store_pairs(fb.obs_ws + (size_t)(o0 + i) * OBS_WS + OBS_R, r[s], 4);
     }
-    for (int c = 0; c < 6; ++c)   // Hx_i^T r_i, before r is reflected
-        u6[c] = Hx[c] * r[0] + Hx[6 + c] * r[1] + Hx[12 + c] * r[2] + Hx[18 + c] * r[3];
-    if (own) store_pairs(fb.obs_ws + (size_t)(o0 + l) * OBS_WS + OBS_R, r, 4);
-    // ---- Householder QR of H_f across the wave (rows 4i..4i+3 in segment lane i) ----
-    CT V[12];
+    // ---- Householder QR of H_f across the segment (rows 4i..4i+3 with observation i) ----
+    CT V[OPL][12];
     CT tau[3];
-    for (int e = 0; e < 12; ++e) V[e] = 0;
+#pragma unroll
+    for (int s = 0; s < OPL; ++s)
+        for (int e = 0; e < 12; ++e) V[s][e] = 0;
     for (int j = 0; j < 3; ++j) {
-        CT alpha = __shfl(Hf[3 * j + j], b0, 64);   // pivot row j lives in the segment's first lane
+        CT alpha = __shfl(Hf[0][3 * j + j], b0, 64);   // pivot row j: observation 0, the segment's first lane
         CT xs = 0;
-        for (int a = 0; a < 4; ++a) {
-            int row = 4 * l + a;
-            if (row > j && own) xs += Hf[3 * a + j] * Hf[3 * a + j];
-        }
+#pragma unroll
+        for (int s = 0; s < OPL; ++s)
+            for (int a = 0; a < 4; ++a) {
+                const int row = 4 * (l + S * s) + a;
+                if (row > j && l + S * s < M) xs += Hf[s][3 * a + j] * Hf[s][3 * a + j];
+            }
         xs = seg_sum<S>(xs);
         CT tj = 0, scale = 0, beta = alpha;
         if (xs != CT(0)) {
@@ -769,88 +778,88 @@ __global__ void __launch_bounds__(256) k_feature(DevState<T> st, Params<T> prm, 
         }
         tau[j] = tj;
         // v_j: v[j] = 1, v[row > j] = Hf[row][j] * scale, 0 above
-        for (int a = 0; a < 4; ++a) {
-            int row = 4 * l + a;
-            CT v = 0;
-            if (own) v = row == j ? CT(1) : (row > j ? Hf[3 * a + j] * scale : CT(0));
-            V[3 * a + j] = v;
-        }
+#pragma unroll
+        for (int s = 0; s < OPL; ++s)
+            for (int a = 0; a < 4; ++a) {
+                const int row = 4 * (l + S * s) + a;
+                CT v = 0;
+                if (l + S * s < M) v = row == j ? CT(1) : (row > j ? Hf[s][3 * a + j] * scale : CT(0));
+                V[s][3 * a + j] = v;
+            }
         // apply H_j to the remaining H_f columns and to r
         for (int c = j + 1; c <= 3; ++c) {
             CT w = 0;
-            for (int a = 0; a < 4; ++a) w += V[3 * a + j] * (c < 3 ? Hf[3 * a + c] : r[a]);
+#pragma unroll
+            for (int s = 0; s < OPL; ++s)
+                for (int a = 0; a < 4; ++a) w += V[s][3 * a + j] * (c < 3 ? Hf[s][3 * a + c] : r[s][a]);
             w = seg_sum<S>(w);
-            for (int a = 0; a < 4; ++a) {
-                if (c < 3) Hf[3 * a + c] -= tj * V[3 * a + j] * w;
-                else r[a] -= tj * V[3 * a + j] * w;
-            }
+#pragma unroll
+            for (int s = 0; s < OPL; ++s)
+                for (int a = 0; a < 4; ++a) {
+                    if (c < 3) Hf[s][3 * a + c] -= tj * V[s][3 * a + j] * w;
+                    else r[s][a] -= tj * V[s][3 * a + j] * w;
+                }
         }
     }
     // ---- w_j = v_j^T X_{j-1}: 6 columns per observation, local to the lane ----
     CT d10 = 0, d20 = 0, d21 = 0;
-    for (int a = 0; a < 4; ++a) {
-        d10 += V[3 * a + 1] * V[3 * a];
-        d20 += V[3 * a + 2] * V[3 * a];
-        d21 += V[3 * a + 2] * V[3 * a + 1];
-    }
+#pragma unroll
+    for (int s = 0; s < OPL; ++s)
+        for (int a = 0; a < 4; ++a) {
+            d10 += V[s][3 * a + 1] * V[s][3 * a];
+            d20 += V[s][3 * a + 2] * V[s][3 * a];
+            d21 += V[s][3 * a + 2] * V[s][3 * a + 1];
+        }
     d10 = seg_sum<S>(d10);
     d20 = seg_sum<S>(d20);
     d21 = seg_sum<S>(d21);
-    // top 3 rows of V (all in the segment's first lane) and g = (Q^T r)[0:3], broadcast
+    // top 3 rows of V (observation 0: slot 0 of the segment's first lane) and g = (Q^T r)[0:3]
     CT V0[9], gr[3];
-    for (int e = 0; e < 9; ++e) V0[e] = __shfl(V[e], b0, 64);
-    for (int t = 0; t < 3; ++t) gr[t] = __shfl(r[t], b0, 64);
-    if (!own) return;
-    CT W[18];
-    for (int c = 0; c < 6; ++c) {
-        CT w0 = 0, w1 = 0, w2 = 0;
-        for (int a = 0; a < 4; ++a) {
-            w0 += V[3 * a] * Hx[6 * a + c];
-            w1 += V[3 * a + 1] * Hx[6 * a + c];
-            w2 += V[3 * a + 2] * Hx[6 * a + c];
-        }
-        w1 -= tau[0] * d10 * w0;
-        w2 -= tau[0] * d20 * w0 + tau[1] * d21 * w1;
-        W[c] = w0; W[6 + c] = w1; W[12 + c] = w2;
-    }
-    T* ws = fb.obs_ws + (size_t)(o0 + l) * OBS_WS;
-    store_pairs(ws + OBS_HX, Hx, 24);
-    if (fb.compact) {   // compact factors: only the LDS / global gate and the QR merge read them
-        store_pairs(ws + OBS_V, V, 12);
-        store_pairs(ws + OBS_W, W, 18);
-        store_pairs(ws + OBS_QR, r, 4);
-        if (l == 0)
-            for (int j = 0; j < 3; ++j) fb.tau[4 * f + j] = (T)tau[j];
-    }
-    // Gram terms.  (Q^T Hx)[t][i-block] = [i == 0] Hx_0[t] - sum_j tau_j V_0[t][j] W_j(i)
-    CT rec[OBG_STRIDE];   // G | DS | UB | pad, stored as 16-byte pairs
-    for (int t = 0; t < 3; ++t)
+    for (int e = 0; e < 9; ++e) V0[e] = __shfl(V[0][e], b0, 64);
+    for (int t = 0; t < 3; ++t) gr[t] = __shfl(r[0][t], b0, 64);
+#pragma unroll
+    for (int s = 0; s < OPL; ++s) {
+        const int i = l + S * s;
+        if (i >= M) continue;
+        CT W[18];
         for (int c = 0; c < 6; ++c) {
-            CT v = l == 0 ? Hx[6 * t + c] : CT(0);
-            for (int j = 0; j < 3; ++j) v -= tau[j] * V0[3 * t + j] * W[6 * j + c];
-            rec[OBG_G + 6 * t + c] = v;
+            CT w0 = 0, w1 = 0, w2 = 0;
+            for (int a = 0; a < 4; ++a) {
+                w0 += V[s][3 * a] * Hx[s][6 * a + c];
+                w1 += V[s][3 * a + 1] * Hx[s][6 * a + c];
+                w2 += V[s][3 * a + 2] * Hx[s][6 * a + c];
+            }
+            w1 -= tau[0] * d10 * w0;
+            w2 -= tau[0] * d20 * w0 + tau[1] * d21 * w1;
+            W[c] = w0; W[6 + c] = w1; W[12 + c] = w2;
         }
-    for (int x = 0, e = 0; x < 6; ++x)
-        for (int y = 0; y <= x; ++y, ++e)
-            rec[OBG_DS + e] = Hx[x] * Hx[y] + Hx[6 + x] * Hx[6 + y] + Hx[12 + x] * Hx[12 + y] + Hx[18 + x] * Hx[18 + y];
-    for (int c = 0; c < 6; ++c)
-        rec[OBG_UB + c] = u6[c] - (rec[OBG_G + c] * gr[0] + rec[OBG_G + 6 + c] * gr[1] + rec[OBG_G + 12 + c] * gr[2]);
-    for (int e = OBG_UB + 6; e < OBG_STRIDE; ++e) rec[e] = 0;
-    store_pairs(fb.obs_g + (size_t)(o0 + l) * OBG_STRIDE, rec, OBG_STRIDE);
+        T* ws = fb.obs_ws + (size_t)(o0 + i) * OBS_WS;
+        store_pairs(ws + OBS_HX, Hx[s], 24);
+        if (fb.compact) {   // compact factors: only the LDS / global gate and the QR merge read them
+            store_pairs(ws + OBS_V, V[s], 12);
+            store_pairs(ws + OBS_W, W, 18);
+            store_pairs(ws + OBS_QR, r[s], 4);
+            if (i == 0)
+                for (int j = 0; j < 3; ++j) fb.tau[4 * f + j] = (T)tau[j];
+        }
+        // Gram terms.  (Q^T Hx)[t][i-block] = [i == 0] Hx_0[t] - sum_j tau_j V_0[t][j] W_j(i)
+        CT rec[OBG_STRIDE];   // G | DS | UB | pad, stored as 16-byte pairs
+        for (int t = 0; t < 3; ++t)
+            for (int c = 0; c < 6; ++c) {
+                CT v = i == 0 ? Hx[s][6 * t + c] : CT(0);
+                for (int j = 0; j < 3; ++j) v -= tau[j] * V0[3 * t + j] * W[6 * j + c];
+                rec[OBG_G + 6 * t + c] = v;
+            }
+        for (int x = 0, e = 0; x < 6; ++x)
+            for (int y = 0; y <= x; ++y, ++e)
+                rec[OBG_DS + e] = Hx[s][x] * Hx[s][y] + Hx[s][6 + x] * Hx[s][6 + y] + Hx[s][12 + x] * Hx[s][12 + y] +
+                                  Hx[s][18 + x] * Hx[s][18 + y];
+        for (int c = 0; c < 6; ++c)
+            rec[OBG_UB + c] = u6[s][c] - (rec[OBG_G + c] * gr[0] + rec[OBG_G + 6 + c] * gr[1] + rec[OBG_G + 12 + c] * gr[2]);
+        for (int e = OBG_UB + 6; e < OBG_STRIDE; ++e) rec[e] = 0;
+        store_pairs(fb.obs_g + (size_t)(o0 + i) * OBG_STRIDE, rec, OBG_STRIDE);
+    }
 }
-
-// Dense row `row` (0 <= row < 4M) of Q^T Hx for observation column block i.
-template <typename T>
-__device__ __forceinline__ T qthx_entry(const T* ws_row_obs, const T* ws_col_obs, const T* tau,
-                                        int row, int i, int c) {
-    // ws_row_obs: workspace of the observation owning `row`; ws_col_obs: of obs i
-    const int a = row & 3;
-    T v = ((row >> 2) == i) ? ws_row_obs[OBS_HX + 6 * a + c] : T(0);
-    const T* V = ws_row_obs + OBS_V + 3 * a;
-    const T* W = ws_col_obs + OBS_W;
-    return v - (tau[0] * V[0] * W[c] + tau[1] * V[1] * W[6 + c] + tau[2] * V[2] * W[12 + c]);
-}
-
 // ===========================================================================
 // Gating (msckf.py:606-614): one workgroup per feature.
 // S = H0 P H0^T + sigma^2 I is formed in observation space:
@@ -1391,9 +1400,9 @@ __global__ void k_select(DevState<T> st, FeatBatch<T> fb, UpdWs<T> ws, int row_c
 // problems) carry no information and produce no row.
 // Output: rows 0..n-1 of [F | r_F] in H_thin (KT), n = rank in info[1].
 // ===========================================================================
-// features staged per round (one staging wave each): 4, or 2 when the
-// double-buffered slots of 4 would not fit in LDS
-__host__ __device__ constexpr int info_fb(int Nmax) { return Nmax <= 40 ? 4 : 2; }
+// features staged per round (one staging wave each): 4, 2 or 1, as many as
+// the double-buffered slots fit in LDS
+__host__ __device__ constexpr int info_fb(int Nmax) { return Nmax <= 40 ? 4 : (Nmax <= 80 ? 2 : 1); }
 
 // Doubles per staging slot: a feature's M <= Nmax records copied contiguously,
 // rounded up to whole 1 KiB global_load_lds wave-instructions.
@@ -1415,8 +1424,8 @@ __global__ void __launch_bounds__(NT) k_info(DevState<T> st, FeatBatch<T> fb, Up
     double* rec = reinterpret_cast<double*>(smem_raw);                      // [2][FB][SLOT]
     double* fvec = rec + (size_t)2 * INFO_FB * SLOT;                         // [Cmax + 1]
     double* dval = fvec + Cmax + 1;                                          // [Cmax]
-    unsigned long long* mask = reinterpret_cast<unsigned long long*>(dval + Cmax);   // [2][FB]
-    int* chosen = reinterpret_cast<int*>(mask + 2 * INFO_FB);                // [Cmax]
+    unsigned long long* mask = reinterpret_cast<unsigned long long*>(dval + Cmax);   // [2][FB][2] cams 0..127
+    int* chosen = reinterpret_cast<int*>(mask + 4 * INFO_FB);                // [Cmax]
     int* pos = chosen + Cmax;                                                // [2][FB][Nmax] cam -> record
     __shared__ int s_p, s_stop;
     __shared__ double s_inv, s_d0;
@@ -1426,7 +1435,8 @@ __global__ void __launch_bounds__(NT) k_info(DevState<T> st, FeatBatch<T> fb, Up
     bool act[BPT];
 #pragma unroll
     for (int m = 0; m < BPT; ++m) {
-        const int blk = tid + NT * m;
+        // blocks of this workgroup: part blockIdx.y of the filter's lower-triangle blocks
+        const int blk = blockIdx.y * (NT * BPT) + tid + NT * m;
         int i = (int)((sqrtf(8.0f * (float)blk + 1.0f) - 1.0f) * 0.5f);
         while (i * (i + 1) / 2 > blk) --i;
         while ((i + 1) * (i + 2) / 2 <= blk) ++i;
@@ -1452,24 +1462,27 @@ __global__ void __launch_bounds__(NT) k_info(DevState<T> st, FeatBatch<T> fb, Up
         for (int s = wave; s < INFO_FB; s += nwave) {
             const int f = f0 + s;
             int* ps = pos + (buf * INFO_FB + s) * Nmax;
-            unsigned long long mk = 0;
+            unsigned long long mk[2] = {0, 0};
             int o0 = 0, M = 0;
             if (f < fend && fb.include[f]) {
                 o0 = fb.obs_off[f];
                 M = fb.obs_off[f + 1] - o0;
-                if (lane < M) {
-                    const int cam = fb.obs_cam[o0 + lane];
-                    mk = 1ull << cam;
-                    ps[cam] = lane;
+                for (int o = lane; o < M; o += 64) {
+                    const int cam = fb.obs_cam[o0 + o];
+                    mk[cam >> 6] |= 1ull << (cam & 63);
+                    ps[cam] = o;
                 }
             }
-            unsigned lo = (unsigned)mk, hi = (unsigned)(mk >> 32);
 #pragma unroll
-            for (int w = 32; w >= 1; w >>= 1) {
-                lo |= (unsigned)__shfl_xor((int)lo, w, 64);
-                hi |= (unsigned)__shfl_xor((int)hi, w, 64);
+            for (int h = 0; h < 2; ++h) {
+                unsigned lo = (unsigned)mk[h], hi = (unsigned)(mk[h] >> 32);
+#pragma unroll
+                for (int w = 32; w >= 1; w >>= 1) {
+                    lo |= (unsigned)__shfl_xor((int)lo, w, 64);
+                    hi |= (unsigned)__shfl_xor((int)hi, w, 64);
+                }
+                if (lane == 0) mask[(buf * INFO_FB + s) * 2 + h] = ((unsigned long long)hi << 32) | lo;
             }
-            if (lane == 0) mask[buf * INFO_FB + s] = ((unsigned long long)hi << 32) | lo;
             // after every ordinary global load above: the copy below may stay in flight
             const char* src = reinterpret_cast<const char*>(fb.obs_g + (size_t)o0 * OBG_STRIDE);
             double* dst = rec + (size_t)(buf * INFO_FB + s) * SLOT;
@@ -1488,12 +1501,12 @@ __global__ void __launch_bounds__(NT) k_info(DevState<T> st, FeatBatch<T> fb, Up
         const int buf = it & 1;
         if (f0 + INFO_FB < fend) stage(f0 + INFO_FB, buf ^ 1);
         for (int s = 0; s < INFO_FB; ++s) {
-            const unsigned long long mk = mask[buf * INFO_FB + s];
+            const unsigned long long* mk = mask + (buf * INFO_FB + s) * 2;
             const int* ps = pos + (buf * INFO_FB + s) * Nmax;
             const double* rs = rec + (size_t)(buf * INFO_FB + s) * SLOT;
 #pragma unroll
             for (int m = 0; m < BPT; ++m) {
-                if (!act[m] || !((mk >> I[m]) & (mk >> J[m]) & 1ull)) continue;
+                if (!act[m] || !((mk[I[m] >> 6] >> (I[m] & 63)) & (mk[J[m] >> 6] >> (J[m] & 63)) & 1ull)) continue;
                 const double* gi = rs + ps[I[m]] * OBG_STRIDE;
                 const double* gj = rs + ps[J[m]] * OBG_STRIDE;
 #pragma unroll
@@ -1541,7 +1554,7 @@ __global__ void __launch_bounds__(NT) k_info(DevState<T> st, FeatBatch<T> fb, Up
 #pragma unroll
                 for (int x = 0; x < 6; ++x) F[(size_t)(6 * I[m] + x) * ldf + Cmax] = bv[m][x];
         }
-        if (tid == 0) info[1] = C;
+        if (tid == 0 && blockIdx.y == 0) info[1] = C;
         return;
     }
     // ---- augmented outer-product Cholesky with diagonal pivoting ----
@@ -1908,12 +1921,14 @@ void launch_feature(hipStream_t s, const DevState<T>& st, const Params<T>& prm, 
         const int cnt = sc.off[c + 1] - sc.off[c];
         if (cnt == 0) continue;
         const int* list = sc.list + sc.off[c];
-        const int waves = (cnt * SegClasses::S[c] + 63) / 64, blocks = (waves + 3) / 4;
+        const int lanes = SegClasses::S[c] < 64 ? SegClasses::S[c] : 64;   // S = 128: 2 observations per lane
+        const int waves = (cnt * lanes + 63) / 64, blocks = (waves + 3) / 4;
         switch (SegClasses::S[c]) {
-            case 8: hipLaunchKernelGGL((k_feature<T, 8>), dim3(blocks), dim3(256), 0, s, st, prm, fb, list, cnt); break;
-            case 16: hipLaunchKernelGGL((k_feature<T, 16>), dim3(blocks), dim3(256), 0, s, st, prm, fb, list, cnt); break;
-            case 32: hipLaunchKernelGGL((k_feature<T, 32>), dim3(blocks), dim3(256), 0, s, st, prm, fb, list, cnt); break;
-            default: hipLaunchKernelGGL((k_feature<T, 64>), dim3(blocks), dim3(256), 0, s, st, prm, fb, list, cnt); break;
+            case 8: hipLaunchKernelGGL((k_feature<T, 8, 1>), dim3(blocks), dim3(256), 0, s, st, prm, fb, list, cnt); break;
+            case 16: hipLaunchKernelGGL((k_feature<T, 16, 1>), dim3(blocks), dim3(256), 0, s, st, prm, fb, list, cnt); break;
+            case 32: hipLaunchKernelGGL((k_feature<T, 32, 1>), dim3(blocks), dim3(256), 0, s, st, prm, fb, list, cnt); break;
+            case 64: hipLaunchKernelGGL((k_feature<T, 64, 1>), dim3(blocks), dim3(256), 0, s, st, prm, fb, list, cnt); break;
+            default: hipLaunchKernelGGL((k_feature<T, 64, 2>), dim3(blocks), dim3(256), 0, s, st, prm, fb, list, cnt); break;
         }
     }
 }
@@ -2011,7 +2026,8 @@ template <typename T, int BPT, int NT>
 static void launch_info_cfg(hipStream_t s, const DevState<T>& st, const FeatBatch<T>& fb, const UpdWs<T>& ws) {
     const int fbn = info_fb(st.Nmax);
     const size_t lds = ((size_t)2 * fbn * info_slot_doubles(st.Nmax) + 2 * (size_t)ws.Cmax + 1) * sizeof(double) +
-                       2 * fbn * sizeof(unsigned long long) + ((size_t)ws.Cmax + 2 * fbn * st.Nmax) * sizeof(int);
+                       4 * fbn * sizeof(unsigned long long) + ((size_t)ws.Cmax + 2 * fbn * st.Nmax) * sizeof(int);
+    const int nblk = st.Nmax * (st.Nmax + 1) / 2, parts = (nblk + NT * BPT - 1) / (NT * BPT);
     static size_t attr = 64 * 1024;   // dynamic LDS granted so far (default 64 KB)
     if (lds > attr) {
         (void)hipFuncSetAttribute((const void*)k_info<T, BPT, NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2023,7 +2039,9 @@ static void launch_info_cfg(hipStream_t s, const DevState<T>& st, const FeatBatc
         const char* e = getenv("MSCKF_INFO_PHASES");
         phases = e ? atoi(e) : 3;
     }
-    hipLaunchKernelGGL((k_info<T, BPT, NT>), dim3(st.B), dim3(NT), lds, s, st, fb, ws, INFO_TOL_REL, phases,
+    // the pivoted Cholesky needs every block in one workgroup: update_mode() only
+    // selects it when parts == 1
+    hipLaunchKernelGGL((k_info<T, BPT, NT>), dim3(st.B, parts), dim3(NT), lds, s, st, fb, ws, INFO_TOL_REL, phases,
                        update_mode(ws.Cmax) == UPD_CHOL ? 1 : 0);
 }
 
@@ -2041,7 +2059,8 @@ int update_mode(int Cmax) {
         if (e && e[0] == 'q') mode = UPD_QR;
         if (e && e[0] == 'p') mode = UPD_PCHOL;
     }
-    if (mode == UPD_CHOL && !kalman_chol_supported(Cmax)) return UPD_PCHOL;
+    const int N = Cmax / 6;
+    if (mode == UPD_PCHOL && N * (N + 1) / 2 > 1024) return UPD_CHOL;   // k_info's pivoted Cholesky: one workgroup
     return mode;
 }
 
@@ -2054,8 +2073,7 @@ void launch_compress(hipStream_t s, const DevState<T>& st, const FeatBatch<T>& f
     const int nblk = st.Nmax * (st.Nmax + 1) / 2;   // 6x6 cam-pair blocks of A (lower triangle)
     if (nblk <= 256) launch_info_cfg<T, 1, 256>(s, st, fb, ws);
     else if (nblk <= 512) launch_info_cfg<T, 1, 512>(s, st, fb, ws);
-    else if (nblk <= 1024) launch_info_cfg<T, 1, 1024>(s, st, fb, ws);
-    else launch_info_cfg<T, 3, 1024>(s, st, fb, ws);   // Nmax <= 64 (3072 blocks)
+    else launch_info_cfg<T, 1, 1024>(s, st, fb, ws);   // Nmax > 44: several workgroups per filter (assembly only)
 }
 
 template <typename T>

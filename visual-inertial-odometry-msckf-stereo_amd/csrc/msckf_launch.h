@@ -71,8 +71,8 @@ void launch_triangulate(hipStream_t, const DevState<T>&, const Params<T>&, const
 // Per-feature kernels packed S lanes per feature: features listed by class
 // (M <= S), 64/S features per wavefront.
 struct SegClasses {
-    static constexpr int NC = 4;
-    static constexpr int S[NC] = {8, 16, 32, 64};
+    static constexpr int NC = 5;
+    static constexpr int S[NC] = {8, 16, 32, 64, 128};   // 128: a whole wavefront, 2 observations per lane
     const int* list = nullptr;
     int off[NC + 1] = {};
 };
@@ -103,6 +103,7 @@ enum UpdateMode { UPD_CHOL = 0, UPD_PCHOL = 1, UPD_QR = 2 };
 int update_mode(int Cmax);
 bool feature_needs_compact(int maxM, int Cmax);
 bool kalman_chol_supported(int Cmax);
+size_t kalman_global_ws_doubles(int Cmax);
 template <typename T>
 void launch_kalman_chol(hipStream_t, const DevState<T>&, const Params<T>&, const UpdWs<T>&, KernelTimer*);
 template <typename T>
