@@ -21,6 +21,7 @@
 
 #include "msckf_common.h"
 #include "msckf_launch.h"
+#include "msckf_rchol.h"
 
 namespace msckf {
 
@@ -1341,6 +1342,87 @@ __global__ void __launch_bounds__(256) k_gate_wave(DevState<T> st, Params<T> prm
 #undef OK
 }
 
+// Large-track gating (34 < M <= 62): the saddle-point LDL^T of k_gate_wave on
+// rchol_core's fp64 register tiles, one workgroup per feature.  The 4M Y
+// pivots are eliminated; the trailing 4x4 tile is the negated
+// [[H_f^T Y^-1 H_f, .], [., r^T Y^-1 r]] block, finished by one thread with
+// the three negative pivots: gamma = -(last pivot).  Y entries are formed
+// on load from the fp64-staged Hx rows and the P blocks.
+template <typename T, int NT, int TPL>
+__global__ void __launch_bounds__(NT) k_gate_big(DevState<T> st, Params<T> prm, FeatBatch<T> fb,
+                                                 const int* __restrict__ flist) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    const int f = flist[blockIdx.x];
+    if (!fb.valid[f]) {
+        if (threadIdx.x == 0) { fb.gamma[f] = T(NAN); fb.accept[f] = 0; }
+        return;
+    }
+    const int b = fb.feat_filter[f];
+    const int o0 = fb.obs_off[f], M = fb.obs_off[f + 1] - o0, n4 = 4 * M;
+    const int nrow = M + 1;
+    double* hx = reinterpret_cast<double*>(smem_raw);   // [M][24] Hx rows, then [M][4] residuals
+    double* rr = hx + 24 * M;
+    double* corner = rr + 4 * M;                         // [16]
+    int* slot = reinterpret_cast<int*>(corner + 16);     // [M]
+    double* lds = reinterpret_cast<double*>(slot + ((M + 3) & ~3));   // rchol panel buffers
+    const T* ws = fb.obs_ws + (size_t)o0 * OBS_WS;
+    for (int e = threadIdx.x; e < 24 * M; e += NT) {
+        const int o = e / 24;
+        hx[e] = (double)ws[(size_t)o * OBS_WS + OBS_HX + (e - 24 * o)];
+    }
+    for (int e = threadIdx.x; e < 4 * M; e += NT) rr[e] = (double)ws[(size_t)(e >> 2) * OBS_WS + OBS_R + (e & 3)];
+    for (int i = threadIdx.x; i < M; i += NT) slot[i] = fb.obs_cam[o0 + i];
+    __syncthreads();
+    const T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
+    const int ldp = st.Dmax;
+    const double s2 = (double)prm.sigma2;
+    auto load = [&](int i, int j) -> double {
+        if (i < j) { const int t = i; i = j; j = t; }
+        if (i >= n4) {   // [H_f^T ; r^T] rows, zero corner
+            if (j >= n4) return 0.0;
+            const int x = i - n4, l = j >> 2, c = j & 3;
+            return x < 3 ? -hx[24 * l + 6 * c + 3 + x] : rr[4 * l + c];
+        }
+        const int oi = i >> 2, oj = j >> 2;
+        const double* hi = hx + 24 * oi + 6 * (i & 3);
+        const double* hj = hx + 24 * oj + 6 * (j & 3);
+        const T* Pb = P + (size_t)(21 + 6 * slot[oi]) * ldp + 21 + 6 * slot[oj];
+        double y = i == j ? s2 : 0.0;
+        for (int u = 0; u < 6; ++u) {
+            double t = 0;
+            for (int v = 0; v < 6; ++v) t += (double)Pb[(size_t)u * ldp + v] * hj[v];
+            y += hi[u] * t;
+        }
+        return y;
+    };
+    auto panel = [](int, int, double, double, double, double) {};
+    auto trail = [&](int i, int j, double v) { corner[(i - n4) * 4 + (j - n4)] = v; };
+    const bool ok = rchol_core<NT, TPL>(nrow, nrow, M, lds, load, panel, trail);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        T gam = T(INFINITY);
+        if (ok) {
+            const double* a = corner;
+            const double d0 = a[0];
+            const double l10 = a[4] / d0, l20 = a[8] / d0, l30 = a[12] / d0;
+            const double d1 = a[5] - l10 * l10 * d0;
+            const double l21 = (a[9] - l20 * l10 * d0) / d1;
+            const double l31 = (a[13] - l30 * l10 * d0) / d1;
+            const double d2 = a[10] - l20 * l20 * d0 - l21 * l21 * d1;
+            const double l32 = (a[14] - l30 * l20 * d0 - l31 * l21 * d1) / d2;
+            const double d3 = a[15] - l30 * l30 * d0 - l31 * l31 * d1 - l32 * l32 * d2;
+            if (d0 < 0.0 && d1 < 0.0 && d2 < 0.0 && -d3 == -d3) gam = (T)(-d3);
+        }
+        fb.gamma[f] = gam;
+        fb.accept[f] = (gam < fb.chi2[f]) ? 1 : 0;
+    }
+}
+
+size_t gate_big_lds_bytes(int maxM) {
+    return (24 * (size_t)maxM + 4 * maxM + 16) * sizeof(double) + ((maxM + 3) & ~3) * sizeof(int) +
+           rchol_lds_doubles(maxM + 1) * sizeof(double);
+}
+
 // ===========================================================================
 // Stacking in feature order with the row cap (msckf.py:671-679): one thread
 // per filter walks its features; decides the compression (msckf.py:549).
@@ -1992,7 +2074,21 @@ void launch_gate(hipStream_t s, const DevState<T>& st, const Params<T>& prm, con
         if (cnt == 0) continue;
         const int maxM = gc.maxM[c];
         const int* list = gc.list + gc.off[c];
-        if (mode == 0 && c < GateClasses::NC - 1) {
+        if (mode == 0 && c == GateClasses::NC - 2) {   // 34 < M <= 62: register tiles, one workgroup per feature
+            const int nrow = maxM + 1, tiles = nrow * (nrow + 1) / 2;
+            const size_t lds = gate_big_lds_bytes(maxM);
+            if (tiles <= 256 * 4) {
+                static bool a1 = false;
+                if (!a1) { (void)hipFuncSetAttribute((const void*)k_gate_big<T, 256, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); a1 = true; }
+                hipLaunchKernelGGL((k_gate_big<T, 256, 4>), dim3(cnt), dim3(256), lds, s, st, prm, fb, list);
+            } else {
+                static bool a2 = false;
+                if (!a2) { (void)hipFuncSetAttribute((const void*)k_gate_big<T, 512, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); a2 = true; }
+                hipLaunchKernelGGL((k_gate_big<T, 512, 4>), dim3(cnt), dim3(512), lds, s, st, prm, fb, list);
+            }
+            continue;
+        }
+        if (mode == 0 && c < GateClasses::NC - 2) {
             switch (GateClasses::TPL[c]) {
                 case 1: launch_gate_wave<T, 1>(s, st, prm, fb, list, cnt, maxM); break;
                 case 2: launch_gate_wave<T, 2>(s, st, prm, fb, list, cnt, maxM); break;

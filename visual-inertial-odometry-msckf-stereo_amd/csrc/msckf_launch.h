@@ -79,14 +79,15 @@ struct SegClasses {
 template <typename T>
 void launch_feature(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&, const SegClasses&);
 // Feature index lists per gating size class (device pointer + host offsets).
-// Gating size classes by observation count M.  Class c < NC-1 runs the
+// Gating size classes by observation count M.  Class c < NC-2 runs the
 // one-wave register-tile kernel with TPL[c] 4x4 tiles per lane (enough for the
-// (M+1)(M+2)/2 tiles of the augmented 4M+1 matrix); the last class runs the
-// workgroup LDS kernel.
+// (M+1)(M+2)/2 tiles of the augmented 4M+4 matrix); class NC-2 (M <= 62) the
+// workgroup register-tile kernel k_gate_big; the last class the workgroup LDS
+// kernel (or its global-memory variant).
 struct GateClasses {
-    static constexpr int NC = 8;
-    static constexpr int LIM[NC] = {9, 14, 18, 21, 26, 30, 34, 1 << 30};
-    static constexpr int TPL[NC - 1] = {1, 2, 3, 4, 6, 8, 10};
+    static constexpr int NC = 9;
+    static constexpr int LIM[NC] = {9, 14, 18, 21, 26, 30, 34, 62, 1 << 30};
+    static constexpr int TPL[NC - 2] = {1, 2, 3, 4, 6, 8, 10};   // one-wave classes
     const int* list = nullptr;
     int off[NC + 1] = {};
     int maxM[NC] = {};

@@ -1,0 +1,134 @@
+// msckf_rchol.h -- register-tile blocked partial Cholesky shared by the
+// Kalman stages (msckf_kalman.hip) and the large-track gating kernel.
+#pragma once
+#include "msckf_common.h"
+
+namespace msckf {
+
+// ===========================================================================
+// Register-tile partial Cholesky.  The lower tiles (ti, tl), tl < ncol,
+// tl <= ti < nrow, enumerated column-major; tile t lives in thread t % NT,
+// slot t / NT.  Eliminates tile columns 0..nelim-1 (4 pivots per step):
+//   1. owners of the step's tile column dump it to LDS (double-buffered)
+//   2. every thread factors the 4x4 diagonal tile (uniform) and transforms
+//      panel rows (one row per thread): W = A_panel L_d^-T -> LDS + panel()
+//   3. every tile right of the panel takes A -= W_i W_l^T from registers
+// Two barriers per step.  Tiles in columns >= nelim end as the Schur
+// complement and are handed to trail().  In the LDS column buffer each 4-row
+// block takes RB = 18 doubles (144 B): consecutive lanes read consecutive
+// blocks with ds_read_b128, and a 144-B stride spreads a 16-lane group over
+// all 64 banks (a 128-B stride would put it on two).
+// load(i, j) must be symmetric on the square part (diagonal tiles read both
+// triangles).
+// ===========================================================================
+constexpr int RB = 18;   // doubles per 4-row block of the LDS column buffer
+
+template <int NT, int TPL, class Load, class Panel, class Trail>
+__device__ __forceinline__ bool rchol_core(int nrow, int ncol, int nelim, double* lds, Load load, Panel panel,
+                                           Trail trail) {
+    const int tid = threadIdx.x;
+    const int ntiles = ncol * nrow - ncol * (ncol - 1) / 2;
+    int crd[TPL], tlmax[TPL];
+#pragma unroll
+    for (int s = 0; s < TPL; ++s) {
+        const int t = NT * s + tid;
+        const int c = colmajor_col(t < ntiles ? t : 0, nrow);
+        const int rem = (t < ntiles ? t : 0) - (c * nrow - c * (c - 1) / 2);
+        crd[s] = t < ntiles ? ((c + rem) | (c << 16)) : -1;
+        const int tm = NT * s + NT - 1 < ntiles - 1 ? NT * s + NT - 1 : ntiles - 1;
+        tlmax[s] = NT * s < ntiles ? colmajor_col(tm, nrow) : -1;
+    }
+#define RTI(s) (crd[s] & 0xffff)
+#define RTL(s) (crd[s] >> 16)
+#define ROK(s) (crd[s] >= 0)
+    double a[TPL][4][4];
+#pragma unroll
+    for (int s = 0; s < TPL; ++s) {
+        const int i0 = 4 * RTI(s), j0 = 4 * RTL(s);
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+#pragma unroll
+            for (int y = 0; y < 4; ++y) a[s][x][y] = ROK(s) ? load(i0 + x, j0 + y) : 0.0;
+    }
+    bool fail = false;
+    for (int tj = 0; tj < nelim; ++tj) {
+        double* buf = lds + (tj & 1) * RB * nrow;   // [nrow][RB]: rows 4 t + x at RB t + 4 x
+#pragma unroll
+        for (int s = 0; s < TPL; ++s) {
+            if (!ROK(s) || RTL(s) != tj) continue;
+            double* dst = buf + RB * RTI(s);
+#pragma unroll
+            for (int x = 0; x < 4; ++x)
+#pragma unroll
+                for (int y = 0; y < 4; ++y) dst[4 * x + y] = a[s][x][y];
+        }
+        LDS_BARRIER();
+        const double* dt = buf + RB * tj;
+        const double l00 = sqrt(dt[0]);
+        const double i00 = 1.0 / l00;
+        const double l10 = dt[4] * i00, l20 = dt[8] * i00, l30 = dt[12] * i00;
+        const double l11 = sqrt(dt[5] - l10 * l10);
+        const double i11 = 1.0 / l11;
+        const double l21 = (dt[9] - l20 * l10) * i11, l31 = (dt[13] - l30 * l10) * i11;
+        const double l22 = sqrt(dt[10] - l20 * l20 - l21 * l21);
+        const double i22 = 1.0 / l22;
+        const double l32 = (dt[14] - l30 * l20 - l31 * l21) * i22;
+        const double l33 = sqrt(dt[15] - l30 * l30 - l31 * l31 - l32 * l32);
+        const double i33 = 1.0 / l33;
+        if (!(l00 > 0.0) || !(l11 > 0.0) || !(l22 > 0.0) || !(l33 > 0.0)) { fail = true; break; }
+        for (int r = 4 * tj + 4 + tid; r < 4 * nrow; r += NT) {
+            double* row = buf + RB * (r >> 2) + 4 * (r & 3);
+            const double w0 = row[0] * i00;
+            const double w1 = (row[1] - w0 * l10) * i11;
+            const double w2 = (row[2] - w0 * l20 - w1 * l21) * i22;
+            const double w3 = (row[3] - w0 * l30 - w1 * l31 - w2 * l32) * i33;
+            row[0] = w0; row[1] = w1; row[2] = w2; row[3] = w3;
+            panel(r, 4 * tj, w0, w1, w2, w3);
+        }
+        if (tid < 4) {
+            const int r = 4 * tj + tid;
+            if (tid == 0) panel(r, 4 * tj, l00, 0.0, 0.0, 0.0);
+            if (tid == 1) panel(r, 4 * tj, l10, l11, 0.0, 0.0);
+            if (tid == 2) panel(r, 4 * tj, l20, l21, l22, 0.0);
+            if (tid == 3) panel(r, 4 * tj, l30, l31, l32, l33);
+        }
+        LDS_BARRIER();
+#pragma unroll
+        for (int s = 0; s < TPL; ++s) {
+            if (tlmax[s] <= tj) continue;   // slot entirely in finished columns
+            if (!ROK(s) || RTL(s) <= tj) continue;
+            const double* ri = buf + RB * RTI(s);
+            const double* rl = buf + RB * RTL(s);
+            double u[4][4], w[4][4];
+#pragma unroll
+            for (int x = 0; x < 4; ++x)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) { u[x][c] = ri[4 * x + c]; w[x][c] = rl[4 * x + c]; }
+#pragma unroll
+            for (int x = 0; x < 4; ++x)
+#pragma unroll
+                for (int y = 0; y < 4; ++y)
+                    a[s][x][y] -= u[x][0] * w[y][0] + u[x][1] * w[y][1] + u[x][2] * w[y][2] + u[x][3] * w[y][3];
+            asm volatile("" ::: "memory");
+        }
+    }
+    if (!fail) {
+#pragma unroll
+        for (int s = 0; s < TPL; ++s) {
+            if (!ROK(s) || RTL(s) < nelim) continue;
+            const int i0 = 4 * RTI(s), j0 = 4 * RTL(s);
+#pragma unroll
+            for (int x = 0; x < 4; ++x)
+#pragma unroll
+                for (int y = 0; y < 4; ++y) trail(i0 + x, j0 + y, a[s][x][y]);
+        }
+    }
+#undef RTI
+#undef RTL
+#undef ROK
+    return !fail;
+}
+
+__host__ __device__ constexpr int rchol_lds_doubles(int nrow) { return 2 * RB * nrow; }
+
+}  // namespace msckf
