@@ -462,20 +462,26 @@ size_t kalman_global_ws_doubles(int Cmax) {   // per filter, 0 when the register
 }
 
 // ===========================================================================
-// 64 x 64 output tile, 256 threads (4 x 4 each), K in steps of 16 through LDS.
-// A(i, k) and B(k, j) are accessors; *_KFAST says whether consecutive k are
-// contiguous in memory for that operand (selects the coalesced load mapping).
+// 64 x 64 output tile on the matrix cores: 256 threads = 4 waves, wave w owns
+// the 32 x 32 quarter (w >> 1, w & 1) as 2 x 2 v_mfma_f64_16x16x4 tiles; K in
+// steps of 16 staged through LDS ([k][i] / [k][j], rows padded to 80 doubles so
+// the two k-rows a 32-lane group reads land on disjoint banks).  A(i, k) and
+// B(k, j) are accessors; *_KFAST says whether consecutive k are contiguous in
+// memory for that operand (selects the coalesced load mapping).  store(i, j, v)
+// receives every in-range output element once.
 // ===========================================================================
-constexpr int GT = 64, GK = 16;
+constexpr int GT = 64, GK = 16, GPAD = 80;
 
-template <bool A_KFAST, bool B_KFAST, class FA, class FB>
-__device__ __forceinline__ void gemm64(int m, int n, int kb, int ke, int i0, int j0, FA A, FB B, double acc[4][4]) {
-    __shared__ __attribute__((aligned(16))) double sa[GK][GT + 4], sb[GK][GT + 4];
-    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+template <bool A_KFAST, bool B_KFAST, class FA, class FB, class FS>
+__device__ __forceinline__ void gemm64(int m, int n, int kb, int ke, int i0, int j0, FA A, FB B, FS store) {
+    __shared__ __attribute__((aligned(16))) double sa[GK][GPAD], sb[GK][GPAD];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wr = w >> 1, wc = w & 1, lc = lane & 15, lr = lane >> 4;
+    v4d acc[2][2];
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-        for (int v = 0; v < 4; ++v) acc[u][v] = 0;
+        for (int ni = 0; ni < 2; ++ni) acc[mi][ni] = v4d{0.0, 0.0, 0.0, 0.0};
     for (int k0 = kb; k0 < ke; k0 += GK) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -489,18 +495,32 @@ __device__ __forceinline__ void gemm64(int m, int n, int kb, int ke, int i0, int
             sb[k2][jj] = (gj < n && gk2 < ke) ? B(gk2, gj) : 0.0;
         }
         __syncthreads();
-#pragma unroll 4
-        for (int kk = 0; kk < GK; ++kk) {
-            double av[4], bv[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) { av[u] = sa[kk][4 * ty + u]; bv[u] = sb[kk][4 * tx + u]; }
+        for (int kc = 0; kc < GK / 4; ++kc) {
+            const int kr = 4 * kc + lr;
+            double av[2], bv[2];
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
+            for (int t = 0; t < 2; ++t) {
+                av[t] = sa[kr][32 * wr + 16 * t + lc];
+                bv[t] = sb[kr][32 * wc + 16 * t + lc];
+            }
 #pragma unroll
-                for (int v = 0; v < 4; ++v) acc[u][v] += av[u] * bv[v];
+            for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < 2; ++ni)
+                    acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[mi], bv[ni], acc[mi][ni], 0, 0, 0);
         }
         __syncthreads();
     }
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = i0 + 32 * wr + 16 * mi + lr + 4 * r, j = j0 + 32 * wc + 16 * ni + lc;
+                if (i < m && j < n) store(i, j, acc[mi][ni][r]);
+            }
 }
 
 // ---- stage B1: G = A Lc (C x C) ----
@@ -515,18 +535,10 @@ __global__ void __launch_bounds__(256) k_kal_b1(DevState<T> st, UpdWs<T> ws) {
     const KT* Am = ws.Hthin + (size_t)b * ws.Cmax * lda;
     const KT* Lc = ws.Lc + (size_t)b * Cpw * Cpw;
     KT* G = ws.G + (size_t)b * ws.Cmax * lda;
-    double acc[4][4];
     gemm64<true, false>(C, C, j0 & ~(GK - 1), C, i0, j0,
                         [&](int i, int k) { return Am[(size_t)i * lda + k]; },
-                        [&](int k, int j) { return k >= j ? Lc[(size_t)k * Cpw + j] : 0.0; }, acc);
-    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-            const int i = i0 + 4 * ty + u, j = j0 + 4 * tx + v;
-            if (i < C && j < C) G[(size_t)i * lda + j] = acc[u][v];
-        }
+                        [&](int k, int j) { return k >= j ? Lc[(size_t)k * Cpw + j] : 0.0; },
+                        [&](int i, int j, double v) { G[(size_t)i * lda + j] = v; });
 }
 
 // ---- stage B2: [T | c] = s2 I + Lc^T [G | b] (lower triangle of T, and c) ----
@@ -543,22 +555,123 @@ __global__ void __launch_bounds__(256) k_kal_b2(DevState<T> st, Params<T> prm, U
     const KT* G = ws.G + (size_t)b * ws.Cmax * ld;
     const KT* Hb = ws.Hthin + (size_t)b * ws.Cmax * ld;   // b in column Cmax
     KT* Tm = ws.Tm + (size_t)b * ws.Cmax * ld;
-    double acc[4][4];
+    const double s2 = (double)prm.sigma2;
     gemm64<false, false>(C, C + 1, i0 & ~(GK - 1), C, i0, j0,
                          [&](int i, int k) { return k >= i ? Lc[(size_t)k * Cpw + i] : 0.0; },
                          [&](int k, int j) { return j < C ? G[(size_t)k * ld + j] : Hb[(size_t)k * ld + ws.Cmax]; },
-                         acc);
-    const double s2 = (double)prm.sigma2;
-    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-            const int i = i0 + 4 * ty + u, j = j0 + 4 * tx + v;
-            if (i >= C) continue;
-            if (j < C && j <= i) Tm[(size_t)i * ld + j] = acc[u][v] + (i == j ? s2 : 0.0);
-            if (j == C) Tm[(size_t)i * ld + C] = acc[u][v];
+                         [&](int i, int j, double v) {
+                             if (j < C && j <= i) Tm[(size_t)i * ld + j] = v + (i == j ? s2 : 0.0);
+                             if (j == C) Tm[(size_t)i * ld + C] = v;
+                         });
+}
+
+// ---- stage B, one workgroup per filter (production path when C <= 16 * 12) ----
+// Phase 1: G = A Lc over the full nT x nT tile grid (wave w owns tiles w + 16 s);
+// Phase 2: lower tiles of T = s2 I + Lc^T G and c = Lc^T b.  K streams in
+// chunks of 16 rows through double-buffered LDS images [k][col]; both operands
+// are row slices in memory (A is stored symmetric), so every load is coalesced.
+// Chunks that meet only the zero upper triangle of Lc are skipped per tile.
+template <int TPW>
+__device__ __forceinline__ void tile_of(int t, int nT, bool lower, int& ti, int& tj) {
+    if (!lower) {
+        ti = t / nT;
+        tj = t - ti * nT;
+        return;
+    }
+    int i = (int)((sqrtf(8.0f * (float)t + 1.0f) - 1.0f) * 0.5f);
+    while (i * (i + 1) / 2 > t) --i;
+    while ((i + 1) * (i + 2) / 2 <= t) ++i;
+    ti = i;
+    tj = t - i * (i + 1) / 2;
+}
+
+template <typename T, int TPW>
+__global__ void __launch_bounds__(1024) k_kal_b(DevState<T> st, Params<T> prm, UpdWs<T> ws) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    const int b = blockIdx.x;
+    if (ws.info[4 * b] == 0) return;
+    const int C = 6 * st.ncams[b], nT = (C + 15) / 16, Cq = 16 * nT;
+    const int tid = threadIdx.x, lane = tid & 63, lc = lane & 15, lr = lane >> 4;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int ld = ws.Cmax + 1, Cpw = ws.Cp;
+    const KT* Am = ws.Hthin + (size_t)b * ws.Cmax * ld;   // b in column Cmax
+    const KT* Lc = ws.Lc + (size_t)b * Cpw * Cpw;
+    KT* G = ws.G + (size_t)b * ws.Cmax * ld;
+    KT* Tm = ws.Tm + (size_t)b * ws.Cmax * ld;
+    double* img = reinterpret_cast<double*>(smem_raw);   // [2 buf][2 op][16][Cq], then [2][16] b chunk
+    double* bb = img + 4 * 16 * Cq;
+    v4d acc[TPW];
+    int ti[TPW], tj[TPW];
+    // operand 0 = rows of X (A in phase 1, Lc in phase 2), operand 1 = rows of Y (Lc, G)
+    auto stage = [&](int ph, int k0, int buf) {
+        double* i0 = img + (2 * buf) * 16 * Cq;
+        double* i1 = i0 + 16 * Cq;
+        for (int e = tid; e < 16 * Cq; e += 1024) {
+            const int k = e / Cq, c = e - k * Cq, gk = k0 + k;
+            const bool in = gk < C && c < C;
+            const double lcv = (in && c <= gk) ? Lc[(size_t)gk * Cpw + c] : 0.0;
+            if (ph == 0) {
+                i0[e] = in ? Am[(size_t)gk * ld + c] : 0.0;
+                i1[e] = lcv;
+            } else {
+                i0[e] = lcv;
+                i1[e] = in ? G[(size_t)gk * ld + c] : 0.0;
+            }
         }
+        if (ph == 1 && tid < 16) bb[buf * 16 + tid] = k0 + tid < C ? Am[(size_t)(k0 + tid) * ld + ws.Cmax] : 0.0;
+    };
+    double ca = 0.0;
+    for (int ph = 0; ph < 2; ++ph) {
+        const int ntl = ph == 0 ? nT * nT : nT * (nT + 1) / 2;
+#pragma unroll
+        for (int s = 0; s < TPW; ++s) {
+            const int t = wv + 16 * s;
+            int a, c;
+            tile_of<TPW>(t, nT, ph == 1, a, c);
+            ti[s] = __builtin_amdgcn_readfirstlane(t < ntl ? a : -1);
+            tj[s] = __builtin_amdgcn_readfirstlane(c);
+            acc[s] = v4d{0.0, 0.0, 0.0, 0.0};
+        }
+        stage(ph, 0, 0);
+        __syncthreads();
+        for (int k0 = 0, it = 0; k0 < C; k0 += 16, ++it) {
+            const int buf = it & 1;
+            if (k0 + 16 < C) stage(ph, k0 + 16, buf ^ 1);
+            const double* i0 = img + (2 * buf) * 16 * Cq;
+            const double* i1 = i0 + 16 * Cq;
+#pragma unroll
+            for (int s = 0; s < TPW; ++s) {
+                if (ti[s] < 0) continue;
+                // Lc[k][j] = 0 for j > k: phase 1 needs k >= 16 tj, phase 2 k >= 16 ti
+                if (k0 + 15 < 16 * (ph == 0 ? tj[s] : ti[s])) continue;
+#pragma unroll
+                for (int kc = 0; kc < 4; ++kc) {
+                    const int kr = (4 * kc + lr) * Cq;
+                    acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(i0[kr + 16 * ti[s] + lc], i1[kr + 16 * tj[s] + lc],
+                                                                  acc[s], 0, 0, 0);
+                }
+            }
+            if (ph == 1 && tid < C) {
+#pragma unroll
+                for (int k = 0; k < 16; ++k) ca += i0[k * Cq + tid] * bb[buf * 16 + k];
+            }
+            __syncthreads();
+        }
+        const double s2 = (double)prm.sigma2;
+#pragma unroll
+        for (int s = 0; s < TPW; ++s) {
+            if (ti[s] < 0) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = 16 * ti[s] + lr + 4 * r, j = 16 * tj[s] + lc;
+                if (i >= C || j >= C) continue;
+                if (ph == 0) G[(size_t)i * ld + j] = acc[s][r];
+                else if (j <= i) Tm[(size_t)i * ld + j] = acc[s][r] + (i == j ? s2 : 0.0);
+            }
+        }
+        __syncthreads();   // G visible to the whole workgroup before phase 2 streams it
+    }
+    if (tid < C) Tm[(size_t)tid * ld + C] = ca;
 }
 
 // ---- stage E: P+ = blockdiag(S_ii, 0) + s2 W W^T (lower tiles, mirrored), dx = W y ----
@@ -575,25 +688,98 @@ __global__ void __launch_bounds__(256) k_kal_e(DevState<T> st, Params<T> prm, Up
     const KT* Sii = ws.Sii + (size_t)b * KW * KW;
     T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
     KT* dx = ws.dx + (size_t)b * (st.Dmax + ws.Cmax);
-    double acc[4][4];
-    gemm64<true, true>(D, D + 1, 0, C, i0, j0, [&](int i, int k) { return W[(size_t)i * Cpw + k]; },
-                       [&](int k, int j) { return W[(size_t)(j < D ? j : D) * Cpw + k]; }, acc);
     const double s2 = (double)prm.sigma2;
-    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    gemm64<true, true>(D, D + 1, 0, C, i0, j0, [&](int i, int k) { return W[(size_t)i * Cpw + k]; },
+                       [&](int k, int j) { return W[(size_t)(j < D ? j : D) * Cpw + k]; },
+                       [&](int i, int j, double v) {
+                           if (j < D && j <= i) {
+                               double p = s2 * v;
+                               if (i < 21 && j < 21) p += Sii[i * KW + j];
+                               P[(size_t)i * ld + j] = (T)p;
+                               P[(size_t)j * ld + i] = (T)p;
+                           }
+                           if (j == D) dx[i] = v;
+                       });
+}
+
+// ---- stage E, one workgroup per filter (production path when D fits) ----
+// 16 waves; wave w owns lower 16 x 16 tiles t = w + 16 s (s < TPW) of P+ as
+// MFMA accumulators.  W streams once through double-buffered LDS in chunks of
+// 16 columns ([k][row] images, so each MFMA operand is one ds_read_b64); the
+// same chunks give dx = W y (thread i < D accumulates row i).
+template <typename T, int TPW>
+__global__ void __launch_bounds__(1024) k_kal_e1(DevState<T> st, Params<T> prm, UpdWs<T> ws) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    const int b = blockIdx.x;
+    if (ws.info[4 * b] == 0 || ws.info[4 * b + 3] < 0) return;
+    const int C = 6 * st.ncams[b], D = 21 + C, nT = (D + 15) / 16, Dp = 16 * nT;
+    const int tid = threadIdx.x, lane = tid & 63, lc = lane & 15, lr = lane >> 4;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int ntiles = nT * (nT + 1) / 2;
+    const int Cpw = ws.Cp, ld = st.Dmax;
+    const KT* W = ws.W + (size_t)b * (st.Dmax + 1) * Cpw;
+    double* img = reinterpret_cast<double*>(smem_raw);   // [2][16][Dp] chunk images, then [2][16] y
+    double* yb = img + 2 * 16 * Dp;
+    int ti[TPW], tj[TPW];
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int s = 0; s < TPW; ++s) {   // row-major lower enumeration of the tile grid
+        const int t = wv + 16 * s;
+        int i = (int)((sqrtf(8.0f * (float)t + 1.0f) - 1.0f) * 0.5f);
+        while (i * (i + 1) / 2 > t) --i;
+        while ((i + 1) * (i + 2) / 2 <= t) ++i;
+        ti[s] = __builtin_amdgcn_readfirstlane(t < ntiles ? i : -1);
+        tj[s] = __builtin_amdgcn_readfirstlane(t - i * (i + 1) / 2);
+    }
+    v4d acc[TPW];
 #pragma unroll
-        for (int v = 0; v < 4; ++v) {
-            const int i = i0 + 4 * ty + u, j = j0 + 4 * tx + v;
-            if (i >= D) continue;
-            if (j < D && j <= i) {
-                double p = s2 * acc[u][v];
-                if (i < 21 && j < 21) p += Sii[i * KW + j];
-                P[(size_t)i * ld + j] = (T)p;
-                P[(size_t)j * ld + i] = (T)p;
-            }
-            if (j == D) dx[i] = acc[u][v];
+    for (int s = 0; s < TPW; ++s) acc[s] = v4d{0.0, 0.0, 0.0, 0.0};
+    double dxa = 0.0;
+    auto stage = [&](int k0, int buf) {   // W[:, k0:k0+16] -> img[buf][k][row], y chunk
+        double* im = img + buf * 16 * Dp;
+        for (int e = tid; e < 16 * Dp; e += 1024) {
+            const int row = e >> 4, k = e & 15;
+            im[k * Dp + row] = (row < D && k0 + k < C) ? W[(size_t)row * Cpw + k0 + k] : 0.0;
         }
+        if (tid < 16) yb[buf * 16 + tid] = k0 + tid < C ? W[(size_t)D * Cpw + k0 + tid] : 0.0;
+    };
+    stage(0, 0);
+    __syncthreads();
+    for (int k0 = 0, it = 0; k0 < C; k0 += 16, ++it) {
+        const int buf = it & 1;
+        if (k0 + 16 < C) stage(k0 + 16, buf ^ 1);
+        const double* im = img + buf * 16 * Dp;
+#pragma unroll
+        for (int s = 0; s < TPW; ++s) {
+            if (ti[s] < 0) continue;
+#pragma unroll
+            for (int kc = 0; kc < 4; ++kc) {
+                const double* kr = im + (4 * kc + lr) * Dp;
+                acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(kr[16 * ti[s] + lc], kr[16 * tj[s] + lc], acc[s], 0, 0, 0);
+            }
+        }
+        if (tid < D) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) dxa += im[k * Dp + tid] * yb[buf * 16 + k];
+        }
+        __syncthreads();
+    }
+    const double s2 = (double)prm.sigma2;
+    const KT* Sii = ws.Sii + (size_t)b * KW * KW;
+    T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
+#pragma unroll
+    for (int s = 0; s < TPW; ++s) {
+        if (ti[s] < 0) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = 16 * ti[s] + lr + 4 * r, j = 16 * tj[s] + lc;
+            if (i >= D || j >= D || j > i) continue;
+            double p = s2 * acc[s][r];
+            if (i < 21 && j < 21) p += Sii[i * KW + j];
+            P[(size_t)i * ld + j] = (T)p;
+            P[(size_t)j * ld + i] = (T)p;
+        }
+    }
+    if (tid < D) ws.dx[(size_t)b * (st.Dmax + ws.Cmax) + tid] = dxa;
 }
 
 // ===========================================================================
@@ -673,6 +859,26 @@ static void launch_c16(hipStream_t s, const DevState<T>& st, const UpdWs<T>& ws,
     hipLaunchKernelGGL((k_kal_c16<T, NW, TPW>), dim3(groups, st.B), dim3(64 * NW), lds, s, st, ws, ner, dbg);
 }
 
+template <typename T, int TPW>
+static void launch_e1(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const UpdWs<T>& ws, size_t lds) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_kal_e1<T, TPW>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr = true;
+    }
+    hipLaunchKernelGGL((k_kal_e1<T, TPW>), dim3(st.B), dim3(1024), lds, s, st, prm, ws);
+}
+
+template <typename T, int TPW>
+static void launch_b(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const UpdWs<T>& ws, size_t lds) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_kal_b<T, TPW>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr = true;
+    }
+    hipLaunchKernelGGL((k_kal_b<T, TPW>), dim3(st.B), dim3(1024), lds, s, st, prm, ws);
+}
+
 template <typename T>
 void launch_kalman_chol(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const UpdWs<T>& ws,
                         KernelTimer* kt) {
@@ -705,8 +911,14 @@ void launch_kalman_chol(hipStream_t s, const DevState<T>& st, const Params<T>& p
     }
     const int tiles = (Cmax + GT - 1) / GT;
     kt->begin(s, "kalman_b");
-    hipLaunchKernelGGL(k_kal_b1<T>, dim3(tiles, tiles, st.B), dim3(256), 0, s, st, ws);
-    hipLaunchKernelGGL(k_kal_b2<T>, dim3((Cmax + 1 + GT - 1) / GT, tiles, st.B), dim3(256), 0, s, st, prm, ws);
+    if (Cq <= 16 * 8) {
+        launch_b<T, 4>(s, st, prm, ws, (4 * 16 * (size_t)Cq + 32) * sizeof(double));
+    } else if (Cq <= 16 * 12) {
+        launch_b<T, 9>(s, st, prm, ws, (4 * 16 * (size_t)Cq + 32) * sizeof(double));
+    } else {   // large windows: 64 x 64 output tiles, one workgroup each
+        hipLaunchKernelGGL(k_kal_b1<T>, dim3(tiles, tiles, st.B), dim3(256), 0, s, st, ws);
+        hipLaunchKernelGGL(k_kal_b2<T>, dim3((Cmax + 1 + GT - 1) / GT, tiles, st.B), dim3(256), 0, s, st, prm, ws);
+    }
     kt->end(s);
     if (glob) {
         kt->begin(s, "kalman_c");
@@ -740,9 +952,17 @@ void launch_kalman_chol(hipStream_t s, const DevState<T>& st, const Params<T>& p
         else launch_c_cfg<T, 512, 4>(s, st, ws, groups, ner, lds);
         kt->end(s);
     }
-    const int dt = (st.Dmax + GT - 1) / GT, dt1 = (st.Dmax + 1 + GT - 1) / GT;
     kt->begin(s, "kalman_e");
-    hipLaunchKernelGGL(k_kal_e<T>, dim3(dt1, dt, st.B), dim3(256), 0, s, st, prm, ws);
+    const int nTe = (st.Dmax + 15) / 16, tilesE = nTe * (nTe + 1) / 2;
+    const size_t ldsE = (2 * 16 * 16 * (size_t)nTe + 32) * sizeof(double);
+    if (tilesE <= 16 * 6) {
+        launch_e1<T, 6>(s, st, prm, ws, ldsE);
+    } else if (tilesE <= 16 * 8) {
+        launch_e1<T, 8>(s, st, prm, ws, ldsE);
+    } else {   // large windows: one 64 x 64 tile per workgroup
+        const int dt = (st.Dmax + GT - 1) / GT, dt1 = (st.Dmax + 1 + GT - 1) / GT;
+        hipLaunchKernelGGL(k_kal_e<T>, dim3(dt1, dt, st.B), dim3(256), 0, s, st, prm, ws);
+    }
     kt->end(s);
 }
 
