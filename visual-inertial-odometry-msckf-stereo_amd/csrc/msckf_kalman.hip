@@ -565,19 +565,16 @@ __global__ void __launch_bounds__(256) k_kal_b2(DevState<T> st, Params<T> prm, U
                          });
 }
 
-// ---- stage B, one workgroup per filter (production path when C <= 16 * 12) ----
-// Phase 1: G = A Lc over the full nT x nT tile grid (wave w owns tiles w + 16 s);
-// Phase 2: lower tiles of T = s2 I + Lc^T G and c = Lc^T b.  K streams in
-// chunks of 16 rows through double-buffered LDS images [k][col]; both operands
-// are row slices in memory (A is stored symmetric), so every load is coalesced.
-// Chunks that meet only the zero upper triangle of Lc are skipped per tile.
-template <int TPW>
-__device__ __forceinline__ void tile_of(int t, int nT, bool lower, int& ti, int& tj) {
-    if (!lower) {
-        ti = t / nT;
-        tj = t - ti * nT;
-        return;
-    }
+// ---- stage B, one workgroup per filter (production path when C <= 16 * NTM) ----
+// Phase 1: G = A Lc over the full nT x nT tile grid; the NW = WR x WC waves
+// each own a (NTM/WR) x (NTM/WC) block of 16 x 16 tiles, so one k-step reads
+// NTM/WR + NTM/WC operands for their product of MFMAs.
+// Phase 2: lower tiles of T = s2 I + Lc^T G (wave w owns tiles w + NW s of the
+// row-major lower enumeration) and c = Lc^T b.  K streams in chunks of 16 rows
+// through double-buffered LDS images [k][col]; both operands are row slices in
+// memory (A is stored symmetric), so every load is coalesced.  Chunks that
+// meet only the zero upper triangle of Lc are skipped per tile.
+__device__ __forceinline__ void lower_tile(int t, int& ti, int& tj) {
     int i = (int)((sqrtf(8.0f * (float)t + 1.0f) - 1.0f) * 0.5f);
     while (i * (i + 1) / 2 > t) --i;
     while ((i + 1) * (i + 2) / 2 <= t) ++i;
@@ -585,8 +582,12 @@ __device__ __forceinline__ void tile_of(int t, int nT, bool lower, int& ti, int&
     tj = t - i * (i + 1) / 2;
 }
 
-template <typename T, int TPW>
-__global__ void __launch_bounds__(1024) k_kal_b(DevState<T> st, Params<T> prm, UpdWs<T> ws) {
+template <typename T, int NW, int WR, int WC, int NTM>
+__global__ void __launch_bounds__(64 * NW) k_kal_b(DevState<T> st, Params<T> prm, UpdWs<T> ws) {
+    static_assert(WR * WC == NW && NTM % WR == 0 && NTM % WC == 0, "wave grid");
+    constexpr int BR = NTM / WR, BC = NTM / WC;                  // phase-1 tile block per wave
+    constexpr int TP2 = (NTM * (NTM + 1) / 2 + NW - 1) / NW;     // phase-2 tiles per wave
+    constexpr int NT = 64 * NW, Q = (16 * 16 * NTM + NT - 1) / NT;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int b = blockIdx.x;
     if (ws.info[4 * b] == 0) return;
@@ -600,78 +601,139 @@ __global__ void __launch_bounds__(1024) k_kal_b(DevState<T> st, Params<T> prm, U
     KT* Tm = ws.Tm + (size_t)b * ws.Cmax * ld;
     double* img = reinterpret_cast<double*>(smem_raw);   // [2 buf][2 op][16][Cq], then [2][16] b chunk
     double* bb = img + 4 * 16 * Cq;
-    v4d acc[TPW];
-    int ti[TPW], tj[TPW];
-    // operand 0 = rows of X (A in phase 1, Lc in phase 2), operand 1 = rows of Y (Lc, G)
-    auto stage = [&](int ph, int k0, int buf) {
-        double* i0 = img + (2 * buf) * 16 * Cq;
-        double* i1 = i0 + 16 * Cq;
-        for (int e = tid; e < 16 * Cq; e += 1024) {
+    // operand 0 = rows of X (A in phase 1, Lc in phase 2), operand 1 = rows of Y (Lc, G).
+    // load() issues the next chunk's global reads into registers before the
+    // MFMAs of the current one; put() writes them to the other LDS buffer after.
+    double r0[Q], r1[Q], rb = 0.0;
+    auto load = [&](int ph, int k0) {
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const int e = tid + NT * q;
             const int k = e / Cq, c = e - k * Cq, gk = k0 + k;
-            const bool in = gk < C && c < C;
+            const bool in = e < 16 * Cq && gk < C && c < C;
             const double lcv = (in && c <= gk) ? Lc[(size_t)gk * Cpw + c] : 0.0;
-            if (ph == 0) {
-                i0[e] = in ? Am[(size_t)gk * ld + c] : 0.0;
-                i1[e] = lcv;
-            } else {
-                i0[e] = lcv;
-                i1[e] = in ? G[(size_t)gk * ld + c] : 0.0;
+            const double ov = in ? (ph == 0 ? Am : G)[(size_t)gk * ld + c] : 0.0;
+            r0[q] = ph == 0 ? ov : lcv;
+            r1[q] = ph == 0 ? lcv : ov;
+        }
+        if (ph == 1 && tid < 16) rb = k0 + tid < C ? Am[(size_t)(k0 + tid) * ld + ws.Cmax] : 0.0;
+    };
+    auto put = [&](int ph, int buf) {
+        double* i0 = img + (2 * buf) * 16 * Cq;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const int e = tid + NT * q;
+            if (e < 16 * Cq) {
+                i0[e] = r0[q];
+                i0[16 * Cq + e] = r1[q];
             }
         }
-        if (ph == 1 && tid < 16) bb[buf * 16 + tid] = k0 + tid < C ? Am[(size_t)(k0 + tid) * ld + ws.Cmax] : 0.0;
+        if (ph == 1 && tid < 16) bb[buf * 16 + tid] = rb;
     };
-    double ca = 0.0;
-    for (int ph = 0; ph < 2; ++ph) {
-        const int ntl = ph == 0 ? nT * nT : nT * (nT + 1) / 2;
+    // ---- phase 1: G = A Lc ----
+    {
+        const int tr0 = BR * (wv / WC), tc0 = BC * (wv % WC);
+        v4d acc[BR][BC];
 #pragma unroll
-        for (int s = 0; s < TPW; ++s) {
-            const int t = wv + 16 * s;
-            int a, c;
-            tile_of<TPW>(t, nT, ph == 1, a, c);
-            ti[s] = __builtin_amdgcn_readfirstlane(t < ntl ? a : -1);
-            tj[s] = __builtin_amdgcn_readfirstlane(c);
-            acc[s] = v4d{0.0, 0.0, 0.0, 0.0};
-        }
-        stage(ph, 0, 0);
+        for (int x = 0; x < BR; ++x)
+#pragma unroll
+            for (int y = 0; y < BC; ++y) acc[x][y] = v4d{0.0, 0.0, 0.0, 0.0};
+        load(0, 0);
+        put(0, 0);
         __syncthreads();
         for (int k0 = 0, it = 0; k0 < C; k0 += 16, ++it) {
             const int buf = it & 1;
-            if (k0 + 16 < C) stage(ph, k0 + 16, buf ^ 1);
+            const bool more = k0 + 16 < C;
+            if (more) load(0, k0 + 16);
             const double* i0 = img + (2 * buf) * 16 * Cq;
             const double* i1 = i0 + 16 * Cq;
 #pragma unroll
-            for (int s = 0; s < TPW; ++s) {
-                if (ti[s] < 0) continue;
-                // Lc[k][j] = 0 for j > k: phase 1 needs k >= 16 tj, phase 2 k >= 16 ti
-                if (k0 + 15 < 16 * (ph == 0 ? tj[s] : ti[s])) continue;
+            for (int kc = 0; kc < 4; ++kc) {
+                const int kr = (4 * kc + lr) * Cq;
+                double av[BR], bv[BC];
 #pragma unroll
-                for (int kc = 0; kc < 4; ++kc) {
-                    const int kr = (4 * kc + lr) * Cq;
+                for (int x = 0; x < BR; ++x) av[x] = tr0 + x < nT ? i0[kr + 16 * (tr0 + x) + lc] : 0.0;
+#pragma unroll
+                for (int y = 0; y < BC; ++y) bv[y] = tc0 + y < nT ? i1[kr + 16 * (tc0 + y) + lc] : 0.0;
+#pragma unroll
+                for (int x = 0; x < BR; ++x) {
+                    if (tr0 + x >= nT) continue;
+#pragma unroll
+                    for (int y = 0; y < BC; ++y) {
+                        // Lc[k][j] = 0 for j > k: column tile tc needs k >= 16 tc
+                        if (tc0 + y >= nT || k0 + 15 < 16 * (tc0 + y)) continue;
+                        acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[x], bv[y], acc[x][y], 0, 0, 0);
+                    }
+                }
+            }
+            if (more) put(0, buf ^ 1);
+            __syncthreads();
+        }
+#pragma unroll
+        for (int x = 0; x < BR; ++x)
+#pragma unroll
+            for (int y = 0; y < BC; ++y)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int i = 16 * (tr0 + x) + lr + 4 * r, j = 16 * (tc0 + y) + lc;
+                    if (i < C && j < C) G[(size_t)i * ld + j] = acc[x][y][r];
+                }
+        __syncthreads();   // G visible to the whole workgroup before phase 2 streams it
+    }
+    // ---- phase 2: T = s2 I + Lc^T G (lower), c = Lc^T b ----
+    {
+        const int ntl = nT * (nT + 1) / 2;
+        v4d acc[TP2];
+        int ti[TP2], tj[TP2];
+#pragma unroll
+        for (int s = 0; s < TP2; ++s) {
+            const int t = wv + NW * s;
+            int x, y;
+            lower_tile(t, x, y);
+            ti[s] = __builtin_amdgcn_readfirstlane(t < ntl ? x : -1);
+            tj[s] = __builtin_amdgcn_readfirstlane(y);
+            acc[s] = v4d{0.0, 0.0, 0.0, 0.0};
+        }
+        double ca = 0.0;
+        load(1, 0);
+        put(1, 0);
+        __syncthreads();
+        for (int k0 = 0, it = 0; k0 < C; k0 += 16, ++it) {
+            const int buf = it & 1;
+            const bool more = k0 + 16 < C;
+            if (more) load(1, k0 + 16);
+            const double* i0 = img + (2 * buf) * 16 * Cq;
+            const double* i1 = i0 + 16 * Cq;
+#pragma unroll
+            for (int kc = 0; kc < 4; ++kc) {
+                const int kr = (4 * kc + lr) * Cq;
+#pragma unroll
+                for (int s = 0; s < TP2; ++s) {
+                    // Lc[k][i] = 0 for i > k: row tile ti needs k >= 16 ti
+                    if (ti[s] < 0 || k0 + 15 < 16 * ti[s]) continue;
                     acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(i0[kr + 16 * ti[s] + lc], i1[kr + 16 * tj[s] + lc],
                                                                   acc[s], 0, 0, 0);
                 }
             }
-            if (ph == 1 && tid < C) {
+            if (tid < C) {
 #pragma unroll
                 for (int k = 0; k < 16; ++k) ca += i0[k * Cq + tid] * bb[buf * 16 + k];
             }
+            if (more) put(1, buf ^ 1);
             __syncthreads();
         }
         const double s2 = (double)prm.sigma2;
 #pragma unroll
-        for (int s = 0; s < TPW; ++s) {
+        for (int s = 0; s < TP2; ++s) {
             if (ti[s] < 0) continue;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int i = 16 * ti[s] + lr + 4 * r, j = 16 * tj[s] + lc;
-                if (i >= C || j >= C) continue;
-                if (ph == 0) G[(size_t)i * ld + j] = acc[s][r];
-                else if (j <= i) Tm[(size_t)i * ld + j] = acc[s][r] + (i == j ? s2 : 0.0);
+                if (i < C && j <= i) Tm[(size_t)i * ld + j] = acc[s][r] + (i == j ? s2 : 0.0);
             }
         }
-        __syncthreads();   // G visible to the whole workgroup before phase 2 streams it
+        if (tid < C) Tm[(size_t)tid * ld + C] = ca;
     }
-    if (tid < C) Tm[(size_t)tid * ld + C] = ca;
 }
 
 // ---- stage E: P+ = blockdiag(S_ii, 0) + s2 W W^T (lower tiles, mirrored), dx = W y ----
@@ -707,8 +769,8 @@ __global__ void __launch_bounds__(256) k_kal_e(DevState<T> st, Params<T> prm, Up
 // MFMA accumulators.  W streams once through double-buffered LDS in chunks of
 // 16 columns ([k][row] images, so each MFMA operand is one ds_read_b64); the
 // same chunks give dx = W y (thread i < D accumulates row i).
-template <typename T, int TPW>
-__global__ void __launch_bounds__(1024) k_kal_e1(DevState<T> st, Params<T> prm, UpdWs<T> ws) {
+template <typename T, int NW, int TPW>
+__global__ void __launch_bounds__(64 * NW) k_kal_e1(DevState<T> st, Params<T> prm, UpdWs<T> ws) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int b = blockIdx.x;
     if (ws.info[4 * b] == 0 || ws.info[4 * b + 3] < 0) return;
@@ -723,7 +785,7 @@ __global__ void __launch_bounds__(1024) k_kal_e1(DevState<T> st, Params<T> prm, 
     int ti[TPW], tj[TPW];
 #pragma unroll
     for (int s = 0; s < TPW; ++s) {   // row-major lower enumeration of the tile grid
-        const int t = wv + 16 * s;
+        const int t = wv + NW * s;
         int i = (int)((sqrtf(8.0f * (float)t + 1.0f) - 1.0f) * 0.5f);
         while (i * (i + 1) / 2 > t) --i;
         while ((i + 1) * (i + 2) / 2 <= t) ++i;
@@ -733,27 +795,42 @@ __global__ void __launch_bounds__(1024) k_kal_e1(DevState<T> st, Params<T> prm, 
     v4d acc[TPW];
 #pragma unroll
     for (int s = 0; s < TPW; ++s) acc[s] = v4d{0.0, 0.0, 0.0, 0.0};
-    double dxa = 0.0;
-    auto stage = [&](int k0, int buf) {   // W[:, k0:k0+16] -> img[buf][k][row], y chunk
-        double* im = img + buf * 16 * Dp;
-        for (int e = tid; e < 16 * Dp; e += 1024) {
-            const int row = e >> 4, k = e & 15;
-            im[k * Dp + row] = (row < D && k0 + k < C) ? W[(size_t)row * Cpw + k0 + k] : 0.0;
+    double dxa = 0.0, dxb = 0.0;
+    // W[:, k0:k0+16] -> img[buf][k][row] and the y chunk; load() before the
+    // current chunk's MFMAs, put() after them
+    constexpr int NT = 64 * NW, Q = (16 * 16 * (NW * TPW <= 96 ? 13 : 15) + NT - 1) / NT;
+    double rw[Q], ry = 0.0;
+    auto load = [&](int k0) {
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const int e = tid + NT * q, row = e >> 4, k = e & 15;
+            rw[q] = (e < 16 * Dp && row < D && k0 + k < C) ? W[(size_t)row * Cpw + k0 + k] : 0.0;
         }
-        if (tid < 16) yb[buf * 16 + tid] = k0 + tid < C ? W[(size_t)D * Cpw + k0 + tid] : 0.0;
+        if (tid < 16) ry = k0 + tid < C ? W[(size_t)D * Cpw + k0 + tid] : 0.0;
     };
-    stage(0, 0);
+    auto put = [&](int buf) {
+        double* im = img + buf * 16 * Dp;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const int e = tid + NT * q;
+            if (e < 16 * Dp) im[(e & 15) * Dp + (e >> 4)] = rw[q];
+        }
+        if (tid < 16) yb[buf * 16 + tid] = ry;
+    };
+    load(0);
+    put(0);
     __syncthreads();
     for (int k0 = 0, it = 0; k0 < C; k0 += 16, ++it) {
         const int buf = it & 1;
-        if (k0 + 16 < C) stage(k0 + 16, buf ^ 1);
+        const bool more = k0 + 16 < C;
+        if (more) load(k0 + 16);
         const double* im = img + buf * 16 * Dp;
 #pragma unroll
-        for (int s = 0; s < TPW; ++s) {
-            if (ti[s] < 0) continue;
+        for (int kc = 0; kc < 4; ++kc) {
+            const double* kr = im + (4 * kc + lr) * Dp;
 #pragma unroll
-            for (int kc = 0; kc < 4; ++kc) {
-                const double* kr = im + (4 * kc + lr) * Dp;
+            for (int s = 0; s < TPW; ++s) {
+                if (ti[s] < 0) continue;
                 acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(kr[16 * ti[s] + lc], kr[16 * tj[s] + lc], acc[s], 0, 0, 0);
             }
         }
@@ -761,6 +838,11 @@ __global__ void __launch_bounds__(1024) k_kal_e1(DevState<T> st, Params<T> prm, 
 #pragma unroll
             for (int k = 0; k < 16; ++k) dxa += im[k * Dp + tid] * yb[buf * 16 + k];
         }
+        if (NT + tid < D) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) dxb += im[k * Dp + NT + tid] * yb[buf * 16 + k];
+        }
+        if (more) put(buf ^ 1);
         __syncthreads();
     }
     const double s2 = (double)prm.sigma2;
@@ -780,6 +862,7 @@ __global__ void __launch_bounds__(1024) k_kal_e1(DevState<T> st, Params<T> prm, 
         }
     }
     if (tid < D) ws.dx[(size_t)b * (st.Dmax + ws.Cmax) + tid] = dxa;
+    if (NT + tid < D) ws.dx[(size_t)b * (st.Dmax + ws.Cmax) + NT + tid] = dxb;
 }
 
 // ===========================================================================
@@ -859,24 +942,26 @@ static void launch_c16(hipStream_t s, const DevState<T>& st, const UpdWs<T>& ws,
     hipLaunchKernelGGL((k_kal_c16<T, NW, TPW>), dim3(groups, st.B), dim3(64 * NW), lds, s, st, ws, ner, dbg);
 }
 
-template <typename T, int TPW>
+template <typename T, int NW, int TPW>
 static void launch_e1(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const UpdWs<T>& ws, size_t lds) {
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_kal_e1<T, TPW>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)k_kal_e1<T, NW, TPW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
         attr = true;
     }
-    hipLaunchKernelGGL((k_kal_e1<T, TPW>), dim3(st.B), dim3(1024), lds, s, st, prm, ws);
+    hipLaunchKernelGGL((k_kal_e1<T, NW, TPW>), dim3(st.B), dim3(64 * NW), lds, s, st, prm, ws);
 }
 
-template <typename T, int TPW>
+template <typename T, int NW, int WR, int WC, int NTM>
 static void launch_b(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const UpdWs<T>& ws, size_t lds) {
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_kal_b<T, TPW>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)k_kal_b<T, NW, WR, WC, NTM>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
         attr = true;
     }
-    hipLaunchKernelGGL((k_kal_b<T, TPW>), dim3(st.B), dim3(1024), lds, s, st, prm, ws);
+    hipLaunchKernelGGL((k_kal_b<T, NW, WR, WC, NTM>), dim3(st.B), dim3(64 * NW), lds, s, st, prm, ws);
 }
 
 template <typename T>
@@ -912,9 +997,11 @@ void launch_kalman_chol(hipStream_t s, const DevState<T>& st, const Params<T>& p
     const int tiles = (Cmax + GT - 1) / GT;
     kt->begin(s, "kalman_b");
     if (Cq <= 16 * 8) {
-        launch_b<T, 4>(s, st, prm, ws, (4 * 16 * (size_t)Cq + 32) * sizeof(double));
+        launch_b<T, 8, 4, 2, 8>(s, st, prm, ws, (4 * 16 * (size_t)Cq + 32) * sizeof(double));
     } else if (Cq <= 16 * 12) {
-        launch_b<T, 9>(s, st, prm, ws, (4 * 16 * (size_t)Cq + 32) * sizeof(double));
+        static const int bnw = getenv("MSCKF_KB_NW") ? atoi(getenv("MSCKF_KB_NW")) : 16;
+        if (bnw == 16) launch_b<T, 16, 4, 4, 12>(s, st, prm, ws, (4 * 16 * (size_t)Cq + 32) * sizeof(double));
+        else launch_b<T, 8, 4, 2, 12>(s, st, prm, ws, (4 * 16 * (size_t)Cq + 32) * sizeof(double));
     } else {   // large windows: 64 x 64 output tiles, one workgroup each
         hipLaunchKernelGGL(k_kal_b1<T>, dim3(tiles, tiles, st.B), dim3(256), 0, s, st, ws);
         hipLaunchKernelGGL(k_kal_b2<T>, dim3((Cmax + 1 + GT - 1) / GT, tiles, st.B), dim3(256), 0, s, st, prm, ws);
@@ -955,10 +1042,13 @@ void launch_kalman_chol(hipStream_t s, const DevState<T>& st, const Params<T>& p
     kt->begin(s, "kalman_e");
     const int nTe = (st.Dmax + 15) / 16, tilesE = nTe * (nTe + 1) / 2;
     const size_t ldsE = (2 * 16 * 16 * (size_t)nTe + 32) * sizeof(double);
-    if (tilesE <= 16 * 6) {
-        launch_e1<T, 6>(s, st, prm, ws, ldsE);
-    } else if (tilesE <= 16 * 8) {
-        launch_e1<T, 8>(s, st, prm, ws, ldsE);
+    static const int enw = getenv("MSCKF_KE_NW") ? atoi(getenv("MSCKF_KE_NW")) : 16;
+    if (tilesE <= 16 * 6 && enw == 16) {
+        launch_e1<T, 16, 6>(s, st, prm, ws, ldsE);
+    } else if (tilesE <= 8 * 12) {
+        launch_e1<T, 8, 12>(s, st, prm, ws, ldsE);
+    } else if (tilesE <= 8 * 16) {
+        launch_e1<T, 8, 16>(s, st, prm, ws, ldsE);
     } else {   // large windows: one 64 x 64 tile per workgroup
         const int dt = (st.Dmax + GT - 1) / GT, dt1 = (st.Dmax + 1 + GT - 1) / GT;
         hipLaunchKernelGGL(k_kal_e<T>, dim3(dt1, dt, st.B), dim3(256), 0, s, st, prm, ws);
