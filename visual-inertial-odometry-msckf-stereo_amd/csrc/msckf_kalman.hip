@@ -351,6 +351,153 @@ __global__ void __launch_bounds__(NT) k_kal_c(DevState<T> st, UpdWs<T> ws, int n
     if (!ok && threadIdx.x == 0) ws.info[4 * b + 3] = -1;
 }
 
+// ---- stage C, split form (production path when C <= 16 * NTM) ----
+// C1: Cholesky of T alone (4x4 register tiles, one workgroup per filter), L_T
+//     written over the G workspace (free after stage B).
+// C2: W^T = L_T^-1 X^T with X = [Vc_i ; Lc ; c^T] (E = 22 + C rows) as a
+//     blocked forward substitution on MFMA: wave w owns the 16-row tiles
+//     ct = w + NW t of X and keeps the solved blocks Y'[K] (16 x 16, K < nT) in
+//     registers -- in the MFMA result layout (row = lane/16 + 4 r, col =
+//     lane%16) a solved block's r-th value is exactly the B operand of
+//     k-step r, so no block is re-read.  Step J:
+//         Y'[J] = Linv_JJ (X^T[J] - sum_{K<J} L_T[J, K] Y'[K])
+//     with -L_T[J, 0:16J] staged in LDS ([col][row], 17-double rows) and the
+//     16 x 16 inverses of the diagonal blocks formed once up front.  W^T is
+//     stored row-major over k (coalesced), the layout k_kal_e1<WT=true> reads.
+template <typename T, int NT, int TPL>
+__global__ void __launch_bounds__(NT) k_kal_c1(DevState<T> st, UpdWs<T> ws) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    const int b = blockIdx.x;
+    if (ws.info[4 * b] == 0) return;
+    const int C = 6 * st.ncams[b], Cp = round4(C), nTc = Cp / 4;
+    const int ldt = ws.Cmax + 1;
+    const KT* Tm = ws.Tm + (size_t)b * ws.Cmax * ldt;
+    KT* L = ws.G + (size_t)b * ws.Cmax * ldt;
+    auto load = [&](int i, int j) -> double {
+        if (i >= C || j >= C) return i == j ? 1.0 : 0.0;
+        return i >= j ? Tm[(size_t)i * ldt + j] : Tm[(size_t)j * ldt + i];
+    };
+    auto panel = [&](int r, int c0, double w0, double w1, double w2, double w3) {
+        if (r >= C) return;
+        KT* dst = L + (size_t)r * ldt;
+        const double w[4] = {w0, w1, w2, w3};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (c0 + q < C && c0 + q <= r) dst[c0 + q] = w[q];
+    };
+    auto trail = [](int, int, double) {};
+    const bool ok = rchol_core<NT, TPL>(nTc, nTc, nTc, reinterpret_cast<double*>(smem_raw), load, panel, trail);
+    if (!ok && threadIdx.x == 0) ws.info[4 * b + 3] = -1;
+}
+
+constexpr int C2S = 17;   // LDS row stride (doubles) of the staged L_T block row
+
+template <typename T, int NW, int CT, int NTM>
+__global__ void __launch_bounds__(64 * NW) k_kal_c2(DevState<T> st, UpdWs<T> ws) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    constexpr int NT = 64 * NW;
+    const int b = blockIdx.x;
+    if (ws.info[4 * b] == 0 || ws.info[4 * b + 3] < 0) return;
+    const int C = 6 * st.ncams[b], nT = (C + 15) / 16, E = 22 + C, nE = (E + 15) / 16;
+    const int tid = threadIdx.x, lane = tid & 63, lc = lane & 15, lr = lane >> 4;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int ldt = ws.Cmax + 1, Cpw = ws.Cp, ldw = st.Dmax + 1;
+    const KT* L = ws.G + (size_t)b * ws.Cmax * ldt;
+    const KT* Tm = ws.Tm + (size_t)b * ws.Cmax * ldt;
+    const KT* Lc = ws.Lc + (size_t)b * Cpw * Cpw;
+    const KT* Vi = ws.Vi + (size_t)b * KW * Cpw;
+    KT* Wt = ws.W + (size_t)b * (st.Dmax + 1) * Cpw;
+    double* LI = reinterpret_cast<double*>(smem_raw);   // [NTM][k][i] = Linv_JJ[i][k]
+    double* img = LI + NTM * 256;                        // [col][C2S]: -L_T[16J + i][col]
+    auto Lv = [&](int r, int k) -> double {   // L_T with identity padding beyond C
+        if (r >= C || k >= C) return r == k ? 1.0 : 0.0;
+        return k <= r ? L[(size_t)r * ldt + k] : 0.0;
+    };
+    // diagonal block inverses: the block goes to a per-wave LDS scratch (img is
+    // free until the main loop), lane j < 16 solves column j by forward
+    // substitution straight into LI (rolled loops: this runs once per filter)
+    for (int J = wv; J < nT; J += NW) {
+        double* blk = img + wv * 256;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int e = lane + 64 * q, i = e >> 4, k = e & 15;
+            blk[e] = Lv(16 * J + i, 16 * J + k);
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        if (lane < 16) {
+            double* xj = LI + J * 256 + 16 * lane;   // Linv[i][lane] at xj[i]
+#pragma unroll 1
+            for (int i = 0; i < 16; ++i) {
+                double sv = i == lane ? 1.0 : 0.0;
+#pragma unroll 1
+                for (int k = lane; k < i; ++k) sv -= blk[16 * i + k] * xj[k];
+                xj[i] = i < lane ? 0.0 : sv / blk[17 * i];
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    }
+    auto Xv = [&](int e, int j) -> double {   // X[e][j]
+        if (j >= C) return 0.0;
+        if (e < 21) return Vi[(size_t)e * Cpw + j];
+        if (e < 21 + C) return j <= e - 21 ? Lc[(size_t)(e - 21) * Cpw + j] : 0.0;
+        if (e == 21 + C) return Tm[(size_t)j * ldt + C];
+        return 0.0;
+    };
+    v4d yk[CT][NTM];
+#pragma unroll
+    for (int J = 0; J < NTM; ++J) {
+        if (J >= nT) continue;   // uniform; continue (not break) keeps the loop unrollable
+        if (J > 0) {   // stage -L_T[16J : 16J+16, 0 : 16J]
+            const int w = 16 * J;
+            for (int e = tid; e < 16 * w; e += NT) {
+                const int i = e / w, col = e - i * w;
+                img[col * C2S + i] = -Lv(16 * J + i, col);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int t = 0; t < CT; ++t) {
+            const int ct = wv + NW * t;
+            if (ct >= nE) continue;
+            v4d a0, a1 = v4d{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) a0[q] = Xv(16 * ct + lc, 16 * J + lr + 4 * q);
+#pragma unroll
+            for (int K = 0; K < J; ++K) {
+#pragma unroll
+                for (int kc = 0; kc < 4; ++kc) {
+                    const double av = img[(16 * K + 4 * kc + lr) * C2S + lc];
+                    if (K & 1) a1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, yk[t][K][kc], a1, 0, 0, 0);
+                    else a0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, yk[t][K][kc], a0, 0, 0, 0);
+                }
+            }
+            a0 += a1;
+            v4d y = v4d{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int kc = 0; kc < 4; ++kc)
+                y = __builtin_amdgcn_mfma_f64_16x16x4f64(LI[J * 256 + (4 * kc + lr) * 16 + lc], a0[kc], y, 0, 0, 0);
+            yk[t][J] = y;
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int t = 0; t < CT; ++t) {
+        const int ct = wv + NW * t, col = 16 * ct + lc;
+        if (ct >= nE || col >= E) continue;
+#pragma unroll
+        for (int J = 0; J < NTM; ++J) {
+            if (J >= nT) continue;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int k = 16 * J + lr + 4 * q;
+                if (k < C) Wt[(size_t)k * ldw + col] = yk[t][J][q];
+            }
+        }
+    }
+}
+
 // ===========================================================================
 // Global-memory fallback of stages A and C for windows whose tiles do not fit
 // in one workgroup's registers (Nmax > 36): the same partial Cholesky, in place
@@ -769,7 +916,7 @@ __global__ void __launch_bounds__(256) k_kal_e(DevState<T> st, Params<T> prm, Up
 // MFMA accumulators.  W streams once through double-buffered LDS in chunks of
 // 16 columns ([k][row] images, so each MFMA operand is one ds_read_b64); the
 // same chunks give dx = W y (thread i < D accumulates row i).
-template <typename T, int NW, int TPW>
+template <typename T, int NW, int TPW, bool WT>
 __global__ void __launch_bounds__(64 * NW) k_kal_e1(DevState<T> st, Params<T> prm, UpdWs<T> ws) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int b = blockIdx.x;
@@ -800,20 +947,29 @@ __global__ void __launch_bounds__(64 * NW) k_kal_e1(DevState<T> st, Params<T> pr
     // current chunk's MFMAs, put() after them
     constexpr int NT = 64 * NW, Q = (16 * 16 * (NW * TPW <= 96 ? 13 : 15) + NT - 1) / NT;
     double rw[Q], ry = 0.0;
+    // WT: W stored transposed (row-major over k, leading dimension Dmax + 1; stage C2)
+    const int ldw = st.Dmax + 1;
     auto load = [&](int k0) {
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
-            const int e = tid + NT * q, row = e >> 4, k = e & 15;
-            rw[q] = (e < 16 * Dp && row < D && k0 + k < C) ? W[(size_t)row * Cpw + k0 + k] : 0.0;
+            const int e = tid + NT * q;
+            if (WT) {
+                const int k = e / Dp, row = e - k * Dp;
+                rw[q] = (e < 16 * Dp && row < D && k0 + k < C) ? W[(size_t)(k0 + k) * ldw + row] : 0.0;
+            } else {
+                const int row = e >> 4, k = e & 15;
+                rw[q] = (e < 16 * Dp && row < D && k0 + k < C) ? W[(size_t)row * Cpw + k0 + k] : 0.0;
+            }
         }
-        if (tid < 16) ry = k0 + tid < C ? W[(size_t)D * Cpw + k0 + tid] : 0.0;
+        if (tid < 16)
+            ry = k0 + tid < C ? (WT ? W[(size_t)(k0 + tid) * ldw + D] : W[(size_t)D * Cpw + k0 + tid]) : 0.0;
     };
     auto put = [&](int buf) {
         double* im = img + buf * 16 * Dp;
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
             const int e = tid + NT * q;
-            if (e < 16 * Dp) im[(e & 15) * Dp + (e >> 4)] = rw[q];
+            if (e < 16 * Dp) im[WT ? e : (e & 15) * Dp + (e >> 4)] = rw[q];
         }
         if (tid < 16) yb[buf * 16 + tid] = ry;
     };
@@ -943,14 +1099,35 @@ static void launch_c16(hipStream_t s, const DevState<T>& st, const UpdWs<T>& ws,
 }
 
 template <typename T, int NW, int TPW>
-static void launch_e1(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const UpdWs<T>& ws, size_t lds) {
+static void launch_e1(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const UpdWs<T>& ws, size_t lds,
+                      bool wt) {
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_kal_e1<T, NW, TPW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)hipFuncSetAttribute((const void*)k_kal_e1<T, NW, TPW, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        (void)hipFuncSetAttribute((const void*)k_kal_e1<T, NW, TPW, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   160 * 1024);
         attr = true;
     }
-    hipLaunchKernelGGL((k_kal_e1<T, NW, TPW>), dim3(st.B), dim3(64 * NW), lds, s, st, prm, ws);
+    if (wt) hipLaunchKernelGGL((k_kal_e1<T, NW, TPW, true>), dim3(st.B), dim3(64 * NW), lds, s, st, prm, ws);
+    else hipLaunchKernelGGL((k_kal_e1<T, NW, TPW, false>), dim3(st.B), dim3(64 * NW), lds, s, st, prm, ws);
+}
+
+template <typename T, int NT, int TPL>
+static void launch_c1(hipStream_t s, const DevState<T>& st, const UpdWs<T>& ws, size_t lds) {
+    hipLaunchKernelGGL((k_kal_c1<T, NT, TPL>), dim3(st.B), dim3(NT), lds, s, st, ws);
+}
+template <typename T, int NW, int CT, int NTM>
+static void launch_c2(hipStream_t s, const DevState<T>& st, const UpdWs<T>& ws) {
+    constexpr int IMG = 16 * NTM * C2S > NW * 256 ? 16 * NTM * C2S : NW * 256;
+    const size_t lds = (NTM * 256 + IMG) * sizeof(double);
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_kal_c2<T, NW, CT, NTM>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        attr = true;
+    }
+    hipLaunchKernelGGL((k_kal_c2<T, NW, CT, NTM>), dim3(st.B), dim3(64 * NW), lds, s, st, ws);
 }
 
 template <typename T, int NW, int WR, int WC, int NTM>
@@ -1007,9 +1184,23 @@ void launch_kalman_chol(hipStream_t s, const DevState<T>& st, const Params<T>& p
         hipLaunchKernelGGL(k_kal_b2<T>, dim3((Cmax + 1 + GT - 1) / GT, tiles, st.B), dim3(256), 0, s, st, prm, ws);
     }
     kt->end(s);
+    // split stage C (C1 + C2) whenever the register tiles of C1 and C2 fit
+    static const int csplit = getenv("MSCKF_KAL_C_SPLIT") ? atoi(getenv("MSCKF_KAL_C_SPLIT")) : 1;
+    const bool split = csplit && !glob && !mf && Cq <= 16 * 12;
     if (glob) {
         kt->begin(s, "kalman_c");
         hipLaunchKernelGGL(k_kal_gc<T>, dim3(st.B), dim3(256), 0, s, st, ws);
+        kt->end(s);
+    } else if (split) {
+        const int nTc = Cp / 4;
+        RcholCfg c;
+        pick_rchol(nTc * (nTc + 1) / 2, c);
+        const size_t lds = rchol_lds_doubles(nTc) * sizeof(double);
+        kt->begin(s, "kalman_c");
+        if (c.nt == 256) launch_c1<T, 256, 4>(s, st, ws, lds);
+        else launch_c1<T, 512, 4>(s, st, ws, lds);
+        if (Cq <= 16 * 8) launch_c2<T, 7, 2, 8>(s, st, ws);
+        else launch_c2<T, 7, 2, 12>(s, st, ws);
         kt->end(s);
     } else if (mf) {   // stage C, MFMA tiles: T + as many extra-row tiles as fit, the rest in more groups
         const int nTc = Cq / 16, Tt = nTc * (nTc + 1) / 2;
@@ -1044,12 +1235,13 @@ void launch_kalman_chol(hipStream_t s, const DevState<T>& st, const Params<T>& p
     const size_t ldsE = (2 * 16 * 16 * (size_t)nTe + 32) * sizeof(double);
     static const int enw = getenv("MSCKF_KE_NW") ? atoi(getenv("MSCKF_KE_NW")) : 16;
     if (tilesE <= 16 * 6 && enw == 16) {
-        launch_e1<T, 16, 6>(s, st, prm, ws, ldsE);
+        launch_e1<T, 16, 6>(s, st, prm, ws, ldsE, split);
     } else if (tilesE <= 8 * 12) {
-        launch_e1<T, 8, 12>(s, st, prm, ws, ldsE);
+        launch_e1<T, 8, 12>(s, st, prm, ws, ldsE, split);
     } else if (tilesE <= 8 * 16) {
-        launch_e1<T, 8, 16>(s, st, prm, ws, ldsE);
-    } else {   // large windows: one 64 x 64 tile per workgroup
+        launch_e1<T, 8, 16>(s, st, prm, ws, ldsE, split);
+    } else {
+        if (split) { fprintf(stderr, "msckf: split stage C needs k_kal_e1\n"); abort(); }   // large windows: one 64 x 64 tile per workgroup
         const int dt = (st.Dmax + GT - 1) / GT, dt1 = (st.Dmax + 1 + GT - 1) / GT;
         hipLaunchKernelGGL(k_kal_e<T>, dim3(dt1, dt, st.B), dim3(256), 0, s, st, prm, ws);
     }
