@@ -231,6 +231,9 @@ __device__ __forceinline__ float fast_sqrt(float x) { return sqrtf(x); }
 __device__ __forceinline__ double fast_sqrt(double x) { return sqrt(x); }
 __device__ __forceinline__ float fast_rcp(float x) { return 1.0f / x; }
 __device__ __forceinline__ double fast_rcp(double x) { return 1.0 / x; }
+// Pivot reciprocals of the gating LDL^T: v_rcp_f32 (1 ulp) in fp32, IEEE division in fp64.
+__device__ __forceinline__ float pivot_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ double pivot_rcp(double x) { return 1.0 / x; }
 
 // Column-major enumeration of the lower tiles (ti >= tl) of a grid with nrow
 // tile rows: column c holds nrow - c tiles and starts at c nrow - c (c - 1) / 2.

@@ -1252,17 +1252,19 @@ __global__ void __launch_bounds__(256) k_gate_wave(DevState<T> st, Params<T> prm
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         // 2. every lane factors the diagonal tile (uniform): A_d = L_d D L_d^T
+        // (one reciprocal per pivot: l_i0 d0 = A_i0, l_i1 d1 = A_i1 - l_i0 A_10, ...)
         const T* dt = wd + GB * tj;
-        const T d0 = dt[0];
-        const T l10 = dt[4] / d0, l20 = dt[8] / d0, l30 = dt[12] / d0;
-        const T d1 = dt[5] - l10 * l10 * d0;
-        const T l21 = (dt[9] - l20 * l10 * d0) / d1;
-        const T l31 = (dt[13] - l30 * l10 * d0) / d1;
-        const T d2 = dt[10] - l20 * l20 * d0 - l21 * l21 * d1;
-        const T l32 = (dt[14] - l30 * l20 * d0 - l31 * l21 * d1) / d2;
-        const T d3 = dt[15] - l30 * l30 * d0 - l31 * l31 * d1 - l32 * l32 * d2;
+        const T d0 = dt[0], e0 = pivot_rcp(d0);
+        const T l10 = dt[4] * e0, l20 = dt[8] * e0, l30 = dt[12] * e0;
+        const T d1 = dt[5] - l10 * dt[4], e1 = pivot_rcp(d1);
+        const T m21 = dt[9] - l20 * dt[4], m31 = dt[13] - l30 * dt[4];   // l21 d1, l31 d1
+        const T l21 = m21 * e1, l31 = m31 * e1;
+        const T d2 = dt[10] - l20 * dt[8] - l21 * m21, e2 = pivot_rcp(d2);
+        const T m32 = dt[14] - l30 * dt[8] - l31 * m21;                    // l32 d2
+        const T l32 = m32 * e2;
+        const T d3 = dt[15] - l30 * dt[12] - l31 * m31 - l32 * m32;
         if (!(d0 > T(0)) || !(d1 > T(0)) || !(d2 > T(0)) || !(d3 > T(0))) { fail = true; break; }
-        const T e0 = T(1) / d0, e1 = T(1) / d1, e2 = T(1) / d2, e3 = T(1) / d3;
+        const T e3 = pivot_rcp(d3);
         // 3. panel rows below the diagonal tile: W = A L_d^-T; store W D^-1 by
         //    row and W transposed by 4-row block
         for (int q = 4 * tj + 4 + lane; q < 4 * nT; q += 64) {
