@@ -85,7 +85,6 @@ def flops_model(probs, B, accepted, valid, feat_off):
         p = probs[b % len(probs)]
         C = 6 * p.N
         D = 21 + C
-        Cp = (C + 3) // 4 * 4
         M = p.track_lengths().astype(float)
         acc = accepted[feat_off[b]:feat_off[b + 1]].astype(float)
         val = valid[feat_off[b]:feat_off[b + 1]].astype(float)
@@ -95,14 +94,13 @@ def flops_model(probs, B, accepted, valid, feat_off):
         # information assembly: per included feature, every observed cam pair takes G_i^T G_j (3 x 6 x 6)
         tot["compress"] += 2 * float(np.sum(acc * (54.0 * M * (M + 1) + 27 * M)))
         if acc.sum() > 0:
-            N = Cp + 24
-            tot["kalman_a"] += 2 * (N ** 3 - (N - Cp) ** 3) / 6
+            # algorithmic (implementation-independent) counts: partial Cholesky over the
+            # C cam pivots of the (C+21)^2 [P_cc P_ci; P_ic P_ii]; G = A Lc and Lc^T G;
+            # Cholesky of T plus the forward substitution of the E = 22 + C extra rows
+            N = C + 21
+            tot["kalman_a"] += 2 * (N ** 3 - (N - C) ** 3) / 6
             tot["kalman_b"] += 2 * (C ** 3 / 2 + C ** 3 / 6 + C * C / 2)
-            ER = (22 + C + 3) // 4
-            nTc = Cp // 4
-            ner_max = (2048 - nTc * (nTc + 1) // 2) // nTc
-            groups = -(-ER // ner_max)
-            tot["kalman_c"] += 2 * (groups * Cp ** 3 / 6 + (22 + C) * Cp * Cp / 2)
+            tot["kalman_c"] += 2 * (C ** 3 / 6 + (22 + C) * C * C / 2)
             tot["kalman_e"] += 2 * (D * (D + 1) / 2 * C + D * C)
         R = float(np.sum(k * acc))
         n = min(R, C)
