@@ -46,6 +46,7 @@ def parse():
     ap.add_argument("--unique", type=int, default=32, help="distinct synthetic problems tiled over the batch")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-ate", action="store_true", help="skip the ATE replay leg")
     return ap.parse_args()
 
 
@@ -152,6 +153,30 @@ def cpu_baseline(args, probs):
                       "numpy/OpenBLAS 1 thread, oracle/msckf_oracle.py" % (done, args.N, args.F)}
 
 
+def ate_leg():
+    """The metric's second half, "ATE RMSE vs ref": the deterministic replay
+    (msckf_amd.replay) of the 200-frame synthetic stereo+IMU stream through the
+    drop-in MSCKF class (fp64, batch of one), against the reference filter's
+    own trajectory on the same stream (tests/golden/sequence_s1.npz, written by
+    tools/gen_golden.py from the reference) and against the stream's ground
+    truth (SE(3)-aligned)."""
+    import msckf_amd
+    from msckf_amd.replay import FeatureStream, replay
+    from msckf_amd.trajectory import Trajectory, ate
+    g = np.load(os.path.join(ROOT, "tests", "golden", "sequence_s1.npz"), allow_pickle=False)
+    st = FeatureStream.from_synthetic(synth.make_sequence(int(g["n_frames"]), int(g["seed"])))
+    flt = msckf_amd.MSCKF()
+    t0 = time.perf_counter()
+    traj = replay(flt, st)
+    el = time.perf_counter() - t0
+    flt.close()
+    ref = Trajectory(g["rec"][:, 0], g["rec"][:, 5:8])
+    return {"ate_vs_ref_m": ate(traj, ref, align="none"), "ate_vs_gt_m": round(ate(traj, st.gt), 5),
+            "frames": len(traj), "frames_per_s": round(len(traj) / el, 1),
+            "sequence": "synthetic stereo+IMU stream s1 (%d frames, 200 Hz IMU), reference trajectory from "
+                        "tests/golden/sequence_s1.npz; fp64, host loop + one filter per call" % len(traj)}
+
+
 def main():
     args = parse()
     grp = replicas.init("nccl")      # replicas only: RCCL carries the barriers and the max of the timing
@@ -213,6 +238,8 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args, probs)
+    if rank == 0 and not args.no_ate:
+        out["ate"] = ate_leg()
     if rank == 0:
         print(json.dumps(out), flush=True)
     ctx.close()
