@@ -110,6 +110,36 @@ int msckf_update(msckf_ctx_t* ctx, int filter, int nf, const int32_t* obs_off,
  * removes the given cam slots (any order). */
 int msckf_prune(msckf_ctx_t* ctx, int filter, int n, const int32_t* cam_slots);
 
+/* ---- multi-filter forms (batched multi-sequence scheduling, SURVEY 8(f)
+ * item 3): the per-filter calls above applied to a list of distinct filter
+ * slots in ONE launch each.  The single-filter entry points are these with a
+ * list of one.  A feature batch for several filters goes through
+ * msckf_batch_load + msckf_batch_triangulate / msckf_batch_update.
+ *
+ * msckf_propagate_batch: filter filters[w] takes samples
+ *   [sample_off[w], sample_off[w+1]) of dt / gyro (n x 3) / acc (n x 3)
+ *   (batch_imu_processing -> process_model, msckf.py:262-368).
+ * msckf_augment_batch: state_augmentation (msckf.py:385-407) of each listed filter.
+ * msckf_prune_batch: P compaction + cam removal (msckf.py:803-818); filter
+ *   filters[w] drops cam slots cam_slots[slot_off[w] .. slot_off[w+1]).
+ * msckf_get_states_batch: IMU records (nfilt x MSCKF_IMU_LEN) and, if
+ *   cams_out != NULL, cam records (nfilt x n_cam_capacity x MSCKF_CAM_LEN,
+ *   zero past each filter's n_cams) and cam counts -- publish
+ *   (msckf.py:888-908) and find_redundant_cam_states (msckf.py:691-727).
+ * msckf_get_cov_diag_batch: out[w * n + k] = P_w[i0 + k][i0 + k]
+ *   (online_reset, msckf.py:869-871).
+ * msckf_batch_triangulate: Feature.initialize_position (feature.py:167-295)
+ *   of every feature of the loaded batch; results via msckf_batch_results. */
+int msckf_propagate_batch(msckf_ctx_t* ctx, int nfilt, const int32_t* filters, const int32_t* sample_off,
+                          const double* dt, const double* gyro, const double* acc);
+int msckf_augment_batch(msckf_ctx_t* ctx, int nfilt, const int32_t* filters);
+int msckf_prune_batch(msckf_ctx_t* ctx, int nfilt, const int32_t* filters, const int32_t* slot_off,
+                      const int32_t* cam_slots);
+int msckf_get_states_batch(msckf_ctx_t* ctx, int nfilt, const int32_t* filters, double* imu_out,
+                           double* cams_out, int32_t* ncams_out);
+int msckf_get_cov_diag_batch(msckf_ctx_t* ctx, int nfilt, const int32_t* filters, int i0, int n, double* out);
+int msckf_batch_triangulate(msckf_ctx_t* ctx);
+
 /* ---- throughput mode: B independent filters, one launch chain per step ----
  * msckf_batch_load copies features for ALL filter slots to HBM once:
  * feat_off[B+1] splits the nf features over slots.  msckf_batch_update then

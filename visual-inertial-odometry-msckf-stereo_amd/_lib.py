@@ -62,6 +62,12 @@ _SIGS = {
     "msckf_triangulate": (C.c_int, [_P, C.c_int, C.c_int, _I, _I, _D, _D, _U8]),
     "msckf_update": (C.c_int, [_P, C.c_int, C.c_int, _I, _I, _D, _D, _D, C.c_int, _U8, _D, _I]),
     "msckf_prune": (C.c_int, [_P, C.c_int, C.c_int, _I]),
+    "msckf_propagate_batch": (C.c_int, [_P, C.c_int, _I, _I, _D, _D, _D]),
+    "msckf_augment_batch": (C.c_int, [_P, C.c_int, _I]),
+    "msckf_prune_batch": (C.c_int, [_P, C.c_int, _I, _I, _I]),
+    "msckf_get_states_batch": (C.c_int, [_P, C.c_int, _I, _D, _D, _I]),
+    "msckf_get_cov_diag_batch": (C.c_int, [_P, C.c_int, _I, C.c_int, C.c_int, _D]),
+    "msckf_batch_triangulate": (C.c_int, [_P]),
     "msckf_batch_load": (C.c_int, [_P, _I, _I, _I, _D, _D, _D]),
     "msckf_batch_update": (C.c_int, [_P, C.c_int, C.c_int]),
     "msckf_batch_results": (C.c_int, [_P, _U8, _D, _D, _U8, _I]),
@@ -236,6 +242,53 @@ class Context:
         slots = _i32(slots)
         with self.lock:
             self._check(self.lib.msckf_prune(self.h, f, len(slots), _ptr(slots, C.c_int32)))
+
+    # ---- multi-filter forms (one launch for a list of filter slots) ----
+    def propagate_batch(self, filters, sample_off, dt, gyro, acc):
+        filters, sample_off = _i32(filters), _i32(sample_off)
+        n = int(sample_off[-1]) if len(sample_off) else 0
+        dt = _f64(dt).reshape(n)
+        gyro = _f64(gyro, (n, 3))
+        acc = _f64(acc, (n, 3))
+        with self.lock:
+            self._check(self.lib.msckf_propagate_batch(self.h, len(filters), _ptr(filters, C.c_int32),
+                                                       _ptr(sample_off, C.c_int32), _ptr(dt, C.c_double),
+                                                       _ptr(gyro, C.c_double), _ptr(acc, C.c_double)))
+
+    def augment_batch(self, filters):
+        filters = _i32(filters)
+        with self.lock:
+            self._check(self.lib.msckf_augment_batch(self.h, len(filters), _ptr(filters, C.c_int32)))
+
+    def prune_batch(self, filters, slot_off, slots):
+        filters, slot_off, slots = _i32(filters), _i32(slot_off), _i32(slots)
+        with self.lock:
+            self._check(self.lib.msckf_prune_batch(self.h, len(filters), _ptr(filters, C.c_int32),
+                                                   _ptr(slot_off, C.c_int32), _ptr(slots, C.c_int32)))
+
+    def get_states_batch(self, filters, want_cams=True):
+        """(imu records (n, IMU_LEN), list of cam arrays (n_cams_w, CAM_LEN))."""
+        filters = _i32(filters)
+        n = len(filters)
+        imu = np.zeros((n, IMU_LEN))
+        cams = np.zeros((n, self.Nmax, CAM_LEN)) if want_cams else None
+        nc = np.zeros(n, np.int32)
+        with self.lock:
+            self._check(self.lib.msckf_get_states_batch(self.h, n, _ptr(filters, C.c_int32), _ptr(imu, C.c_double),
+                                                        _ptr(cams, C.c_double), _ptr(nc, C.c_int32)))
+        cl = [cams[w, :nc[w]].copy() for w in range(n)] if want_cams else [None] * n
+        return imu, cl
+
+    def cov_diag_batch(self, filters, i0, n):
+        filters = _i32(filters)
+        out = np.zeros((len(filters), n))
+        with self.lock:
+            self._check(self.lib.msckf_get_cov_diag_batch(self.h, len(filters), _ptr(filters, C.c_int32), i0, n,
+                                                           _ptr(out, C.c_double)))
+        return out
+
+    def batch_triangulate(self):
+        self._check(self.lib.msckf_batch_triangulate(self.h))
 
     # ---- throughput mode ----
     def batch_load(self, feat_off, obs_off, obs_cam, obs_z, p_w=None, chi2=None):

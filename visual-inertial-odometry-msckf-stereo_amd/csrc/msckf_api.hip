@@ -482,8 +482,43 @@ int do_get_state(msckf_ctx* c, int f, double* imu, double* cams, double* P, int*
     return 0;
 }
 
+// Per-filter stages over a list of filter slots: one launch for all of them
+// (a single-filter call is a list of one).
+int check_list(msckf_ctx* c, int nfilt, const int32_t* filters) {
+    if (nfilt < 0 || (nfilt > 0 && !filters)) FAIL(-1, "bad filter list");
+    std::vector<char> seen(c->B, 0);
+    for (int i = 0; i < nfilt; ++i) {
+        if (filters[i] < 0 || filters[i] >= c->B) FAIL(-1, "filter slot %d out of range [0,%d)", filters[i], c->B);
+        if (seen[filters[i]]) FAIL(-1, "filter slot %d listed twice", filters[i]);
+        seen[filters[i]] = 1;
+    }
+    return 0;
+}
+
+// uploads int lists to iscratch back to back; returns device pointers
+int upload_ints(msckf_ctx* c, std::initializer_list<const std::vector<int>*> lists, std::vector<const int*>& out) {
+    size_t tot = 0;
+    for (auto* l : lists) tot += l->size();
+    HIPC(c->iscratch.ensure(tot + 1));
+    std::vector<int> flat;
+    flat.reserve(tot);
+    out.clear();
+    for (auto* l : lists) {
+        out.push_back(c->iscratch.p + flat.size());
+        flat.insert(flat.end(), l->begin(), l->end());
+    }
+    if (tot) HIPC(hipMemcpyAsync(c->iscratch.p, flat.data(), tot * sizeof(int), hipMemcpyHostToDevice, c->stream));
+    return 0;
+}
+
 template <typename T>
-int do_propagate(msckf_ctx* c, int f, int n, const double* dt, const double* gyro, const double* acc) {
+int do_propagate_batch(msckf_ctx* c, int nfilt, const int32_t* filters, const int32_t* smp_off, const double* dt,
+                       const double* gyro, const double* acc) {
+    if (nfilt <= 0) return 1;
+    if (smp_off[0] != 0) FAIL(-1, "sample offsets must start at 0");
+    for (int i = 0; i < nfilt; ++i)
+        if (smp_off[i + 1] < smp_off[i]) FAIL(-1, "sample offsets not monotone");
+    const int n = smp_off[nfilt];
     if (n <= 0) return 1;
     std::vector<double> smp((size_t)n * 7);
     for (int k = 0; k < n; ++k) {
@@ -493,10 +528,14 @@ int do_propagate(msckf_ctx* c, int f, int n, const double* dt, const double* gyr
             smp[7 * k + 4 + i] = acc[3 * k + i];
         }
     }
+    std::vector<int> fl(filters, filters + nfilt), off(smp_off, smp_off + nfilt + 1);
+    std::vector<const int*> d;
+    if (int r = upload_ints(c, {&fl, &off}, d)) return r;
     HIPC(c->scratch.ensure(smp.size() * sizeof(T)));
     HIPC(upload<T>(c, c->scratch.p, smp.data(), smp.size()));
     c->timer.begin(c->stream, "propagate");
-    launch_propagate<T>(c->stream, dev_state<T>(c), make_params<T>(c), f, n, reinterpret_cast<T*>(c->scratch.p));
+    launch_propagate<T>(c->stream, dev_state<T>(c), make_params<T>(c), nfilt, d[0], d[1],
+                        reinterpret_cast<T*>(c->scratch.p));
     c->timer.end(c->stream);
     HIPC(hipGetLastError());
     HIPC(hipStreamSynchronize(c->stream));
@@ -505,48 +544,111 @@ int do_propagate(msckf_ctx* c, int f, int n, const double* dt, const double* gyr
 }
 
 template <typename T>
-int do_augment(msckf_ctx* c, int f) {
-    if (c->h_ncams[f] >= c->Nmax) FAIL(-1, "cam-state capacity %d exhausted", c->Nmax);
+int do_augment_batch(msckf_ctx* c, int nfilt, const int32_t* filters) {
+    if (nfilt <= 0) return 1;
+    for (int i = 0; i < nfilt; ++i)
+        if (c->h_ncams[filters[i]] >= c->Nmax)
+            FAIL(-1, "filter %d: cam-state capacity %d exhausted", filters[i], c->Nmax);
+    std::vector<int> fl(filters, filters + nfilt);
+    std::vector<const int*> d;
+    if (int r = upload_ints(c, {&fl}, d)) return r;
     c->timer.begin(c->stream, "augment");
-    launch_augment<T>(c->stream, dev_state<T>(c), f);
+    launch_augment<T>(c->stream, dev_state<T>(c), nfilt, d[0]);
     c->timer.end(c->stream);
     HIPC(hipGetLastError());
     HIPC(hipStreamSynchronize(c->stream));
     c->timer.collect();
-    c->h_ncams[f] += 1;
+    for (int i = 0; i < nfilt; ++i) c->h_ncams[filters[i]] += 1;
     return 0;
 }
 
 template <typename T>
-int do_prune(msckf_ctx* c, int f, int n, const int32_t* slots) {
-    const int nc = c->h_ncams[f];
-    std::vector<char> rm(nc, 0);
-    for (int i = 0; i < n; ++i) {
-        if (slots[i] < 0 || slots[i] >= nc) FAIL(-1, "prune slot %d out of range", slots[i]);
-        rm[slots[i]] = 1;
-    }
-    std::vector<int> keep, keep_cams;
-    for (int i = 0; i < 21; ++i) keep.push_back(i);
-    for (int cam = 0; cam < nc; ++cam)
-        if (!rm[cam]) {
-            keep_cams.push_back(cam);
-            for (int e = 0; e < 6; ++e) keep.push_back(21 + 6 * cam + e);
+int do_prune_batch(msckf_ctx* c, int nfilt, const int32_t* filters, const int32_t* slot_off, const int32_t* slots) {
+    if (nfilt <= 0) return 1;
+    if (slot_off[0] != 0) FAIL(-1, "slot offsets must start at 0");
+    std::vector<int> fl(filters, filters + nfilt), keep, keep_off{0}, kcam, kcam_off{0};
+    std::vector<int> new_n(nfilt);
+    for (int w = 0; w < nfilt; ++w) {
+        const int f = filters[w], nc = c->h_ncams[f];
+        if (slot_off[w + 1] < slot_off[w]) FAIL(-1, "slot offsets not monotone");
+        std::vector<char> rm(nc, 0);
+        for (int i = slot_off[w]; i < slot_off[w + 1]; ++i) {
+            if (slots[i] < 0 || slots[i] >= nc) FAIL(-1, "filter %d: prune slot %d out of range", f, slots[i]);
+            rm[slots[i]] = 1;
         }
-    const int Dn = (int)keep.size();
-    HIPC(c->iscratch.ensure(keep.size() + keep_cams.size() + 1));
-    HIPC(c->scratch.ensure((size_t)Dn * Dn * sizeof(T)));
-    HIPC(hipMemcpy(c->iscratch.p, keep.data(), keep.size() * sizeof(int), hipMemcpyHostToDevice));
-    if (!keep_cams.empty())
-        HIPC(hipMemcpy(c->iscratch.p + keep.size(), keep_cams.data(), keep_cams.size() * sizeof(int),
-                       hipMemcpyHostToDevice));
+        for (int i = 0; i < 21; ++i) keep.push_back(i);
+        int kept = 0;
+        for (int cam = 0; cam < nc; ++cam)
+            if (!rm[cam]) {
+                kcam.push_back(cam);
+                ++kept;
+                for (int e = 0; e < 6; ++e) keep.push_back(21 + 6 * cam + e);
+            }
+        keep_off.push_back((int)keep.size());
+        kcam_off.push_back((int)kcam.size());
+        new_n[w] = kept;
+    }
+    std::vector<const int*> d;
+    if (int r = upload_ints(c, {&fl, &keep_off, &keep, &kcam_off, &kcam}, d)) return r;
     c->timer.begin(c->stream, "prune");
-    launch_prune<T>(c->stream, dev_state<T>(c), f, c->iscratch.p, Dn, reinterpret_cast<T*>(c->scratch.p),
-                    c->iscratch.p + keep.size(), (int)keep_cams.size());
+    launch_prune<T>(c->stream, dev_state<T>(c), nfilt, d[0], d[1], d[2], d[3], d[4]);
     c->timer.end(c->stream);
     HIPC(hipGetLastError());
     HIPC(hipStreamSynchronize(c->stream));
     c->timer.collect();
-    c->h_ncams[f] = (int)keep_cams.size();
+    for (int w = 0; w < nfilt; ++w) c->h_ncams[filters[w]] = new_n[w];
+    return 0;
+}
+
+template <typename T>
+int do_cov_diag_batch(msckf_ctx* c, int nfilt, const int32_t* filters, int i0, int n, double* out) {
+    if (nfilt <= 0 || n <= 0) return 0;
+    for (int w = 0; w < nfilt; ++w)
+        if (i0 < 0 || i0 + n > 21 + 6 * c->h_ncams[filters[w]]) FAIL(-1, "diagonal range out of bounds");
+    std::vector<int> fl(filters, filters + nfilt);
+    std::vector<const int*> d;
+    if (int r = upload_ints(c, {&fl}, d)) return r;
+    HIPC(c->scratch.ensure((size_t)nfilt * n * sizeof(T)));
+    launch_cov_diag<T>(c->stream, dev_state<T>(c), nfilt, d[0], i0, n, reinterpret_cast<T*>(c->scratch.p));
+    HIPC(hipGetLastError());
+    return download<T>(c, out, c->scratch.p, (size_t)nfilt * n) == hipSuccess ? 0 : -2;
+}
+
+// IMU records (and optionally cam records) of the listed filters in one D2H
+// copy of the state arrays.
+template <typename T>
+int do_get_states_batch(msckf_ctx* c, int nfilt, const int32_t* filters, double* imu_out, double* cams_out,
+                        int32_t* ncams_out) {
+    const size_t ts = sizeof(T);
+    std::vector<double> imu_all((size_t)c->B * IMU_STRIDE);
+    HIPC(hipStreamSynchronize(c->stream));
+    HIPC(download<T>(c, imu_all.data(), c->imu.p, imu_all.size()));
+    std::vector<double> cams_all;
+    if (cams_out) {
+        cams_all.resize((size_t)c->B * c->Nmax * CAM_STRIDE);
+        HIPC(download<T>(c, cams_all.data(), c->cams.p, cams_all.size()));
+    }
+    (void)ts;
+    for (int w = 0; w < nfilt; ++w) {
+        const int f = filters[w];
+        if (imu_out)
+            for (int e = 0; e < MSCKF_IMU_LEN; ++e) imu_out[(size_t)w * MSCKF_IMU_LEN + e] = imu_all[(size_t)f * IMU_STRIDE + e];
+        if (cams_out)
+            for (int k = 0; k < c->Nmax; ++k)
+                for (int e = 0; e < MSCKF_CAM_LEN; ++e)
+                    cams_out[((size_t)w * c->Nmax + k) * MSCKF_CAM_LEN + e] =
+                        k < c->h_ncams[f] ? cams_all[((size_t)f * c->Nmax + k) * CAM_STRIDE + e] : 0.0;
+        if (ncams_out) ncams_out[w] = c->h_ncams[f];
+    }
+    return 0;
+}
+
+template <typename T>
+int run_triangulate_only(msckf_ctx* c) {
+    c->timer.begin(c->stream, "triangulate");
+    launch_triangulate<T>(c->stream, dev_state<T>(c), make_params<T>(c), feat_batch<T>(c));
+    c->timer.end(c->stream);
+    HIPC(hipGetLastError());
     return 0;
 }
 
@@ -659,32 +761,35 @@ int msckf_get_state(msckf_ctx_t* c, int filter, double* imu, double* cams, doubl
 
 int msckf_get_cov_diag(msckf_ctx_t* c, int filter, int i0, int n, double* out) {
     if (int r = check_ctx(c, filter)) return r;
-    const int D = 21 + 6 * c->h_ncams[filter];
-    if (i0 < 0 || n < 0 || i0 + n > D) FAIL(-1, "diagonal range out of bounds");
-    HIPC(hipStreamSynchronize(c->stream));
-    const size_t ts = c->scalar;
-    for (int i = 0; i < n; ++i) {
-        size_t off = ((size_t)filter * c->Dmax * c->Dmax + (size_t)(i0 + i) * c->Dmax + (i0 + i)) * ts;
-        if (ts == 4) {
-            float v;
-            HIPC(hipMemcpy(&v, c->P.p + off, 4, hipMemcpyDeviceToHost));
-            out[i] = v;
-        } else {
-            HIPC(hipMemcpy(&out[i], c->P.p + off, 8, hipMemcpyDeviceToHost));
-        }
-    }
-    return 0;
+    if (n > 0 && !out) FAIL(-1, "null output");
+    return DISPATCH(c, do_cov_diag_batch, c, 1, &filter, i0, n, out);
 }
 
 int msckf_propagate(msckf_ctx_t* c, int filter, int n, const double* dt, const double* gyro, const double* acc) {
     if (int r = check_ctx(c, filter)) return r;
     if (n > 0 && (!dt || !gyro || !acc)) FAIL(-1, "null sample array");
-    return DISPATCH(c, do_propagate, c, filter, n, dt, gyro, acc);
+    const int32_t off[2] = {0, n > 0 ? n : 0};
+    return DISPATCH(c, do_propagate_batch, c, 1, &filter, off, dt, gyro, acc);
+}
+
+int msckf_propagate_batch(msckf_ctx_t* c, int nfilt, const int32_t* filters, const int32_t* sample_off,
+                          const double* dt, const double* gyro, const double* acc) {
+    if (!c) FAIL(-1, "null context");
+    if (int r = check_list(c, nfilt, filters)) return r;
+    if (nfilt > 0 && !sample_off) FAIL(-1, "null sample offsets");
+    if (nfilt > 0 && sample_off[nfilt] > 0 && (!dt || !gyro || !acc)) FAIL(-1, "null sample array");
+    return DISPATCH(c, do_propagate_batch, c, nfilt, filters, sample_off, dt, gyro, acc);
 }
 
 int msckf_augment(msckf_ctx_t* c, int filter) {
     if (int r = check_ctx(c, filter)) return r;
-    return DISPATCH(c, do_augment, c, filter);
+    return DISPATCH(c, do_augment_batch, c, 1, &filter);
+}
+
+int msckf_augment_batch(msckf_ctx_t* c, int nfilt, const int32_t* filters) {
+    if (!c) FAIL(-1, "null context");
+    if (int r = check_list(c, nfilt, filters)) return r;
+    return DISPATCH(c, do_augment_batch, c, nfilt, filters);
 }
 
 int msckf_triangulate(msckf_ctx_t* c, int filter, int nf, const int32_t* obs_off, const int32_t* obs_cam,
@@ -706,7 +811,37 @@ int msckf_update(msckf_ctx_t* c, int filter, int nf, const int32_t* obs_off, con
 int msckf_prune(msckf_ctx_t* c, int filter, int n, const int32_t* cam_slots) {
     if (int r = check_ctx(c, filter)) return r;
     if (n <= 0) return 1;
-    return DISPATCH(c, do_prune, c, filter, n, cam_slots);
+    if (!cam_slots) FAIL(-1, "null slot list");
+    const int32_t off[2] = {0, n};
+    return DISPATCH(c, do_prune_batch, c, 1, &filter, off, cam_slots);
+}
+
+int msckf_prune_batch(msckf_ctx_t* c, int nfilt, const int32_t* filters, const int32_t* slot_off,
+                      const int32_t* cam_slots) {
+    if (!c) FAIL(-1, "null context");
+    if (int r = check_list(c, nfilt, filters)) return r;
+    if (nfilt > 0 && !slot_off) FAIL(-1, "null slot offsets");
+    if (nfilt > 0 && slot_off[nfilt] > 0 && !cam_slots) FAIL(-1, "null slot list");
+    return DISPATCH(c, do_prune_batch, c, nfilt, filters, slot_off, cam_slots);
+}
+
+int msckf_get_states_batch(msckf_ctx_t* c, int nfilt, const int32_t* filters, double* imu_out, double* cams_out,
+                           int32_t* ncams_out) {
+    if (!c) FAIL(-1, "null context");
+    if (int r = check_list(c, nfilt, filters)) return r;
+    return DISPATCH(c, do_get_states_batch, c, nfilt, filters, imu_out, cams_out, ncams_out);
+}
+
+int msckf_get_cov_diag_batch(msckf_ctx_t* c, int nfilt, const int32_t* filters, int i0, int n, double* out) {
+    if (!c) FAIL(-1, "null context");
+    if (int r = check_list(c, nfilt, filters)) return r;
+    if (nfilt > 0 && n > 0 && !out) FAIL(-1, "null output");
+    return DISPATCH(c, do_cov_diag_batch, c, nfilt, filters, i0, n, out);
+}
+
+int msckf_batch_triangulate(msckf_ctx_t* c) {
+    if (!c) FAIL(-1, "null context");
+    return DISPATCH(c, run_triangulate_only, c);
 }
 
 int msckf_batch_load(msckf_ctx_t* c, const int32_t* feat_off, const int32_t* obs_off, const int32_t* obs_cam,

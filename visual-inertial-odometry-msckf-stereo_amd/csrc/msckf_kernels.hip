@@ -26,8 +26,9 @@
 namespace msckf {
 
 // ===========================================================================
-// IMU propagation: one 256-thread workgroup per filter, the n samples of the
-// frame applied in order.  The 21x21 recursion lives in LDS; the IMU x cam
+// IMU propagation: one 256-thread workgroup per listed filter (batched over
+// filters: workgroup w propagates filters[w] with samples
+// [smp_off[w], smp_off[w+1])), the samples of the frame applied in order.  The 21x21 recursion lives in LDS; the IMU x cam
 // cross block is updated once with the product Phi_n...Phi_1 (the per-sample
 // full-P symmetrisation of msckf.py:362-363 is a no-op on the cam x cam
 // block and only re-rounds the cross block).
@@ -43,14 +44,19 @@ __device__ void mm21(const T* A, const T* B, T* C, int tid) {   // C = A B (21x2
 }
 
 template <typename T>
-__global__ void __launch_bounds__(256) k_propagate(DevState<T> st, Params<T> prm, int filter,
-                                                   int n, const T* __restrict__ samples) {
+__global__ void __launch_bounds__(256) k_propagate(DevState<T> st, Params<T> prm,
+                                                   const int* __restrict__ filters,
+                                                   const int* __restrict__ smp_off,
+                                                   const T* __restrict__ samples_all) {
     __shared__ T F[441], Phi[441], Fdt2[441], Fdt3[441], A[441], Bm[441], P11[441], PhiT[441];
     __shared__ T G[21 * 12], PG[21 * 12];
     __shared__ T s_R[9], s_gyro[3], s_acc[3], s_dt;
     __shared__ T s_imu[IMU_STRIDE];
     const int tid = threadIdx.x;
-    const int b = filter;
+    const int b = filters[blockIdx.x];
+    const int n = smp_off[blockIdx.x + 1] - smp_off[blockIdx.x];
+    const T* samples = samples_all + 7 * (size_t)smp_off[blockIdx.x];
+    if (n <= 0) return;
     T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
     const int ld = st.Dmax;
     T* imu = st.imu + (size_t)b * IMU_STRIDE;
@@ -302,14 +308,14 @@ __global__ void __launch_bounds__(256) k_propagate(DevState<T> st, Params<T> prm
 }
 
 // ===========================================================================
-// State augmentation: one workgroup per filter.
+// State augmentation: one workgroup per listed filter.
 // ===========================================================================
 template <typename T>
-__global__ void __launch_bounds__(256) k_augment(DevState<T> st, int filter) {
+__global__ void __launch_bounds__(256) k_augment(DevState<T> st, const int* __restrict__ filters) {
     __shared__ T J[6 * 21];
     __shared__ T X[36];
     const int tid = threadIdx.x;
-    const int b = filter;
+    const int b = filters[blockIdx.x];
     T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
     const int ld = st.Dmax;
     const T* imu = st.imu + (size_t)b * IMU_STRIDE;
@@ -365,35 +371,60 @@ __global__ void __launch_bounds__(256) k_augment(DevState<T> st, int filter) {
 }
 
 // ===========================================================================
-// P compaction (msckf.py:803-818): gather kept rows/cols into scratch, copy back.
+// P compaction (msckf.py:803-818), in place: one workgroup per listed filter.
+// P'[i][j] = P[keep[i]][keep[j]] with keep ascending, so keep[i] >= i: rows
+// are moved in chunks of R through LDS, every read of a chunk before any of
+// its writes -- a later chunk only reads rows keep[i'] >= i' that no earlier
+// chunk has written.  keep_off / kcam_off delimit each filter's kept indices
+// (error-state rows; cam slots) in the concatenated lists.
 // ===========================================================================
 template <typename T>
-__global__ void k_prune_gather(DevState<T> st, int filter, const int* __restrict__ keep, int Dn,
-                               T* __restrict__ scratch) {
-    const T* P = st.P + (size_t)filter * st.Dmax * st.Dmax;
-    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < Dn * Dn; e += gridDim.x * blockDim.x) {
-        int i = e / Dn, j = e % Dn;
-        scratch[e] = P[(size_t)keep[i] * st.Dmax + keep[j]];
+__global__ void __launch_bounds__(256) k_prune(DevState<T> st, const int* __restrict__ filters,
+                                               const int* __restrict__ keep_off, const int* __restrict__ keep_all,
+                                               const int* __restrict__ kcam_off,
+                                               const int* __restrict__ keep_cams_all, int R) {
+    extern __shared__ unsigned char prune_lds[];
+    T* buf = reinterpret_cast<T*>(prune_lds);          // [R][Dn]
+    const int b = filters[blockIdx.x];
+    const int* keep = keep_all + keep_off[blockIdx.x];
+    const int Dn = keep_off[blockIdx.x + 1] - keep_off[blockIdx.x];
+    T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
+    const int ld = st.Dmax;
+    for (int i0 = 0; i0 < Dn; i0 += R) {
+        const int nr = min(R, Dn - i0);
+        for (int e = threadIdx.x; e < nr * Dn; e += blockDim.x) {
+            const int r = e / Dn, j = e - r * Dn;
+            buf[e] = P[(size_t)keep[i0 + r] * ld + keep[j]];
+        }
+        __syncthreads();
+        for (int e = threadIdx.x; e < nr * Dn; e += blockDim.x) {
+            const int r = e / Dn, j = e - r * Dn;
+            P[(size_t)(i0 + r) * ld + j] = buf[e];
+        }
+        __syncthreads();
     }
-}
-
-template <typename T>
-__global__ void k_prune_scatter(DevState<T> st, int filter, int Dn, const T* __restrict__ scratch,
-                                const int* __restrict__ keep_cams, int nkeep) {
-    T* P = st.P + (size_t)filter * st.Dmax * st.Dmax;
-    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < Dn * Dn; e += gridDim.x * blockDim.x) {
-        int i = e / Dn, j = e % Dn;
-        P[(size_t)i * st.Dmax + j] = scratch[e];
-    }
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        T* cams = st.cams + (size_t)filter * st.Nmax * CAM_STRIDE;
+    if (threadIdx.x == 0) {
+        const int* keep_cams = keep_cams_all + kcam_off[blockIdx.x];
+        const int nkeep = kcam_off[blockIdx.x + 1] - kcam_off[blockIdx.x];
+        T* cams = st.cams + (size_t)b * st.Nmax * CAM_STRIDE;
         for (int c = 0; c < nkeep; ++c) {   // keep_cams ascending, in-place forward copy
-            int src = keep_cams[c];
+            const int src = keep_cams[c];
             if (src != c)
                 for (int e = 0; e < CAM_STRIDE; ++e) cams[c * CAM_STRIDE + e] = cams[src * CAM_STRIDE + e];
         }
-        st.ncams[filter] = nkeep;
+        st.ncams[b] = nkeep;
     }
+}
+
+// Covariance diagonal entries [i0, i0 + n) of the listed filters (online
+// reset, msckf.py:869-871), out[w * n + k].
+template <typename T>
+__global__ void k_cov_diag(DevState<T> st, const int* __restrict__ filters, int nfilt, int i0, int n,
+                           T* __restrict__ out) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= nfilt * n) return;
+    const int w = e / n, k = i0 + e % n;
+    out[e] = st.P[(size_t)filters[w] * st.Dmax * st.Dmax + (size_t)k * st.Dmax + k];
 }
 
 // ===========================================================================
@@ -1976,21 +2007,31 @@ __global__ void __launch_bounds__(64) k_correct(DevState<T> st, UpdWs<T> ws) {
 // Host launchers
 // ===========================================================================
 template <typename T>
-void launch_propagate(hipStream_t s, const DevState<T>& st, const Params<T>& prm, int filter, int n,
-                      const T* samples) {
-    hipLaunchKernelGGL(k_propagate<T>, dim3(1), dim3(256), 0, s, st, prm, filter, n, samples);
+void launch_propagate(hipStream_t s, const DevState<T>& st, const Params<T>& prm, int nfilt, const int* filters,
+                      const int* smp_off, const T* samples) {
+    if (nfilt <= 0) return;
+    hipLaunchKernelGGL(k_propagate<T>, dim3(nfilt), dim3(256), 0, s, st, prm, filters, smp_off, samples);
 }
 template <typename T>
-void launch_augment(hipStream_t s, const DevState<T>& st, int filter) {
-    hipLaunchKernelGGL(k_augment<T>, dim3(1), dim3(256), 0, s, st, filter);
+void launch_augment(hipStream_t s, const DevState<T>& st, int nfilt, const int* filters) {
+    if (nfilt <= 0) return;
+    hipLaunchKernelGGL(k_augment<T>, dim3(nfilt), dim3(256), 0, s, st, filters);
 }
 template <typename T>
-void launch_prune(hipStream_t s, const DevState<T>& st, int filter, const int* keep, int Dn, T* scratch,
-                  const int* keep_cams, int nkeep) {
-    int nb = (Dn * Dn + 255) / 256;
-    nb = nb < 1024 ? nb : 1024;
-    hipLaunchKernelGGL(k_prune_gather<T>, dim3(nb), dim3(256), 0, s, st, filter, keep, Dn, scratch);
-    hipLaunchKernelGGL(k_prune_scatter<T>, dim3(nb), dim3(256), 0, s, st, filter, Dn, scratch, keep_cams, nkeep);
+void launch_prune(hipStream_t s, const DevState<T>& st, int nfilt, const int* filters, const int* keep_off,
+                  const int* keep, const int* kcam_off, const int* keep_cams) {
+    if (nfilt <= 0) return;
+    const int row = st.Dmax * (int)sizeof(T);
+    int R = (48 * 1024) / row;
+    R = R < 1 ? 1 : (R > 32 ? 32 : R);
+    hipLaunchKernelGGL(k_prune<T>, dim3(nfilt), dim3(256), (size_t)R * row, s, st, filters, keep_off, keep,
+                       kcam_off, keep_cams, R);
+}
+template <typename T>
+void launch_cov_diag(hipStream_t s, const DevState<T>& st, int nfilt, const int* filters, int i0, int n, T* out) {
+    if (nfilt <= 0 || n <= 0) return;
+    hipLaunchKernelGGL(k_cov_diag<T>, dim3((nfilt * n + 255) / 256), dim3(256), 0, s, st, filters, nfilt, i0, n,
+                       out);
 }
 template <typename T>
 void launch_triangulate(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const FeatBatch<T>& fb) {
@@ -2209,9 +2250,12 @@ void launch_kalman(hipStream_t s, const DevState<T>& st, const Params<T>& prm, c
 }
 
 #define INSTANTIATE(T)                                                                                    \
-    template void launch_propagate<T>(hipStream_t, const DevState<T>&, const Params<T>&, int, int, const T*); \
-    template void launch_augment<T>(hipStream_t, const DevState<T>&, int);                               \
-    template void launch_prune<T>(hipStream_t, const DevState<T>&, int, const int*, int, T*, const int*, int); \
+    template void launch_propagate<T>(hipStream_t, const DevState<T>&, const Params<T>&, int, const int*,     \
+                                      const int*, const T*);                                               \
+    template void launch_augment<T>(hipStream_t, const DevState<T>&, int, const int*);                     \
+    template void launch_prune<T>(hipStream_t, const DevState<T>&, int, const int*, const int*, const int*,  \
+                                  const int*, const int*);                                                 \
+    template void launch_cov_diag<T>(hipStream_t, const DevState<T>&, int, const int*, int, int, T*);      \
     template void launch_triangulate<T>(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&); \
     template void launch_feature<T>(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&, const SegClasses&); \
     template void launch_gate<T>(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&, const GateClasses&); \

@@ -59,13 +59,18 @@ struct KernelTimer {
     }
 };
 
+// Per-filter stages batched over a device list of filter slots (one
+// workgroup per listed filter).
 template <typename T>
-void launch_propagate(hipStream_t, const DevState<T>&, const Params<T>&, int filter, int n, const T* samples);
+void launch_propagate(hipStream_t, const DevState<T>&, const Params<T>&, int nfilt, const int* filters,
+                      const int* smp_off, const T* samples);
 template <typename T>
-void launch_augment(hipStream_t, const DevState<T>&, int filter);
+void launch_augment(hipStream_t, const DevState<T>&, int nfilt, const int* filters);
 template <typename T>
-void launch_prune(hipStream_t, const DevState<T>&, int filter, const int* keep, int Dn, T* scratch,
-                  const int* keep_cams, int nkeep);
+void launch_prune(hipStream_t, const DevState<T>&, int nfilt, const int* filters, const int* keep_off,
+                  const int* keep, const int* kcam_off, const int* keep_cams);
+template <typename T>
+void launch_cov_diag(hipStream_t, const DevState<T>&, int nfilt, const int* filters, int i0, int n, T* out);
 template <typename T>
 void launch_triangulate(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&);
 // Per-feature kernels packed S lanes per feature: features listed by class

@@ -14,6 +14,12 @@ nullspace projection, gating, stacking, compression of the stacked rows
 (information assembly), the Kalman update and covariance compaction.  There is
 no CPU fallback.
 
+Every device interaction of a frame is expressed as a request yielded by a
+step generator (``_frame_steps``); ``feature_callback`` serves the requests
+one by one on this filter's slot, while ``scheduler.MultiMSCKF`` advances many
+filters' generators in lock step and serves each kind of request for all of
+them with one batched launch.  Both paths run the same host logic.
+
 Differences from the reference that are deliberate:
 * the reference's IMU-buffer race between the IMU and vio threads
   (msckf.py:173 vs 287) is removed -- every call holds the context lock;
@@ -48,14 +54,17 @@ class Feature:
 class MSCKF:
     ROW_CAP = 1500   # msckf.py:678
 
-    def __init__(self, config=None, dtype=np.float64, device=0, cam_capacity=None):
+    def __init__(self, config=None, dtype=np.float64, device=0, cam_capacity=None, ctx=None, slot=0):
         if config is None:
             config = FilterConfig()
         elif not isinstance(config, FilterConfig):
             config = FilterConfig.from_reference(config)
         self.config = config
         cap = cam_capacity or (config.max_cam_state_size + 2)
-        self.ctx = _lib.Context(config, n_filters=1, n_cam_capacity=cap, dtype=dtype, device=device)
+        self._own_ctx = ctx is None
+        self.ctx = ctx if ctx is not None else _lib.Context(config, n_filters=1, n_cam_capacity=cap, dtype=dtype,
+                                                            device=device)
+        self.slot = slot
         self._lock = threading.RLock()
         self.imu_msg_buffer = []
         self.map_server: "OrderedDict[int, Feature]" = OrderedDict()
@@ -75,7 +84,7 @@ class MSCKF:
                             q_null=[0, 0, 0, 1], p_null=np.zeros(3), v_null=np.zeros(3),
                             R_imu_cam0=T_cam0_imu[:3, :3].T, t_cam0_imu=T_cam0_imu[:3, 3],
                             gravity=config.gravity, alias=False)
-        self.ctx.set_state(0, imu, None, self._initial_cov())
+        self.ctx.set_state(self.slot, imu, None, self._initial_cov())
 
     # ------------------------------------------------------------ helpers --
     def _initial_cov(self):
@@ -90,17 +99,51 @@ class MSCKF:
         return P
 
     def imu_state(self):
-        imu, _, _ = self.ctx.get_state(0, want_P=False)
+        imu, _, _ = self.ctx.get_state(self.slot, want_P=False)
         return _lib.unpack_imu(imu)
 
     def cam_states(self):
         """OrderedDict cam id -> dict(q, p, q_null) in slot order."""
-        _, cams, _ = self.ctx.get_state(0, want_P=False)
+        _, cams, _ = self.ctx.get_state(self.slot, want_P=False)
+        return self._cam_dict(cams)
+
+    def _cam_dict(self, cams):
         return OrderedDict((cid, dict(q=cams[i, 0:4], p=cams[i, 4:7], q_null=cams[i, 7:11]))
                            for i, cid in enumerate(self.cam_ids))
 
     def state_cov(self):
-        return self.ctx.get_state(0, want_P=True)[2]
+        return self.ctx.get_state(self.slot, want_P=True)[2]
+
+    # ------------------------------------------------- device request server --
+    def _serve(self, req):
+        """Executes one request of the step generators on this filter's slot."""
+        kind, f, ctx = req[0], self.slot, self.ctx
+        if kind == "propagate":
+            return ctx.propagate(f, req[1], req[2], req[3])
+        if kind == "augment":
+            return ctx.augment(f)
+        if kind == "triangulate":
+            return ctx.triangulate(f, req[1], req[2], req[3])
+        if kind == "update":
+            return ctx.update(f, *req[1:])
+        if kind == "states":
+            imu, cams, _ = ctx.get_state(f, want_P=False)
+            return imu, cams
+        if kind == "prune":
+            return ctx.prune(f, req[1])
+        if kind == "cov_diag":
+            return ctx.cov_diag(f, req[1], req[2])
+        if kind == "set_state":
+            return ctx.set_state(f, req[1], req[2], req[3])
+        raise ValueError("unknown request %r" % (kind,))
+
+    def _drive(self, gen):
+        try:
+            req = next(gen)
+            while True:
+                req = gen.send(self._serve(req))
+        except StopIteration as e:
+            return e.value
 
     # ----------------------------------------------------------- callbacks --
     def imu_callback(self, imu_msg):
@@ -108,7 +151,7 @@ class MSCKF:
         with self._lock:
             self.imu_msg_buffer.append(imu_msg)
             if not self.is_gravity_set and len(self.imu_msg_buffer) >= 200:
-                self._initialize_gravity_and_bias()
+                self._drive(self._initialize_gravity_and_bias())
                 self.is_gravity_set = True
 
     def _initialize_gravity_and_bias(self):
@@ -121,30 +164,36 @@ class MSCKF:
         bg = sw / len(self.imu_msg_buffer)
         g_imu = sa / len(self.imu_msg_buffer)
         g = np.array([0.0, 0.0, -np.linalg.norm(g_imu)])
-        imu, _, _ = self.ctx.get_state(0, want_P=False)
+        imu, _ = yield ("states",)
+        imu = imu.copy()
         imu[_lib.I_BG:_lib.I_BG + 3] = bg
         imu[_lib.I_G:_lib.I_G + 3] = g
         imu[_lib.I_Q:_lib.I_Q + 4] = from_two_vectors(-g, g_imu)
-        self.ctx.set_state(0, imu, None, self._initial_cov() if not self.cam_ids else None)
+        yield ("set_state", imu, None, self._initial_cov() if not self.cam_ids else None)
 
     def feature_callback(self, feature_msg):
         """msckf.py:180-233"""
         with self._lock:
-            if not self.is_gravity_set:
-                return None
-            if self.is_first_img:
-                self.is_first_img = False
-                self.imu_timestamp = feature_msg.timestamp
-            self._batch_imu_processing(feature_msg.timestamp)
-            self._state_augmentation()
-            self._add_feature_observations(feature_msg)
-            self._remove_lost_features()
-            self._prune_cam_state_buffer()
-            try:
-                return self.publish(feature_msg.timestamp)
-            finally:
-                self._n_published += 1
-                self._online_reset()
+            return self._drive(self._frame_steps(feature_msg))
+
+    def _frame_steps(self, feature_msg):
+        """The body of feature_callback as a request generator; returns the
+        vio_result (or None before gravity initialisation)."""
+        if not self.is_gravity_set:
+            return None
+        if self.is_first_img:
+            self.is_first_img = False
+            self.imu_timestamp = feature_msg.timestamp
+        yield from self._batch_imu_processing(feature_msg.timestamp)
+        yield from self._state_augmentation()
+        self._add_feature_observations(feature_msg)
+        yield from self._remove_lost_features()
+        yield from self._prune_cam_state_buffer()
+        imu, _ = yield ("states",)
+        res = self._publish_from(feature_msg.timestamp, _lib.unpack_imu(imu))
+        self._n_published += 1
+        yield from self._online_reset()
+        return res
 
     # ---------------------------------------------------------- propagation --
     def _batch_imu_processing(self, time_bound):
@@ -165,7 +214,7 @@ class MSCKF:
             used += 1
             t_state = t
         if dts:
-            self.ctx.propagate(0, np.array(dts), np.array(ws), np.array(accs))
+            yield ("propagate", np.array(dts), np.array(ws).reshape(-1, 3), np.array(accs).reshape(-1, 3))
         self.imu_timestamp = t_state
         self.imu_id = self._next_id
         self._next_id += 1
@@ -173,7 +222,7 @@ class MSCKF:
 
     def _state_augmentation(self):
         """msckf.py:385-407"""
-        self.ctx.augment(0)
+        yield ("augment",)
         self.cam_ids.append(self.imu_id)
 
     def _add_feature_observations(self, feature_msg):
@@ -212,7 +261,7 @@ class MSCKF:
         if not feats:
             return
         off, cams, zs = self._pack(feats, [list(f.observations.keys()) for f in feats])
-        p, ok = self.ctx.triangulate(0, off, cams, zs)
+        p, ok = yield ("triangulate", off, cams, zs)
         for f, pi, oki in zip(feats, p, ok):
             f.position = pi
             f.is_initialized = bool(oki)
@@ -225,7 +274,7 @@ class MSCKF:
         off, cams, zs = self._pack(feats, cam_lists)
         chi2 = np.array([chi2_threshold(d) for d in dofs])
         pw = np.array([f.position for f in feats])
-        acc, gam, rows = self.ctx.update(0, off, cams, zs, pw, chi2, row_cap)
+        acc, gam, rows = yield ("update", off, cams, zs, pw, chi2, row_cap)
         # reproduce the reference's decision log: features after the row-cap
         # break are never gated (msckf.py:678-679)
         count = 0
@@ -257,7 +306,7 @@ class MSCKF:
         # other, so they are batched into one launch.
         if self.config.optimization.translation_threshold >= 0:
             raise NotImplementedError("check_motion with a positive translation threshold")
-        self._triangulate([f for f in candidates if not f.is_initialized])
+        yield from self._triangulate([f for f in candidates if not f.is_initialized])
         processed = []
         for feat in candidates:
             if not feat.is_initialized:
@@ -270,13 +319,13 @@ class MSCKF:
             return
         cam_lists = [list(f.observations.keys()) for f in processed]
         dofs = [len(cl) - 1 for cl in cam_lists]
-        self._update(processed, cam_lists, dofs, self.ROW_CAP)
+        yield from self._update(processed, cam_lists, dofs, self.ROW_CAP)
         for feat in processed:
             del self.map_server[feat.id]
 
-    def _find_redundant_cam_states(self):
+    def _find_redundant_cam_states(self, cams_arr):
         """msckf.py:691-727 (host; needs the cam poses)."""
-        cams = list(self.cam_states().items())
+        cams = list(self._cam_dict(cams_arr).items())
         key = len(cams) - 4
         ci = key + 1
         first = 0
@@ -301,7 +350,8 @@ class MSCKF:
         """msckf.py:730-818"""
         if len(self.cam_ids) < self.config.max_cam_state_size:
             return
-        rm = self._find_redundant_cam_states()
+        _, cams_arr = yield ("states",)
+        rm = self._find_redundant_cam_states(cams_arr)
         to_init = []
         for feat in self.map_server.values():
             inv = [c for c in rm if c in feat.observations]
@@ -312,7 +362,7 @@ class MSCKF:
                 continue
             if not feat.is_initialized:
                 to_init.append(feat)
-        self._triangulate(to_init)
+        yield from self._triangulate(to_init)
         for feat in to_init:
             if not feat.is_initialized:
                 for c in rm:
@@ -326,21 +376,23 @@ class MSCKF:
             feats.append(feat)
             cam_lists.append(inv)
         if feats:
-            self._update(feats, cam_lists, [len(cl) for cl in cam_lists], 0)
+            yield from self._update(feats, cam_lists, [len(cl) for cl in cam_lists], 0)
         else:   # the reference still calls measurement_update with an empty H
             self.shape_log.append((self._n_published, 0, 21 + 6 * len(self.cam_ids)))
         for feat, cl in zip(feats, cam_lists):
             for c in cl:
                 del feat.observations[c]
         slots = [self.cam_ids.index(c) for c in rm]
-        self.ctx.prune(0, slots)
+        yield ("prune", np.array(slots, np.int32))
         for c in rm:
             self.cam_ids.remove(c)
 
     # ------------------------------------------------------ output / reset --
     def publish(self, time):
         """msckf.py:888-908"""
-        s = self.imu_state()
+        return self._publish_from(time, self.imu_state())
+
+    def _publish_from(self, time, s):
         T_i_w = Isometry3d(to_rotation(s["q"]).T, s["p"])
         Tb = self._T_imu_body
         T_b_w = Tb * T_i_w * Tb.inverse()
@@ -354,13 +406,14 @@ class MSCKF:
         thr = self.config.position_std_threshold
         if thr <= 0:
             return
-        d = self.ctx.cov_diag(0, 12, 3)
+        d = yield ("cov_diag", 12, 3)
         if np.max(np.sqrt(d)) < thr:
             return
         self.cam_ids.clear()
         self.map_server.clear()
-        imu, _, _ = self.ctx.get_state(0, want_P=False)
-        self.ctx.set_state(0, imu, None, self._initial_cov())
+        imu, _ = yield ("states",)
+        yield ("set_state", imu, None, self._initial_cov())
 
     def close(self):
-        self.ctx.close()
+        if self._own_ctx:
+            self.ctx.close()
