@@ -113,7 +113,7 @@ def flops_model(probs, B, accepted, valid, feat_off):
     return tot
 
 
-def pmc_traffic(stage, dtype):
+def pmc_traffic(stage, dtype, workload):
     """HBM bytes per step of a stage's kernels from the committed rocprofv3 PMC
     summary (tools/pmc_summary.py; FETCH_SIZE and WRITE_SIZE from separate
     passes), or None if no summary covers them."""
@@ -122,7 +122,7 @@ def pmc_traffic(stage, dtype):
         return None
     with open(path) as fh:
         summ = json.load(fh)
-    if summ.get("dtype") != dtype:
+    if summ.get("dtype") != dtype or summ.get("workload", "N30xF200xB2048") != workload:
         return None
     return summ.get("stages", {}).get(stage, {}).get("bytes_per_step")
 
@@ -214,7 +214,7 @@ def main():
     roof = None
     if dom_flops:
         ach = dom_flops / (dom_ms * 1e-3) / 1e12
-        traffic = pmc_traffic(dom, args.dtype)
+        traffic = pmc_traffic(dom, args.dtype, "N%dxF%dxB%d" % (args.N, args.F, args.batch))
         roof = {"bound": "mfma", "kernel": dom, "achieved": round(ach, 3), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(ach / peak, 5), "traffic": traffic, "ms_per_step": round(dom_ms, 4),
                 "flops_per_step": dom_flops,

@@ -56,6 +56,8 @@ def main():
     ap.add_argument("--dtype", default="fp32")
     ap.add_argument("-o", "--out", default="profiles/pmc_summary.json")
     ap.add_argument("--source", default="")
+    ap.add_argument("--workload", default="N30xF200xB2048",
+                    help="bench workload the passes ran (bench.py only uses the traffic for the same one)")
     a = ap.parse_args()
     fetch, nf = read(a.fetch)
     write, nw = read(a.write)
@@ -73,7 +75,7 @@ def main():
     for st, d in stages.items():
         d["bytes_per_step"] = (d["fetch_kib"] + d["write_kib"]) * 1024 / a.steps
         d["fetch_x2_bytes_per_step"] = (2 * d["fetch_kib"] + d["write_kib"]) * 1024 / a.steps
-    json.dump({"dtype": a.dtype, "steps": a.steps, "source": a.source, "unit": "bytes",
+    json.dump({"dtype": a.dtype, "steps": a.steps, "workload": a.workload, "source": a.source, "unit": "bytes",
                "stages": stages}, open(a.out, "w"), indent=1, sort_keys=True)
     for st, d in sorted(stages.items(), key=lambda kv: -kv[1]["bytes_per_step"]):
         print("%-18s %10.3f GB/step" % (st, d["bytes_per_step"] / 1e9))
