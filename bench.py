@@ -90,8 +90,9 @@ def flops_model(probs, B, accepted, valid, feat_off):
         acc = accepted[feat_off[b]:feat_off[b + 1]].astype(float)
         val = valid[feat_off[b]:feat_off[b + 1]].astype(float)
         k = 4 * M - 3
-        # gating: Y tiles (4x6 . 6x6 . 6x4 per cam pair) + blocked LDL^T of the (4M+4)^2 saddle-point matrix
-        tot["gate"] += 2 * float(np.sum(val * (240.0 * M * (M + 1) / 2 + (4 * M + 4) ** 3 / 6)))
+        # gating (rank-3 reduced saddle point): 3x3 observation-pair blocks Ht_a P_ab Ht_b^T
+        # (3x6 . 6x6 . 6x3 = 162 FMA per pair) + LDL^T of the (3M+4)^2 matrix
+        tot["gate"] += 2 * float(np.sum(val * (162.0 * M * (M + 1) / 2 + (3 * M + 4) ** 3 / 6)))
         # information assembly: per included feature, every observed cam pair takes G_i^T G_j (3 x 6 x 6)
         tot["compress"] += 2 * float(np.sum(acc * (54.0 * M * (M + 1) + 27 * M)))
         if acc.sum() > 0:

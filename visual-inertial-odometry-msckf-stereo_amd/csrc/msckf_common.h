@@ -25,7 +25,10 @@ enum CamField { C_Q = 0, C_P = 4, C_QN = 7 };
 //   W   3x6  this observation's 6 columns of w_j = v_j^T X_{j-1}
 //   Qr  4    rows of Q^T r
 //   R   4    the observation's residual r_i (before projection)
-constexpr int OBS_HX = 0, OBS_V = 24, OBS_W = 36, OBS_QR = 54, OBS_R = 58, OBS_WS = 62;
+// obs_ws record per observation (T): Hx (4x6), V, W, Q^T r, r -- written only
+// when a compact-factor consumer runs (workgroup gating, QR merge) -- and the
+// rank-3 reduced rows for the register-tile gating: Ht (3x6), [r~ (3) | r_n].
+constexpr int OBS_HX = 0, OBS_V = 24, OBS_W = 36, OBS_QR = 54, OBS_R = 58, OBS_HT = 62, OBS_RT = 80, OBS_WS = 84;
 
 // Per-observation Gram terms written by the feature kernel (always fp64),
 // consumed by the information assembly (k_info).  With G = the top 3 rows of

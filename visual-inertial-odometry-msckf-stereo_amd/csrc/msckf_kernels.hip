@@ -780,10 +780,41 @@ __global__ void __launch_bounds__(256) k_feature(DevState<T> st, Params<T> prm, 
             r[s][1] = (CT)z[1] - pc0[1] / pc0[2];
             r[s][2] = (CT)z[2] - pc1[0] / pc1[2];
             r[s][3] = (CT)z[3] - pc1[1] / pc1[2];
+            // rank-3 rows for the register-tile gating: Hx and H_f factor through
+            // Jc = dz/dpc0 + dz/dpc1 R01 (4x3); the reflector I - v v^T / (1 + |n_3|)
+            // maps Jc's unit left null vector n to -sign(n_3) e_4, so rows 0..2 of
+            // the reflected [Hx | r] are the range rows and row 3 carries only the
+            // residual r_n (its Hx part vanishes).
+            CT J[12] = {a00, 0, a02, 0, a00, a12, 0, 0, 0, 0, 0, 0};
+            for (int m = 0; m < 3; ++m) {
+                J[6 + m] = b00 * R01[m] + b02 * R01[6 + m];
+                J[9 + m] = b00 * R01[3 + m] + b12 * R01[6 + m];
+            }
+            auto det3 = [](const CT* x, const CT* y, const CT* w) {
+                return x[0] * (y[1] * w[2] - y[2] * w[1]) - x[1] * (y[0] * w[2] - y[2] * w[0]) +
+                       x[2] * (y[0] * w[1] - y[1] * w[0]);
+            };
+            CT nv[4] = {det3(J + 3, J + 6, J + 9), -det3(J, J + 6, J + 9), det3(J, J + 3, J + 9),
+                        -det3(J, J + 3, J + 6)};
+            CT nn = sqrt(nv[0] * nv[0] + nv[1] * nv[1] + nv[2] * nv[2] + nv[3] * nv[3]);
+            if (!(nn > 0)) { nv[0] = nv[1] = nv[2] = 0; nv[3] = 1; nn = 1; }
+            for (int k = 0; k < 4; ++k) nv[k] /= nn;
+            const CT beta = 1 / (1 + fabs(nv[3]));
+            nv[3] += nv[3] >= 0 ? CT(1) : CT(-1);
+            CT Ht[18], rt4[4];
+            for (int c = 0; c < 6; ++c) {
+                const CT w = nv[0] * Hx[s][c] + nv[1] * Hx[s][6 + c] + nv[2] * Hx[s][12 + c] + nv[3] * Hx[s][18 + c];
+                for (int a = 0; a < 3; ++a) Ht[6 * a + c] = Hx[s][6 * a + c] - beta * nv[a] * w;
+            }
+            const CT wr = nv[0] * r[s][0] + nv[1] * r[s][1] + nv[2] * r[s][2] + nv[3] * r[s][3];
+            for (int a = 0; a < 4; ++a) rt4[a] = r[s][a] - beta * nv[a] * wr;
+            T* wsr = fb.obs_ws + (size_t)(o0 + i) * OBS_WS;
+            store_pairs(wsr + OBS_HT, Ht, 18);
+            store_pairs(wsr + OBS_RT, rt4, 4);
         }
         for (int c = 0; c < 6; ++c)   // Hx_i^T r_i, before r is reflected
             u6[s][c] = Hx[s][c] * r[s][0] + Hx[s][6 + c] * r[s][1] + Hx[s][12 + c] * r[s][2] + Hx[s][18 + c] * r[s][3];
-        if (own) store_pairs(fb.obs_ws + (size_t)(o0 + i) * OBS_WS + OBS_R, r[s], 4);
+        if (own && fb.compact) store_pairs(fb.obs_ws + (size_t)(o0 + i) * OBS_WS + OBS_R, r[s], 4);
     }
     // ---- Householder QR of H_f across the segment (rows 4i..4i+3 with observation i) ----
     CT V[OPL][12];
@@ -866,8 +897,8 @@ __global__ void __launch_bounds__(256) k_feature(DevState<T> st, Params<T> prm, 
             W[c] = w0; W[6 + c] = w1; W[12 + c] = w2;
         }
         T* ws = fb.obs_ws + (size_t)(o0 + i) * OBS_WS;
-        store_pairs(ws + OBS_HX, Hx[s], 24);
-        if (fb.compact) {   // compact factors: only the LDS / global gate and the QR merge read them
+        if (fb.compact) {   // Hx and the compact factors: only the LDS / global gate and the QR merge read them
+            store_pairs(ws + OBS_HX, Hx[s], 24);
             store_pairs(ws + OBS_V, V[s], 12);
             store_pairs(ws + OBS_W, W, 18);
             store_pairs(ws + OBS_QR, r[s], 4);
@@ -1138,43 +1169,56 @@ __global__ void __launch_bounds__(256) k_gate_lds(DevState<T> st, Params<T> prm,
 }
 
 // One-wavefront gating with the matrix in registers (production path for
-// M <= 34).  With Y = Hx P Hx^T + s2 I (4M x 4M, PD) and N an orthonormal basis
+// M <= 40).  With Y = Hx P Hx^T + s2 I (4M x 4M, PD) and N an orthonormal basis
 // of the left nullspace of H_f, the reference's S = N^T Y N (msckf.py:607-609
 // on H0 = N^T Hx) satisfies the oblique-projection identity
 //   N S^-1 N^T = Y^-1 - Y^-1 H_f (H_f^T Y^-1 H_f)^-1 H_f^T Y^-1,
 // so gamma = r0^T S^-1 r0 is what an LDL^T elimination of the saddle-point
-// matrix
-//     [ Y      H_f  r ]
-//     [ H_f^T  0    0 ]      (4M + 4 square, no pivoting: Y is PD and the
-//     [ r^T    0    0 ]       H_f block's Schur complement is negative definite)
-// leaves in its last pivot: -gamma.  No projection is formed at all.
-// The matrix is held as 4x4 tiles (lower triangle, column-major tile order;
-// tile t belongs to lane t % 64, slot t / 64); tile row M is [H_f^T ; r^T].
+// matrix [[Y, H_f, r], [H_f^T, 0, 0], [r^T, 0, 0]] leaves in its last pivot:
+// -gamma.  No projection is formed at all.
+// Rank-3 reduction: every observation's Hx_i (4x6) and H_f,i (4x3) factor
+// through the 4x3 projection Jacobian Jc_i = dz/dp_c0 + dz/dp_c1 R_c0c1
+// (msckf.py:457-480: dp_c1/dx = R_c0c1 dp_c0/dx), so k_feature rotates each
+// observation's rows by a reflector taking Jc_i's left null vector to e_4:
+// three range rows Ht_i = (Q_i^T Hx_i)[0:3], r~_i, and one null row whose
+// Hx / H_f entries are exactly zero and whose residual r_n,i decouples (pivot
+// s2).  gamma is invariant under these orthogonal row maps (quirk Q4), so
+//   gamma = gamma(saddle point of the 3M range rows) + sum_i r_n,i^2 / s2,
+// a (3M + 4)-square elimination instead of (4M + 4): ~(3/4)^3 of the flops.
+// Layout: the 3M range rows padded to n3 = 4 ceil(3M/4) (padding rows are
+// unit pivots) plus the B row [H_f~^T ; r~^T], as 4x4 tiles (lower triangle,
+// column-major tile order; tile t belongs to lane t % 64, slot t / 64).
+// Y tiles: the wave forms all 3x3 observation-pair blocks
+// Ht_a P_{s_a s_b} Ht_b^T (a >= b) into LDS, then every lane assembles its
+// 4x4 tiles of the compact row space from there.
 // Blocked LDL^T, one tile column per step: the diagonal tile's owner factors
 // it, the panel tiles' owners publish W = A L_d^-T by row through LDS, and
 // every tile right of the panel takes the rank-4 update from registers; slots
 // whose tiles all lie in finished columns are skipped.  The last tile's owner
 // finishes with the three negative pivots.  No workgroup barriers:
-// 4 independent features per 256-thread workgroup.
+// up to 4 independent features (waves) per workgroup, as many as the LDS allows.
 // Panel buffers hold one 4x4 block per tile row, padded to GB floats (80 B) /
 // doubles (144 B) so that consecutive lanes' ds_read_b128 of consecutive
 // blocks hit distinct banks.
 template <typename T>
 __host__ __device__ constexpr int gate_blk() { return sizeof(T) == 8 ? 18 : 20; }
+__host__ __device__ constexpr int gate_nt(int M) { return (3 * M + 3) / 4 + 1; }   // tile rows: Y rows + B row
+template <typename T>
+__host__ __device__ constexpr int gate_area_T(int Mmax) {   // Y block staging / panel buffers
+    return 9 * Mmax * (Mmax + 1) / 2 > 2 * gate_blk<T>() * gate_nt(Mmax) ? 9 * Mmax * (Mmax + 1) / 2
+                                                                       : 2 * gate_blk<T>() * gate_nt(Mmax);
+}
 template <typename T>
 __host__ __device__ constexpr int gate_wave_lds_T(int Mmax) {
-    return 24 * Mmax + 2 * gate_blk<T>() * (Mmax + 1);   // hx, panel rows (raw -> W D^-1), W^T blocks
+    return 22 * Mmax + gate_area_T<T>(Mmax);   // Ht rows, [r~ | r_n], staging / panels
 }
 
 template <typename T, int TPL>
 __global__ void __launch_bounds__(256) k_gate_wave(DevState<T> st, Params<T> prm, FeatBatch<T> fb,
                                                    const int* __restrict__ flist, int nlist, int Mmax, int phases) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-#ifdef GW_PHASES_CONST
-    phases = GW_PHASES_CONST;
-#endif
-    const int li = blockIdx.x * 4 + wv;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wpb = blockDim.x >> 6;
+    const int li = blockIdx.x * wpb + wv;
     if (li >= nlist) return;
     const int f = flist[li];
     if (!fb.valid[f]) {
@@ -1182,18 +1226,30 @@ __global__ void __launch_bounds__(256) k_gate_wave(DevState<T> st, Params<T> prm
         return;
     }
     const int b = fb.feat_filter[f];
-    const int o0 = fb.obs_off[f], M = fb.obs_off[f + 1] - o0;
-    const int nT = M + 1, ntiles = nT * (nT + 1) / 2;
-    T* hx = reinterpret_cast<T*>(smem_raw) + (size_t)wv * gate_wave_lds_T<T>(Mmax);
+    const int o0 = fb.obs_off[f], M = fb.obs_off[f + 1] - o0, M3 = 3 * M;
+    const int nY = (M3 + 3) >> 2;               // Y tile rows = elimination steps
+    const int nT = nY + 1, ntiles = nT * (nT + 1) / 2;
+    T* ht = reinterpret_cast<T*>(smem_raw) + (size_t)wv * gate_wave_lds_T<T>(Mmax);
+    T* rt = ht + 18 * Mmax;                    // [Mmax][4]: r~ (3), r_n
+    T* area = rt + 4 * Mmax;
     constexpr int GB = gate_blk<T>();
-    T* wd = hx + 24 * Mmax;           // [nT][GB]  panel rows: raw tile rows, then W D^-1
-    T* wt = wd + GB * (Mmax + 1);     // [nT][GB]  W^T per 4-row block: wt[blk][4 c + y] = W[4 blk + y][c]
-    int* slot = reinterpret_cast<int*>(reinterpret_cast<T*>(smem_raw) + 4 * gate_wave_lds_T<T>(Mmax)) + wv * Mmax;
+    T* stage = area;                           // [M (M + 1) / 2][9] Y blocks, column-major lower
+    T* wd = area;                              // [nT][GB]  panel rows: raw tile rows, then W D^-1
+    T* wt = area + GB * gate_nt(Mmax);         // [nT][GB]  W^T per 4-row block: wt[blk][4 c + y] = W[4 blk + y][c]
+    int* slot = reinterpret_cast<int*>(reinterpret_cast<T*>(smem_raw) + wpb * gate_wave_lds_T<T>(Mmax)) + wv * Mmax;
     const T* ws = fb.obs_ws + (size_t)o0 * OBS_WS;
-    for (int e = lane; e < 24 * M; e += 64) {
-        const int o = e / 24;
-        hx[e] = ws[(size_t)o * OBS_WS + OBS_HX + (e - 24 * o)];
+    for (int e = lane; e < 18 * M; e += 64) {
+        const int o = e / 18;
+        ht[e] = ws[(size_t)o * OBS_WS + OBS_HT + (e - 18 * o)];
     }
+    T rn2 = 0;
+    for (int e = lane; e < 4 * M; e += 64) {
+        const T v = ws[(size_t)(e >> 2) * OBS_WS + OBS_RT + (e & 3)];
+        rt[e] = v;
+        if ((e & 3) == 3) rn2 += v * v;
+    }
+    rn2 = wave_sum(rn2);
+    const T inv_s2 = T(1) / prm.sigma2;
     for (int i = lane; i < M; i += 64) slot[i] = fb.obs_cam[o0 + i];
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 
@@ -1214,9 +1270,66 @@ __global__ void __launch_bounds__(256) k_gate_wave(DevState<T> st, Params<T> prm
 #define TL(s) (crd[s] >> 16)
 #define OK(s) (crd[s] >= 0)
 
-    // ---- Y = Hx P Hx^T tiles, r row ----
+    // ---- Y: every observation-pair block Ht_a P_ab Ht_b^T (a >= b, 3x3) into
+    // LDS (column-major lower block order, two blocks per lane in flight), then
+    // each lane assembles its tiles from there ----
     const T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
     const int ldp = st.Dmax;
+    const T s2 = prm.sigma2;
+    const int nbk = M * (M + 1) / 2;
+    if (phases & 1) {
+        for (int k0 = 0; k0 < nbk; k0 += 128) {
+            T Pl[2][36];
+            int oa[2], ob[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int k = k0 + 64 * j + lane;
+                const int kc = k < nbk ? k : 0;
+                const int c = colmajor_col(kc, M);
+                ob[j] = c;
+                oa[j] = c + kc - (c * M - c * (c - 1) / 2);
+                const T* Pb = P + (size_t)(21 + 6 * slot[oa[j]]) * ldp + 21 + 6 * slot[ob[j]];
+                // each 6-element block row in wide loads (gfx950 takes dword-aligned
+                // multi-dword global loads: dwordx4 + dwordx2 per fp32 row)
+#pragma unroll
+                for (int u = 0; u < 6; ++u) {
+                    if (k < nbk) {
+                        __builtin_memcpy(Pl[j] + 6 * u, Pb + (size_t)u * ldp, 6 * sizeof(T));
+                    } else {
+#pragma unroll
+                        for (int c2 = 0; c2 < 6; ++c2) Pl[j][6 * u + c2] = T(0);
+                    }
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int k = k0 + 64 * j + lane;
+                if (k >= nbk) continue;
+                const T* Ha = ht + 18 * oa[j];
+                const T* Hb = ht + 18 * ob[j];
+                T* dst = stage + 9 * k;
+#pragma unroll
+                for (int x = 0; x < 3; ++x) {
+                    T t1[6];
+#pragma unroll
+                    for (int c = 0; c < 6; ++c) {
+                        T acc = 0;
+#pragma unroll
+                        for (int u = 0; u < 6; ++u) acc += Ha[6 * x + u] * Pl[j][6 * u + c];
+                        t1[c] = acc;
+                    }
+#pragma unroll
+                    for (int y = 0; y < 3; ++y) {
+                        T acc = 0;
+#pragma unroll
+                        for (int u = 0; u < 6; ++u) acc += t1[u] * Hb[6 * y + u];
+                        dst[3 * x + y] = acc;
+                    }
+                }
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // one wave: its stores are now visible to all lanes
+    }
     T a[TPL][4][4];
 #pragma unroll
     for (int s = 0; s < TPL; ++s) {
@@ -1224,53 +1337,54 @@ __global__ void __launch_bounds__(256) k_gate_wave(DevState<T> st, Params<T> prm
         for (int x = 0; x < 4; ++x)
 #pragma unroll
             for (int y = 0; y < 4; ++y) a[s][x][y] = 0;
-        if (!OK(s) || !(phases & 1)) continue;
-        const int i = TI(s), l = TL(s);
-        if (i < M) {
-            const T* Pb = P + (size_t)(21 + 6 * slot[i]) * ldp + 21 + 6 * slot[l];
-            T Pl[36];
+        // B row: [H_f~^T ; r~^T] with H_f~ = -Ht[:, 3:6]
+        if (!OK(s) || TI(s) != nY || TL(s) >= nY) continue;
 #pragma unroll
-            for (int k = 0; k < 6; ++k)
+        for (int y = 0; y < 4; ++y) {
+            const int p = 4 * TL(s) + y;
+            if (p >= M3) continue;
+            const int o = p / 3, c = p - 3 * o;
 #pragma unroll
-                for (int c = 0; c < 6; ++c) Pl[6 * k + c] = Pb[(size_t)k * ldp + c];
-            const T* Hi = hx + 24 * i;
-            const T* Hl = hx + 24 * l;
-#pragma unroll
-            for (int x = 0; x < 4; ++x) {
-                T t1[6];
-#pragma unroll
-                for (int c = 0; c < 6; ++c) {
-                    T acc = 0;
-#pragma unroll
-                    for (int k = 0; k < 6; ++k) acc += Hi[6 * x + k] * Pl[6 * k + c];
-                    t1[c] = acc;
-                }
-#pragma unroll
-                for (int y = 0; y < 4; ++y) {
-                    T acc = 0;
-#pragma unroll
-                    for (int k = 0; k < 6; ++k) acc += t1[k] * Hl[6 * y + k];
-                    a[s][x][y] = acc;
-                }
-            }
-            if (i == l)
-#pragma unroll
-                for (int x = 0; x < 4; ++x) a[s][x][x] += prm.sigma2;
-        } else if (l < M) {   // [H_f^T ; r^T] for observation l; H_f = -Hx[:, 3:6]
-            const T* Hl = hx + 24 * l;
-#pragma unroll
-            for (int y = 0; y < 4; ++y) {
-#pragma unroll
-                for (int x = 0; x < 3; ++x) a[s][x][y] = -Hl[6 * y + 3 + x];
-                a[s][3][y] = ws[(size_t)l * OBS_WS + OBS_R + y];
-            }
+            for (int x = 0; x < 3; ++x) a[s][x][y] = -ht[18 * o + 6 * c + 3 + x];
+            a[s][3][y] = rt[4 * o + c];
         }
-        asm volatile("" ::: "memory");
     }
 
-    // ---- blocked LDL^T, one 4-wide tile column per step ----
+    if (phases & 1) {
+#pragma unroll
+        for (int s = 0; s < TPL; ++s) {
+            if (!OK(s) || TI(s) >= nY) continue;
+            const int tl = TL(s), ti = TI(s);
+            int oq[4], cq[4], op[4], cp[4];
+#pragma unroll
+            for (int x = 0; x < 4; ++x) {
+                oq[x] = (4 * ti + x) / 3;
+                cq[x] = 4 * ti + x - 3 * oq[x];
+                op[x] = (4 * tl + x) / 3;
+                cp[x] = 4 * tl + x - 3 * op[x];
+            }
+#pragma unroll
+            for (int x = 0; x < 4; ++x)
+#pragma unroll
+                for (int y = 0; y < 4; ++y) {
+                    const int q = 4 * ti + x, p = 4 * tl + y;
+                    T v = q == p ? T(1) : T(0);
+                    if (q < M3 && p < M3) {   // block (max, min) of the pair, column-major lower
+                        const int hi = oq[x] >= op[y] ? oq[x] : op[y], lo = oq[x] >= op[y] ? op[y] : oq[x];
+                        const int e = oq[x] >= op[y] ? 3 * cq[x] + cp[y] : 3 * cp[y] + cq[x];
+                        v = stage[9 * (lo * M - lo * (lo - 1) / 2 + hi - lo) + e];
+                        if (q == p) v += s2;
+                    }
+                    a[s][x][y] = v;
+                }
+            asm volatile("" ::: "memory");
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads done before the panel buffers reuse the area
+    }
+
+    // ---- blocked LDL^T over the nY Y tile columns, 4 pivots per step ----
     bool fail = false;
-    for (int tj = 0; tj < ((phases & 4) ? M : 0); ++tj) {
+    for (int tj = 0; tj < ((phases & 4) ? nY : 0); ++tj) {
         // 1. owners of the tile column dump it (raw rows 4 tj .. 4 nT - 1)
 #pragma unroll
         for (int s = 0; s < TPL; ++s) {
@@ -1351,8 +1465,8 @@ __global__ void __launch_bounds__(256) k_gate_wave(DevState<T> st, Params<T> prm
             asm volatile("" ::: "memory");   // keep one slot's operands live at a time
         }
     }
-    // the last tile [[H_f^T Y^-1 H_f, .], [., r^T Y^-1 r]] (negated): three
-    // negative pivots, then -gamma
+    // the last tile [[H_f~^T Y~^-1 H_f~, .], [., r~^T Y~^-1 r~]] (negated): three
+    // negative pivots, then -gamma of the range rows; the null rows add |r_n|^2 / s2
 #pragma unroll
     for (int s = 0; s < TPL; ++s) {
         if (64 * s + lane == ntiles - 1) {
@@ -1364,7 +1478,7 @@ __global__ void __launch_bounds__(256) k_gate_wave(DevState<T> st, Params<T> prm
             const T d2 = a[s][2][2] - l20 * l20 * d0 - l21 * l21 * d1;
             const T l32 = (a[s][3][2] - l30 * l20 * d0 - l31 * l21 * d1) / d2;
             const T d3 = a[s][3][3] - l30 * l30 * d0 - l31 * l31 * d1 - l32 * l32 * d2;
-            T gam = -d3;
+            T gam = -d3 + rn2 * inv_s2;
             if (fail || !(d0 < T(0)) || !(d1 < T(0)) || !(d2 < T(0)) || !(gam == gam)) gam = T(INFINITY);
             fb.gamma[f] = gam;
             fb.accept[f] = (gam < fb.chi2[f]) ? 1 : 0;
@@ -1375,12 +1489,13 @@ __global__ void __launch_bounds__(256) k_gate_wave(DevState<T> st, Params<T> prm
 #undef OK
 }
 
-// Large-track gating (34 < M <= 62): the saddle-point LDL^T of k_gate_wave on
-// rchol_core's fp64 register tiles, one workgroup per feature.  The 4M Y
-// pivots are eliminated; the trailing 4x4 tile is the negated
-// [[H_f^T Y^-1 H_f, .], [., r^T Y^-1 r]] block, finished by one thread with
-// the three negative pivots: gamma = -(last pivot).  Y entries are formed
-// on load from the fp64-staged Hx rows and the P blocks.
+// Large-track gating (40 < M <= 82): the reduced saddle-point LDL^T of
+// k_gate_wave (3M range rows padded to 4 ceil(3M/4), then the B row
+// [H_f~^T ; r~^T]) on rchol_core's fp64 register tiles, one workgroup per
+// feature.  The Y pivots are eliminated; the trailing 4x4 tile is the negated
+// [[H_f~^T Y~^-1 H_f~, .], [., r~^T Y~^-1 r~]] block, finished by one thread
+// with the three negative pivots: gamma = -(last pivot) + |r_n|^2 / s2.  Y
+// entries are formed on load from the fp64-staged Ht rows and the P blocks.
 template <typename T, int NT, int TPL>
 __global__ void __launch_bounds__(NT) k_gate_big(DevState<T> st, Params<T> prm, FeatBatch<T> fb,
                                                  const int* __restrict__ flist) {
@@ -1391,19 +1506,26 @@ __global__ void __launch_bounds__(NT) k_gate_big(DevState<T> st, Params<T> prm, 
         return;
     }
     const int b = fb.feat_filter[f];
-    const int o0 = fb.obs_off[f], M = fb.obs_off[f + 1] - o0, n4 = 4 * M;
-    const int nrow = M + 1;
-    double* hx = reinterpret_cast<double*>(smem_raw);   // [M][24] Hx rows, then [M][4] residuals
-    double* rr = hx + 24 * M;
-    double* corner = rr + 4 * M;                         // [16]
-    int* slot = reinterpret_cast<int*>(corner + 16);     // [M]
+    const int o0 = fb.obs_off[f], M = fb.obs_off[f + 1] - o0, M3 = 3 * M;
+    const int nrow = gate_nt(M), n3 = 4 * (nrow - 1);
+    double* ht = reinterpret_cast<double*>(smem_raw);   // [M][18] Ht rows, then [M][4] r~ | r_n
+    double* rr = ht + 18 * M;
+    double* corner = rr + 4 * M;                         // [16], then the |r_n|^2 partials
+    int* slot = reinterpret_cast<int*>(corner + 16 + NT / 64);   // [M]
     double* lds = reinterpret_cast<double*>(slot + ((M + 3) & ~3));   // rchol panel buffers
     const T* ws = fb.obs_ws + (size_t)o0 * OBS_WS;
-    for (int e = threadIdx.x; e < 24 * M; e += NT) {
-        const int o = e / 24;
-        hx[e] = (double)ws[(size_t)o * OBS_WS + OBS_HX + (e - 24 * o)];
+    for (int e = threadIdx.x; e < 18 * M; e += NT) {
+        const int o = e / 18;
+        ht[e] = (double)ws[(size_t)o * OBS_WS + OBS_HT + (e - 18 * o)];
     }
-    for (int e = threadIdx.x; e < 4 * M; e += NT) rr[e] = (double)ws[(size_t)(e >> 2) * OBS_WS + OBS_R + (e & 3)];
+    double rn2 = 0;
+    for (int e = threadIdx.x; e < 4 * M; e += NT) {
+        const double v = (double)ws[(size_t)(e >> 2) * OBS_WS + OBS_RT + (e & 3)];
+        rr[e] = v;
+        if ((e & 3) == 3) rn2 += v * v;
+    }
+    rn2 = wave_sum(rn2);
+    if ((threadIdx.x & 63) == 0) corner[16 + (threadIdx.x >> 6)] = rn2;
     for (int i = threadIdx.x; i < M; i += NT) slot[i] = fb.obs_cam[o0 + i];
     __syncthreads();
     const T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
@@ -1411,14 +1533,15 @@ __global__ void __launch_bounds__(NT) k_gate_big(DevState<T> st, Params<T> prm, 
     const double s2 = (double)prm.sigma2;
     auto load = [&](int i, int j) -> double {
         if (i < j) { const int t = i; i = j; j = t; }
-        if (i >= n4) {   // [H_f^T ; r^T] rows, zero corner
-            if (j >= n4) return 0.0;
-            const int x = i - n4, l = j >> 2, c = j & 3;
-            return x < 3 ? -hx[24 * l + 6 * c + 3 + x] : rr[4 * l + c];
+        if (i >= n3) {   // B row [H_f~^T ; r~^T], zero corner
+            if (j >= n3 || j >= M3) return 0.0;
+            const int x = i - n3, o = j / 3, c = j - 3 * o;
+            return x < 3 ? -ht[18 * o + 6 * c + 3 + x] : rr[4 * o + c];
         }
-        const int oi = i >> 2, oj = j >> 2;
-        const double* hi = hx + 24 * oi + 6 * (i & 3);
-        const double* hj = hx + 24 * oj + 6 * (j & 3);
+        if (i >= M3 || j >= M3) return i == j ? 1.0 : 0.0;   // padding rows: unit pivots
+        const int oi = i / 3, oj = j / 3;
+        const double* hi = ht + 18 * oi + 6 * (i - 3 * oi);
+        const double* hj = ht + 18 * oj + 6 * (j - 3 * oj);
         const T* Pb = P + (size_t)(21 + 6 * slot[oi]) * ldp + 21 + 6 * slot[oj];
         double y = i == j ? s2 : 0.0;
         for (int u = 0; u < 6; ++u) {
@@ -1429,10 +1552,12 @@ __global__ void __launch_bounds__(NT) k_gate_big(DevState<T> st, Params<T> prm, 
         return y;
     };
     auto panel = [](int, int, double, double, double, double) {};
-    auto trail = [&](int i, int j, double v) { corner[(i - n4) * 4 + (j - n4)] = v; };
-    const bool ok = rchol_core<NT, TPL>(nrow, nrow, M, lds, load, panel, trail);
+    auto trail = [&](int i, int j, double v) { corner[(i - n3) * 4 + (j - n3)] = v; };
+    const bool ok = rchol_core<NT, TPL>(nrow, nrow, nrow - 1, lds, load, panel, trail);
     __syncthreads();
     if (threadIdx.x == 0) {
+        double rsum = 0;
+        for (int w = 0; w < NT / 64; ++w) rsum += corner[16 + w];
         T gam = T(INFINITY);
         if (ok) {
             const double* a = corner;
@@ -1444,7 +1569,7 @@ __global__ void __launch_bounds__(NT) k_gate_big(DevState<T> st, Params<T> prm, 
             const double d2 = a[10] - l20 * l20 * d0 - l21 * l21 * d1;
             const double l32 = (a[14] - l30 * l20 * d0 - l31 * l21 * d1) / d2;
             const double d3 = a[15] - l30 * l30 * d0 - l31 * l31 * d1 - l32 * l32 * d2;
-            if (d0 < 0.0 && d1 < 0.0 && d2 < 0.0 && -d3 == -d3) gam = (T)(-d3);
+            if (d0 < 0.0 && d1 < 0.0 && d2 < 0.0 && -d3 == -d3) gam = (T)(-d3 + rsum / s2);
         }
         fb.gamma[f] = gam;
         fb.accept[f] = (gam < fb.chi2[f]) ? 1 : 0;
@@ -1452,8 +1577,8 @@ __global__ void __launch_bounds__(NT) k_gate_big(DevState<T> st, Params<T> prm, 
 }
 
 size_t gate_big_lds_bytes(int maxM) {
-    return (24 * (size_t)maxM + 4 * maxM + 16) * sizeof(double) + ((maxM + 3) & ~3) * sizeof(int) +
-           rchol_lds_doubles(maxM + 1) * sizeof(double);
+    return (22 * (size_t)maxM + 16 + 16) * sizeof(double) + ((maxM + 3) & ~3) * sizeof(int) +
+           rchol_lds_doubles(gate_nt(maxM)) * sizeof(double);
 }
 
 // ===========================================================================
@@ -2067,7 +2192,10 @@ size_t gate_lds_bytes(int maxM) {
 template <typename T, int TPL>
 static void launch_gate_wave(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const FeatBatch<T>& fb,
                              const int* list, int cnt, int Mmax) {
-    const size_t lds = 4 * ((size_t)gate_wave_lds_T<T>(Mmax) * sizeof(T) + (size_t)Mmax * sizeof(int));
+    // waves (features) per workgroup: 4 unless their LDS would exceed the CU's 160 KB
+    const size_t per_wave = (size_t)gate_wave_lds_T<T>(Mmax) * sizeof(T) + (size_t)Mmax * sizeof(int);
+    const int wpb = 4 * per_wave <= 160 * 1024 ? 4 : (2 * per_wave <= 160 * 1024 ? 2 : 1);
+    const size_t lds = wpb * per_wave;
     static size_t attr = 64 * 1024;
     if (lds > attr) {
         (void)hipFuncSetAttribute((const void*)k_gate_wave<T, TPL>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2079,8 +2207,8 @@ static void launch_gate_wave(hipStream_t s, const DevState<T>& st, const Params<
         const char* e = getenv("MSCKF_GATE_PHASES");
         phases = e ? atoi(e) : 7;
     }
-    hipLaunchKernelGGL((k_gate_wave<T, TPL>), dim3((cnt + 3) / 4), dim3(256), lds, s, st, prm, fb, list, cnt, Mmax,
-                       phases);
+    hipLaunchKernelGGL((k_gate_wave<T, TPL>), dim3((cnt + wpb - 1) / wpb), dim3(64 * wpb), lds, s, st, prm, fb, list,
+                       cnt, Mmax, phases);
 }
 
 // Features are launched in size classes (by M, listed on the host at load
@@ -2099,7 +2227,7 @@ static int gate_mode() {   // MSCKF_GATE=lds forces the workgroup kernel for eve
 // The workgroup gating kernels and the QR merge read the compact factors
 // (V, W, Q^T r, tau) that k_feature otherwise skips.
 bool feature_needs_compact(int maxM, int Cmax) {
-    return gate_mode() == 1 || maxM > GateClasses::LIM[GateClasses::NC - 2] || update_mode(Cmax) == UPD_QR;
+    return gate_mode() == 1 || maxM > GateClasses::LIM[GateClasses::NC - 2] || update_mode(Cmax) == UPD_QR;   // (also Hx, r)
 }
 
 template <typename T>
@@ -2117,8 +2245,8 @@ void launch_gate(hipStream_t s, const DevState<T>& st, const Params<T>& prm, con
         if (cnt == 0) continue;
         const int maxM = gc.maxM[c];
         const int* list = gc.list + gc.off[c];
-        if (mode == 0 && c == GateClasses::NC - 2) {   // 34 < M <= 62: register tiles, one workgroup per feature
-            const int nrow = maxM + 1, tiles = nrow * (nrow + 1) / 2;
+        if (mode == 0 && c == GateClasses::NC - 2) {   // 40 < M <= 82: register tiles, one workgroup per feature
+            const int nrow = gate_nt(maxM), tiles = nrow * (nrow + 1) / 2;
             const size_t lds = gate_big_lds_bytes(maxM);
             if (tiles <= 256 * 4) {
                 static bool a1 = false;
@@ -2137,9 +2265,9 @@ void launch_gate(hipStream_t s, const DevState<T>& st, const Params<T>& prm, con
                 case 2: launch_gate_wave<T, 2>(s, st, prm, fb, list, cnt, maxM); break;
                 case 3: launch_gate_wave<T, 3>(s, st, prm, fb, list, cnt, maxM); break;
                 case 4: launch_gate_wave<T, 4>(s, st, prm, fb, list, cnt, maxM); break;
+                case 5: launch_gate_wave<T, 5>(s, st, prm, fb, list, cnt, maxM); break;
                 case 6: launch_gate_wave<T, 6>(s, st, prm, fb, list, cnt, maxM); break;
-                case 8: launch_gate_wave<T, 8>(s, st, prm, fb, list, cnt, maxM); break;
-                default: launch_gate_wave<T, 10>(s, st, prm, fb, list, cnt, maxM); break;
+                default: launch_gate_wave<T, 8>(s, st, prm, fb, list, cnt, maxM); break;
             }
             continue;
         }

@@ -90,9 +90,12 @@ void launch_feature(hipStream_t, const DevState<T>&, const Params<T>&, const Fea
 // workgroup register-tile kernel k_gate_big; the last class the workgroup LDS
 // kernel (or its global-memory variant).
 struct GateClasses {
+    // one-wave classes by the tiles of the reduced (3M + 4)-square matrix,
+    // ceil((gate_nt(M) (gate_nt(M) + 1) / 2) / 64) per lane; then the
+    // register-tile workgroup kernel (nT <= 63) and the global-memory kernel
     static constexpr int NC = 9;
-    static constexpr int LIM[NC] = {9, 14, 18, 21, 26, 30, 34, 62, 1 << 30};
-    static constexpr int TPL[NC - 2] = {1, 2, 3, 4, 6, 8, 10};   // one-wave classes
+    static constexpr int LIM[NC] = {12, 18, 24, 28, 30, 34, 40, 82, 1 << 30};
+    static constexpr int TPL[NC - 2] = {1, 2, 3, 4, 5, 6, 8};
     const int* list = nullptr;
     int off[NC + 1] = {};
     int maxM[NC] = {};
