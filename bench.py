@@ -47,6 +47,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-ate", action="store_true", help="skip the ATE replay leg")
+    ap.add_argument("--no-prop", action="store_true", help="skip the IMU-propagation leg")
     return ap.parse_args()
 
 
@@ -154,6 +155,44 @@ def cpu_baseline(args, probs):
                       "numpy/OpenBLAS 1 thread, oracle/msckf_oracle.py" % (done, args.N, args.F)}
 
 
+def propagation_leg(ctx, args, n_samples=10, steps=5):
+    """IMU propagation (A2-A4) reported separately, at the same
+    D, as IMU samples/s: every filter of the batch takes n_samples samples
+    (one frame's worth at 200 Hz IMU / 20 Hz camera) in ONE launch of
+    msckf_propagate_batch.  It is HBM/latency-class work, so its roofline is
+    HBM: algorithmic bytes per filter = read P[0:21, :] (21 D) + write P11
+    (441) and both IMU x cam cross blocks (2 * 21 C), in the context's
+    scalar type.  Device time from HIP events on the launch stream; the
+    host->device copy of the samples is outside it."""
+    B, N = args.batch, args.N
+    rng = np.random.default_rng(5)
+    n = B * n_samples
+    dt = np.full(n, 0.005)
+    gyro = 0.2 * rng.standard_normal((n, 3))
+    acc = rng.standard_normal((n, 3)) + np.array([0.0, 0.0, 9.81])
+    filters = np.arange(B, dtype=np.int32)
+    off = (np.arange(B + 1) * n_samples).astype(np.int32)
+    ctx.restore()
+    ctx.propagate_batch(filters, off, dt, gyro, acc)          # warm-up
+    ctx.set_profiling(True)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ctx.restore()
+        ctx.propagate_batch(filters, off, dt, gyro, acc)
+    ctx.sync()
+    el = time.perf_counter() - t0
+    kms = ctx.kernel_times()["propagate"][0] / steps
+    ts = 4 if args.dtype == "fp32" else 8
+    D, C = 21 + 6 * N, 6 * N
+    nbytes = B * (21 * D + 441 + 2 * 21 * C) * ts
+    gbs = nbytes / (kms * 1e-3) / 1e9
+    return {"value": round(n / (kms * 1e-3), 1), "unit": "IMU samples/s (device time)",
+            "wall_samples_per_s": round(n * steps / el, 1), "filters": B, "samples_per_filter": n_samples,
+            "D": D, "kernel_ms": round(kms, 4),
+            "roofline": {"bound": "hbm", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(gbs / HBM_PEAK_GBS, 5), "bytes_per_launch": nbytes}}
+
+
 def ate_leg():
     """The metric's second half, "ATE RMSE vs ref": the deterministic replay
     (msckf_amd.replay) of the 200-frame synthetic stereo+IMU stream through the
@@ -239,6 +278,8 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args, probs)
+    if not args.no_prop:
+        out["propagation"] = propagation_leg(ctx, args)
     if rank == 0 and not args.no_ate:
         out["ate"] = ate_leg()
     if rank == 0:

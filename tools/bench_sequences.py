@@ -1,0 +1,63 @@
+"""SURVEY config 4 ("all 11 EuRoC sequences batched"), on synthetic streams of
+the same shape (EuRoC is not reachable here): S stereo+IMU sequences replayed
+through ONE device context by the multi-sequence scheduler
+(msckf_amd.scheduler.MultiMSCKF), against the same S sequences replayed one
+after another through the single-filter drop-in class.  Prints one JSON line:
+frames/s of both, the batched launch counts, and ATE vs ground truth.
+
+    python tools/bench_sequences.py [--seqs 11] [--frames 200] [--fp32]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import msckf_pkg  # noqa: E402,F401
+import msckf_amd  # noqa: E402
+from msckf_amd import synth  # noqa: E402
+from msckf_amd.replay import FeatureStream, replay  # noqa: E402
+from msckf_amd.scheduler import MultiMSCKF  # noqa: E402
+from msckf_amd.trajectory import ate  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seqs", type=int, default=11)
+    ap.add_argument("--frames", type=int, default=200)
+    ap.add_argument("--fp32", action="store_true")
+    ap.add_argument("--no-single", action="store_true")
+    a = ap.parse_args()
+    dtype = np.float32 if a.fp32 else np.float64
+    streams = [FeatureStream.from_synthetic(synth.make_sequence(a.frames, 100 + i)) for i in range(a.seqs)]
+    n_frames = sum(s.n_frames for s in streams)
+    multi = MultiMSCKF(a.seqs, dtype=dtype)
+    t0 = time.perf_counter()
+    trajs = multi.run_streams(streams)
+    el_b = time.perf_counter() - t0
+    launches = dict(multi.launches)
+    multi.close()
+    out = {"config": "SURVEY config 4 shape: %d synthetic stereo+IMU sequences x %d frames, %s"
+                     % (a.seqs, a.frames, "fp32" if a.fp32 else "fp64"),
+           "batched_frames_per_s": round(n_frames / el_b, 1), "batched_s": round(el_b, 2),
+           "batched_launches": launches,
+           "ate_vs_gt_m": [round(ate(t, s.gt), 5) for t, s in zip(trajs, streams)]}
+    if not a.no_single:
+        t0 = time.perf_counter()
+        for s in streams:
+            flt = msckf_amd.MSCKF(dtype=dtype)
+            replay(flt, s)
+            flt.close()
+        el_s = time.perf_counter() - t0
+        out["single_frames_per_s"] = round(n_frames / el_s, 1)
+        out["single_s"] = round(el_s, 2)
+        out["speedup"] = round(el_s / el_b, 2)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -9,8 +9,8 @@ OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT/stats $OUT/fetch $OUT/write
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/stats -o run --output-format csv -- \
-    python3 bench.py --steps $STEPS --warmup 1 --no-cpu --no-ate > $OUT/stats/bench.log 2>&1
+    python3 bench.py --steps $STEPS --warmup 1 --no-cpu --no-ate --no-prop > $OUT/stats/bench.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "msckf" -d $OUT/fetch -o run --output-format csv -- \
-    python3 bench.py --steps 1 --warmup 0 --no-cpu --no-ate > $OUT/fetch/bench.log 2>&1
+    python3 bench.py --steps 1 --warmup 0 --no-cpu --no-ate --no-prop > $OUT/fetch/bench.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "msckf" -d $OUT/write -o run --output-format csv -- \
-    python3 bench.py --steps 1 --warmup 0 --no-cpu --no-ate > $OUT/write/bench.log 2>&1
+    python3 bench.py --steps 1 --warmup 0 --no-cpu --no-ate --no-prop > $OUT/write/bench.log 2>&1
