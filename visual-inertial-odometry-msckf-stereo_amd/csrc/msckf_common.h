@@ -212,6 +212,16 @@ __device__ __forceinline__ void mat3_mul(const T* A, const T* B, T* C) {
 // in flight across it (a __syncthreads() emits s_waitcnt vmcnt(0) first, which
 // would drain every prefetch).  Use only where no global data written by
 // another thread is read after the barrier.
+// XCD-aware block index (MI355X_MICROARCH.md, workgroup dispatch: blocks are
+// dealt round-robin over the 8 XCDs, each with its own L2): a bijective remap
+// that gives each XCD a contiguous range of logical blocks, so consecutive
+// blocks (consecutive features of one filter, sharing its P) share an L2.
+// Speed only -- any placement is correct.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+    const int q = nwg >> 3, r = nwg & 7, xcd = orig & 7;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
 #define LDS_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
 
 // Broadcast lane `src` (wave-uniform) of x to the whole wave via v_readlane

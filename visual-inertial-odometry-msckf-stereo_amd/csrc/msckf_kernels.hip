@@ -1188,8 +1188,9 @@ __global__ void __launch_bounds__(256) k_gate_lds(DevState<T> st, Params<T> prm,
 // Layout: the 3M range rows padded to n3 = 4 ceil(3M/4) (padding rows are
 // unit pivots) plus the B row [H_f~^T ; r~^T], as 4x4 tiles (lower triangle,
 // column-major tile order; tile t belongs to lane t % 64, slot t / 64).
-// Y tiles: the wave forms all 3x3 observation-pair blocks
-// Ht_a P_{s_a s_b} Ht_b^T (a >= b) into LDS, then every lane assembles its
+// Y tiles: the wave forms the 3x3 observation-pair blocks
+// Ht_a P_{s_a s_b} Ht_b^T (a >= b) into LDS (in passes over observation
+// columns when the LDS budget is smaller), then every lane assembles its
 // 4x4 tiles of the compact row space from there.
 // Blocked LDL^T, one tile column per step: the diagonal tile's owner factors
 // it, the panel tiles' owners publish W = A L_d^-T by row through LDS, and
@@ -1204,21 +1205,21 @@ template <typename T>
 __host__ __device__ constexpr int gate_blk() { return sizeof(T) == 8 ? 18 : 20; }
 __host__ __device__ constexpr int gate_nt(int M) { return (3 * M + 3) / 4 + 1; }   // tile rows: Y rows + B row
 template <typename T>
-__host__ __device__ constexpr int gate_area_T(int Mmax) {   // Y block staging / panel buffers
-    return 9 * Mmax * (Mmax + 1) / 2 > 2 * gate_blk<T>() * gate_nt(Mmax) ? 9 * Mmax * (Mmax + 1) / 2
-                                                                       : 2 * gate_blk<T>() * gate_nt(Mmax);
+__host__ __device__ constexpr int gate_area_T(int Mmax, int capb) {   // Y block staging / panel buffers
+    return 9 * capb > 2 * gate_blk<T>() * gate_nt(Mmax) ? 9 * capb : 2 * gate_blk<T>() * gate_nt(Mmax);
 }
 template <typename T>
-__host__ __device__ constexpr int gate_wave_lds_T(int Mmax) {
-    return 22 * Mmax + gate_area_T<T>(Mmax);   // Ht rows, [r~ | r_n], staging / panels
+__host__ __device__ constexpr int gate_wave_lds_T(int Mmax, int capb) {
+    return 22 * Mmax + gate_area_T<T>(Mmax, capb);   // Ht rows, [r~ | r_n], staging / panels
 }
 
-template <typename T, int TPL>
+template <typename T, int TPL, bool MP>
 __global__ void __launch_bounds__(256) k_gate_wave(DevState<T> st, Params<T> prm, FeatBatch<T> fb,
-                                                   const int* __restrict__ flist, int nlist, int Mmax, int phases) {
+                                                   const int* __restrict__ flist, int nlist, int Mmax, int capb,
+                                                   int phases) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wpb = blockDim.x >> 6;
-    const int li = blockIdx.x * wpb + wv;
+    const int li = xcd_remap(blockIdx.x, gridDim.x) * wpb + wv;
     if (li >= nlist) return;
     const int f = flist[li];
     if (!fb.valid[f]) {
@@ -1229,14 +1230,14 @@ __global__ void __launch_bounds__(256) k_gate_wave(DevState<T> st, Params<T> prm
     const int o0 = fb.obs_off[f], M = fb.obs_off[f + 1] - o0, M3 = 3 * M;
     const int nY = (M3 + 3) >> 2;               // Y tile rows = elimination steps
     const int nT = nY + 1, ntiles = nT * (nT + 1) / 2;
-    T* ht = reinterpret_cast<T*>(smem_raw) + (size_t)wv * gate_wave_lds_T<T>(Mmax);
+    T* ht = reinterpret_cast<T*>(smem_raw) + (size_t)wv * gate_wave_lds_T<T>(Mmax, capb);
     T* rt = ht + 18 * Mmax;                    // [Mmax][4]: r~ (3), r_n
     T* area = rt + 4 * Mmax;
     constexpr int GB = gate_blk<T>();
-    T* stage = area;                           // [M (M + 1) / 2][9] Y blocks, column-major lower
+    T* stage = area;                           // [capb][9] Y blocks of one pass, column-major lower
     T* wd = area;                              // [nT][GB]  panel rows: raw tile rows, then W D^-1
     T* wt = area + GB * gate_nt(Mmax);         // [nT][GB]  W^T per 4-row block: wt[blk][4 c + y] = W[4 blk + y][c]
-    int* slot = reinterpret_cast<int*>(reinterpret_cast<T*>(smem_raw) + wpb * gate_wave_lds_T<T>(Mmax)) + wv * Mmax;
+    int* slot = reinterpret_cast<int*>(reinterpret_cast<T*>(smem_raw) + wpb * gate_wave_lds_T<T>(Mmax, capb)) + wv * Mmax;
     const T* ws = fb.obs_ws + (size_t)o0 * OBS_WS;
     for (int e = lane; e < 18 * M; e += 64) {
         const int o = e / 18;
@@ -1270,30 +1271,65 @@ __global__ void __launch_bounds__(256) k_gate_wave(DevState<T> st, Params<T> prm
 #define TL(s) (crd[s] >> 16)
 #define OK(s) (crd[s] >= 0)
 
-    // ---- Y: every observation-pair block Ht_a P_ab Ht_b^T (a >= b, 3x3) into
-    // LDS (column-major lower block order, two blocks per lane in flight), then
-    // each lane assembles its tiles from there ----
+    // ---- Y: the observation-pair blocks Ht_a P_ab Ht_b^T (a >= b, 3x3) into
+    // LDS (column-major lower block order), then each lane assembles its tiles
+    // from there.  When the LDS budget holds fewer than all M (M + 1) / 2
+    // blocks (capb), this runs in passes over observation-column ranges that
+    // are multiples of four: columns [c0, c1) <-> tile columns [3 c0 / 4, 3 c1 / 4).
     const T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
     const int ldp = st.Dmax;
     const T s2 = prm.sigma2;
-    const int nbk = M * (M + 1) / 2;
-    if (phases & 1) {
-        for (int k0 = 0; k0 < nbk; k0 += 128) {
-            T Pl[2][36];
-            int oa[2], ob[2];
+    constexpr int BIF = MP ? 1 : 2;   // blocks per lane in flight (multi-pass: the tiles are live meanwhile)
+    T a[TPL][4][4];
+    bool tiles_init = false;
+    auto init_tiles = [&]() {
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int k = k0 + 64 * j + lane;
-                const int kc = k < nbk ? k : 0;
-                const int c = colmajor_col(kc, M);
+        for (int s = 0; s < TPL; ++s) {
+    #pragma unroll
+            for (int x = 0; x < 4; ++x)
+    #pragma unroll
+                for (int y = 0; y < 4; ++y) a[s][x][y] = 0;
+            // B row: [H_f~^T ; r~^T] with H_f~ = -Ht[:, 3:6]
+            if (!OK(s) || TI(s) != nY || TL(s) >= nY) continue;
+    #pragma unroll
+            for (int y = 0; y < 4; ++y) {
+                const int p = 4 * TL(s) + y;
+                if (p >= M3) continue;
+                const int o = p / 3, c = p - 3 * o;
+    #pragma unroll
+                for (int x = 0; x < 3; ++x) a[s][x][y] = -ht[18 * o + 6 * c + 3 + x];
+                a[s][3][y] = rt[4 * o + c];
+            }
+        }
+    };
+    if (MP) { init_tiles(); tiles_init = true; }
+    for (int c0 = 0; c0 < ((phases & 1) ? M : 0);) {
+        int c1 = c0, nbp = 0;
+        while (c1 < M) {
+            const int ce = c1 + 4 < M ? c1 + 4 : M;
+            int grp = 0;
+            for (int c = c1; c < ce; ++c) grp += M - c;
+            if (c1 > c0 && nbp + grp > capb) break;
+            nbp += grp;
+            c1 = ce;
+        }
+        const int kbase = c0 * M - c0 * (c0 - 1) / 2;
+        for (int k0 = 0; k0 < nbp; k0 += 64 * BIF) {
+            T Pl[BIF][36];
+            int oa[BIF], ob[BIF];
+#pragma unroll
+            for (int j = 0; j < BIF; ++j) {
+                const int kk = k0 + 64 * j + lane;
+                const int k = kbase + (kk < nbp ? kk : 0);
+                const int c = colmajor_col(k, M);
                 ob[j] = c;
-                oa[j] = c + kc - (c * M - c * (c - 1) / 2);
+                oa[j] = c + k - (c * M - c * (c - 1) / 2);
                 const T* Pb = P + (size_t)(21 + 6 * slot[oa[j]]) * ldp + 21 + 6 * slot[ob[j]];
                 // each 6-element block row in wide loads (gfx950 takes dword-aligned
                 // multi-dword global loads: dwordx4 + dwordx2 per fp32 row)
 #pragma unroll
                 for (int u = 0; u < 6; ++u) {
-                    if (k < nbk) {
+                    if (kk < nbp) {
                         __builtin_memcpy(Pl[j] + 6 * u, Pb + (size_t)u * ldp, 6 * sizeof(T));
                     } else {
 #pragma unroll
@@ -1302,59 +1338,74 @@ __global__ void __launch_bounds__(256) k_gate_wave(DevState<T> st, Params<T> prm
                 }
             }
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int k = k0 + 64 * j + lane;
-                if (k >= nbk) continue;
+            for (int j = 0; j < BIF; ++j) {
+                const int kk = k0 + 64 * j + lane;
+                if (kk >= nbp) continue;
                 const T* Ha = ht + 18 * oa[j];
                 const T* Hb = ht + 18 * ob[j];
-                T* dst = stage + 9 * k;
+                T* dst = stage + 9 * kk;
+                // packed: column pairs in one v_pk_fma_f32 (not for TPL <= 2, where the extra
+                // VGPRs would cost an occupancy step the LDS does not already cost)
+                if constexpr (sizeof(T) == 4 && TPL >= 3) {
+                    using F2 = float __attribute__((ext_vector_type(2)));
+                    F2 hb01[6];                   // (Hb[0][u], Hb[1][u])
 #pragma unroll
-                for (int x = 0; x < 3; ++x) {
-                    T t1[6];
+                    for (int u = 0; u < 6; ++u) hb01[u] = F2{Hb[u], Hb[6 + u]};
 #pragma unroll
-                    for (int c = 0; c < 6; ++c) {
-                        T acc = 0;
+                    for (int x = 0; x < 3; ++x) {
+                        F2 t2[3] = {F2{0, 0}, F2{0, 0}, F2{0, 0}};   // t1 = Ha[x] P as three column pairs
 #pragma unroll
-                        for (int u = 0; u < 6; ++u) acc += Ha[6 * x + u] * Pl[j][6 * u + c];
-                        t1[c] = acc;
+                        for (int u = 0; u < 6; ++u) {
+                            const float h = Ha[6 * x + u];
+#pragma unroll
+                            for (int c = 0; c < 3; ++c)
+                                t2[c] = __builtin_elementwise_fma(F2{h, h}, F2{Pl[j][6 * u + 2 * c], Pl[j][6 * u + 2 * c + 1]},
+                                                                  t2[c]);
+                        }
+                        const float t1[6] = {t2[0].x, t2[0].y, t2[1].x, t2[1].y, t2[2].x, t2[2].y};
+                        F2 y01 = {0, 0};
+                        float y2 = 0;
+#pragma unroll
+                        for (int u = 0; u < 6; ++u) {
+                            y01 = __builtin_elementwise_fma(F2{t1[u], t1[u]}, hb01[u], y01);
+                            y2 = fmaf(t1[u], Hb[12 + u], y2);
+                        }
+                        dst[3 * x] = y01.x;
+                        dst[3 * x + 1] = y01.y;
+                        dst[3 * x + 2] = y2;
                     }
+                } else {
 #pragma unroll
-                    for (int y = 0; y < 3; ++y) {
-                        T acc = 0;
+                    for (int x = 0; x < 3; ++x) {
+                        T t1[6];
 #pragma unroll
-                        for (int u = 0; u < 6; ++u) acc += t1[u] * Hb[6 * y + u];
-                        dst[3 * x + y] = acc;
+                        for (int c = 0; c < 6; ++c) {
+                            T acc = 0;
+#pragma unroll
+                            for (int u = 0; u < 6; ++u) acc += Ha[6 * x + u] * Pl[j][6 * u + c];
+                            t1[c] = acc;
+                        }
+#pragma unroll
+                        for (int y = 0; y < 3; ++y) {
+                            T acc = 0;
+#pragma unroll
+                            for (int u = 0; u < 6; ++u) acc += t1[u] * Hb[6 * y + u];
+                            dst[3 * x + y] = acc;
+                        }
                     }
                 }
             }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // one wave: its stores are now visible to all lanes
-    }
-    T a[TPL][4][4];
-#pragma unroll
-    for (int s = 0; s < TPL; ++s) {
-#pragma unroll
-        for (int x = 0; x < 4; ++x)
-#pragma unroll
-            for (int y = 0; y < 4; ++y) a[s][x][y] = 0;
-        // B row: [H_f~^T ; r~^T] with H_f~ = -Ht[:, 3:6]
-        if (!OK(s) || TI(s) != nY || TL(s) >= nY) continue;
-#pragma unroll
-        for (int y = 0; y < 4; ++y) {
-            const int p = 4 * TL(s) + y;
-            if (p >= M3) continue;
-            const int o = p / 3, c = p - 3 * o;
-#pragma unroll
-            for (int x = 0; x < 3; ++x) a[s][x][y] = -ht[18 * o + 6 * c + 3 + x];
-            a[s][3][y] = rt[4 * o + c];
-        }
-    }
-
-    if (phases & 1) {
+        if (!MP && !tiles_init) { init_tiles(); tiles_init = true; }   // single pass: tiles born after the blocks
+        const int tl_lo = 3 * c0 / 4, tl_hi = c1 >= M ? nY : 3 * c1 / 4;
 #pragma unroll
         for (int s = 0; s < TPL; ++s) {
-            if (!OK(s) || TI(s) >= nY) continue;
-            const int tl = TL(s), ti = TI(s);
+            if (!OK(s) || tlmax[s] < tl_lo) continue;
+            int cs = crd[s];
+            asm volatile("" : "+v"(cs));   // keep the index arithmetic inside the pass loop (no hoisting)
+            const int tl = cs >> 16, ti = cs & 0xffff;
+            if (tl < tl_lo || tl >= tl_hi || ti >= nY) continue;
             int oq[4], cq[4], op[4], cp[4];
 #pragma unroll
             for (int x = 0; x < 4; ++x) {
@@ -1372,15 +1423,18 @@ __global__ void __launch_bounds__(256) k_gate_wave(DevState<T> st, Params<T> prm
                     if (q < M3 && p < M3) {   // block (max, min) of the pair, column-major lower
                         const int hi = oq[x] >= op[y] ? oq[x] : op[y], lo = oq[x] >= op[y] ? op[y] : oq[x];
                         const int e = oq[x] >= op[y] ? 3 * cq[x] + cp[y] : 3 * cp[y] + cq[x];
-                        v = stage[9 * (lo * M - lo * (lo - 1) / 2 + hi - lo) + e];
+                        v = stage[9 * (lo * M - lo * (lo - 1) / 2 + hi - lo - kbase) + e];
                         if (q == p) v += s2;
                     }
                     a[s][x][y] = v;
                 }
             asm volatile("" ::: "memory");
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads done before the panel buffers reuse the area
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads done before the next pass / the panels reuse the area
+        c0 = c1;
+        if (!MP) break;   // single pass (capb >= M (M + 1) / 2): no back edge, the tiles stay dead in the block loop
     }
+    if (!tiles_init) init_tiles();
 
     // ---- blocked LDL^T over the nY Y tile columns, 4 pivots per step ----
     bool fail = false;
@@ -2189,26 +2243,47 @@ size_t gate_lds_bytes(int maxM) {
            (maxM + 4) * sizeof(int);
 }
 
-template <typename T, int TPL>
-static void launch_gate_wave(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const FeatBatch<T>& fb,
-                             const int* list, int cnt, int Mmax) {
-    // waves (features) per workgroup: 4 unless their LDS would exceed the CU's 160 KB
-    const size_t per_wave = (size_t)gate_wave_lds_T<T>(Mmax) * sizeof(T) + (size_t)Mmax * sizeof(int);
-    const int wpb = 4 * per_wave <= 160 * 1024 ? 4 : (2 * per_wave <= 160 * 1024 ? 2 : 1);
-    const size_t lds = wpb * per_wave;
+template <typename T, int TPL, bool MP>
+static void launch_gate_wave_cfg(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const FeatBatch<T>& fb,
+                                 const int* list, int cnt, int Mmax, int capb, int wpb, size_t lds, int phases) {
     static size_t attr = 64 * 1024;
     if (lds > attr) {
-        (void)hipFuncSetAttribute((const void*)k_gate_wave<T, TPL>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)hipFuncSetAttribute((const void*)k_gate_wave<T, TPL, MP>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)lds);
         attr = lds;
     }
+    hipLaunchKernelGGL((k_gate_wave<T, TPL, MP>), dim3((cnt + wpb - 1) / wpb), dim3(64 * wpb), lds, s, st, prm, fb,
+                       list, cnt, Mmax, capb, phases);
+}
+
+template <typename T, int TPL>
+static void launch_gate_wave(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const FeatBatch<T>& fb,
+                             const int* list, int cnt, int Mmax) {
+    // Y staging capacity: all M (M + 1) / 2 blocks in one pass unless four
+    // waves would then need more than 80 KB (fewer than two workgroups per
+    // CU); then passes of fewer blocks (at least the first group of four
+    // observation columns) sized for 40 KB.  (Measured at 30x200: passes cost
+    // more than the occupancy they buy while two workgroups still fit --
+    // M <= 28: 1.60 ms multi-pass vs 1.40 ms single.)
+    const int nbk = Mmax * (Mmax + 1) / 2, first = 4 * Mmax - 6 > 1 ? 4 * Mmax - 6 : 1;
+    auto per_wave_of = [&](int cb) {
+        return (size_t)gate_wave_lds_T<T>(Mmax, cb) * sizeof(T) + (size_t)Mmax * sizeof(int);
+    };
+    int capb = nbk;
+    if (4 * per_wave_of(capb) > 80 * 1024)
+        for (int parts = 2; 4 * per_wave_of(capb) > 40 * 1024 && capb > first; ++parts)
+            capb = (nbk + parts - 1) / parts > first ? (nbk + parts - 1) / parts : first;
+    // waves (features) per workgroup: 4 unless their LDS would exceed the CU's 160 KB
+    const size_t per_wave = per_wave_of(capb);
+    const int wpb = 4 * per_wave <= 160 * 1024 ? 4 : (2 * per_wave <= 160 * 1024 ? 2 : 1);
+    const size_t lds = wpb * per_wave;
     static int phases = -1;   // MSCKF_GATE_PHASES: profiling aid (bit0 Y tiles, bit2 elimination)
     if (phases < 0) {
         const char* e = getenv("MSCKF_GATE_PHASES");
         phases = e ? atoi(e) : 7;
     }
-    hipLaunchKernelGGL((k_gate_wave<T, TPL>), dim3((cnt + wpb - 1) / wpb), dim3(64 * wpb), lds, s, st, prm, fb, list,
-                       cnt, Mmax, phases);
+    if (capb < nbk) launch_gate_wave_cfg<T, TPL, true>(s, st, prm, fb, list, cnt, Mmax, capb, wpb, lds, phases);
+    else launch_gate_wave_cfg<T, TPL, false>(s, st, prm, fb, list, cnt, Mmax, capb, wpb, lds, phases);
 }
 
 // Features are launched in size classes (by M, listed on the host at load
