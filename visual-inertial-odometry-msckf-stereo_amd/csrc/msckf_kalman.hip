@@ -499,65 +499,131 @@ __global__ void __launch_bounds__(64 * NW) k_kal_c2(DevState<T> st, UpdWs<T> ws)
 }
 
 // ===========================================================================
-// Global-memory fallback of stages A and C for windows whose tiles do not fit
-// in one workgroup's registers (Nmax > 36): the same partial Cholesky, in place
-// on a row-major workspace, one column per step (k_chol's scheme).  Rows
-// < ncol form the square (lower) part; rows >= ncol are extra rows with ncol
-// columns.  Correct at any size, not fast.
+// Stages A and C for windows whose tiles do not fit in one workgroup's
+// registers (Nmax > 36): the same partial Cholesky, in place on a row-major
+// global workspace (rows < ncol: the square lower part; rows >= ncol: extra
+// rows with ncol columns), right-looking and blocked by GNB = 16 pivots.  Each
+// panel step is three launches over all filters: factor the 16 x 16 diagonal
+// block (one wave per filter), the panel rows below it (one row per thread,
+// many workgroups per filter), and the trailing update A -= W W^T on the
+// matrix cores (64 x 64 fp64 MFMA tiles, gemm64 below).  The trailing matrix
+// makes one round trip per 16 pivots instead of one per pivot.
 // ===========================================================================
-__device__ bool gchol_core(KT* A, int ld, int nrow, int ncol, int nelim) {
-    const int tid = threadIdx.x, nt = blockDim.x;
-    __shared__ int s_bad;
-    if (tid == 0) s_bad = 0;
-    __syncthreads();
-    for (int j = 0; j < nelim; ++j) {
-        if (tid == 0) {
-            const KT d = A[(size_t)j * ld + j];
-            if (!(d > 0)) s_bad = 1;
-            A[(size_t)j * ld + j] = sqrt(d > 0 ? d : KT(1));
-        }
-        __syncthreads();
-        if (s_bad) return false;
-        const KT inv = KT(1) / A[(size_t)j * ld + j];
-        for (int i = j + 1 + tid; i < nrow; i += nt) A[(size_t)i * ld + j] *= inv;
-        __syncthreads();
-        // trailing update: rows i > j, columns l in (j, min(i, ncol - 1)]; thread grid 16 columns wide
-        const int lw = ncol - j - 1;
-        if (lw > 0) {
-            for (int i = j + 1 + tid / 16; i < nrow; i += nt / 16) {
-                const KT aij = A[(size_t)i * ld + j];
-                const int lmax = i < ncol ? i : ncol - 1;
-                for (int l = j + 1 + (tid & 15); l <= lmax; l += 16) A[(size_t)i * ld + l] -= aij * A[(size_t)l * ld + j];
-            }
-        }
-        __syncthreads();
-    }
+constexpr int GNB = 16;
+
+// stage 0 = A: [P_cc P_ci; P_ic P_ii] (N = C + 21 square, C pivots);
+// stage 1 = C: T (C square) with the extra rows [Vc_i (21); Lc (C); c^T]
+template <int STAGE, typename T>
+__device__ __forceinline__ bool gdims(const DevState<T>& st, const UpdWs<T>& ws, int b, KT*& A, int& nrow,
+                                      int& ncol, int& nelim) {
+    if (ws.info[4 * b] == 0 || ws.info[4 * b + 3] < 0) return false;
+    const int C = 6 * st.ncams[b];
+    A = ws.Wk + (size_t)b * ws.wk_stride;
+    if (STAGE == 0) { nrow = C + 21; ncol = C + 21; }
+    else { nrow = C + 22 + C; ncol = C; }
+    nelim = C;
     return true;
 }
 
-// stage A: workspace [C + 21][C + 21], index space [cams (C) | IMU (21)]
-template <typename T>
-__global__ void __launch_bounds__(256) k_kal_ga(DevState<T> st, UpdWs<T> ws) {
+// 1. factor the diagonal block A[k:k+nb, k:k+nb] in place (one wave per filter)
+template <int STAGE, typename T>
+__global__ void __launch_bounds__(64) k_gchol_diag(DevState<T> st, UpdWs<T> ws, int k) {
     const int b = blockIdx.x;
-    if (ws.info[4 * b] == 0) return;
-    const int C = 6 * st.ncams[b], N = C + 21, Cpw = ws.Cp;
-    KT* A = ws.Wk + (size_t)b * ws.wk_stride;
+    KT* A;
+    int nrow, ncol, nelim;
+    if (!gdims<STAGE>(st, ws, b, A, nrow, ncol, nelim) || k >= nelim) return;
+    const int ld = ncol, nb = nelim - k < GNB ? nelim - k : GNB;
+    __shared__ double d[GNB][GNB + 1];
+    const int lane = threadIdx.x;
+    for (int e = lane; e < nb * nb; e += 64) {
+        const int i = e / nb, j = e - i * nb;
+        d[i][j] = j <= i ? A[(size_t)(k + i) * ld + k + j] : 0.0;
+    }
+    __syncthreads();
+    bool bad = false;
+    for (int j = 0; j < nb; ++j) {   // right-looking, lane i owns row i
+        const double piv = d[j][j];
+        if (!(piv > 0.0)) { bad = true; break; }
+        const double l = sqrt(piv), inv = 1.0 / l;
+        __syncthreads();
+        if (lane == j) d[j][j] = l;
+        if (lane > j && lane < nb) d[lane][j] *= inv;
+        __syncthreads();
+        if (lane > j && lane < nb) {
+            const double lij = d[lane][j];
+            for (int c = j + 1; c <= lane; ++c) d[lane][c] -= lij * d[c][j];
+        }
+        __syncthreads();
+    }
+    if (bad) {
+        if (lane == 0) ws.info[4 * b + 3] = -1;
+        return;
+    }
+    for (int e = lane; e < nb * nb; e += 64) {
+        const int i = e / nb, j = e - i * nb;
+        if (j <= i) A[(size_t)(k + i) * ld + k + j] = d[i][j];
+    }
+}
+
+// 2. panel rows i >= k + nb: A[i, k:k+nb] <- A[i, k:k+nb] L_kk^-T (one row per thread)
+template <int STAGE, typename T>
+__global__ void __launch_bounds__(256) k_gchol_trsm(DevState<T> st, UpdWs<T> ws, int k) {
+    const int b = blockIdx.y;
+    KT* A;
+    int nrow, ncol, nelim;
+    if (!gdims<STAGE>(st, ws, b, A, nrow, ncol, nelim) || k >= nelim) return;
+    const int ld = ncol, nb = nelim - k < GNB ? nelim - k : GNB;
+    const int i = k + nb + blockIdx.x * 256 + threadIdx.x;
+    if (k + nb + blockIdx.x * 256 >= nrow) return;
+    __shared__ double L[GNB][GNB + 1];
+    for (int e = threadIdx.x; e < nb * nb; e += 256) {
+        const int r = e / nb, c = e - r * nb;
+        L[r][c] = c <= r ? A[(size_t)(k + r) * ld + k + c] : 0.0;
+    }
+    __syncthreads();
+    if (i >= nrow) return;
+    KT* row = A + (size_t)i * ld + k;
+    double x[GNB];
+#pragma unroll
+    for (int j = 0; j < GNB; ++j) {
+        double v = j < nb ? row[j] : 0.0;
+#pragma unroll
+        for (int p = 0; p < j; ++p) v -= x[p] * L[j][p];
+        x[j] = j < nb ? v / L[j][j] : 0.0;
+    }
+#pragma unroll
+    for (int j = 0; j < GNB; ++j)
+        if (j < nb) row[j] = x[j];
+}
+
+// stage A workspace in / out (grid-stride over the N x N lower part, blockIdx.y = filter)
+template <typename T>
+__global__ void __launch_bounds__(256) k_gchol_a_load(DevState<T> st, UpdWs<T> ws) {
+    const int b = blockIdx.y;
+    KT* A;
+    int N, ncol, nelim;
+    if (!gdims<0>(st, ws, b, A, N, ncol, nelim)) return;
+    const int C = nelim;
     const T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
     const int ld = st.Dmax;
     auto map = [&](int i) { return i < C ? 21 + i : i - C; };
-    for (int e = threadIdx.x; e < N * N; e += blockDim.x) {
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < N * N; e += gridDim.x * 256) {
         const int i = e / N, j = e - i * N;
         if (j <= i) A[(size_t)i * N + j] = (KT)P[(size_t)map(i) * ld + map(j)];
     }
-    __syncthreads();
-    if (!gchol_core(A, N, N, N, C)) {
-        if (threadIdx.x == 0) ws.info[4 * b + 3] = -1;
-        return;
-    }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_gchol_a_store(DevState<T> st, UpdWs<T> ws) {
+    const int b = blockIdx.y;
+    KT* A;
+    int N, ncol, nelim;
+    if (!gdims<0>(st, ws, b, A, N, ncol, nelim)) return;
+    const int C = nelim, Cpw = ws.Cp;
     KT* Lc = ws.Lc + (size_t)b * Cpw * Cpw;
     KT* Vi = ws.Vi + (size_t)b * KW * Cpw;
     KT* Sii = ws.Sii + (size_t)b * KW * KW;
-    for (int e = threadIdx.x; e < N * N; e += blockDim.x) {
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < N * N; e += gridDim.x * 256) {
         const int i = e / N, j = e - i * N;
         if (j > i) continue;
         const KT v = A[(size_t)i * N + j];
@@ -567,17 +633,18 @@ __global__ void __launch_bounds__(256) k_kal_ga(DevState<T> st, UpdWs<T> ws) {
     }
 }
 
-// stage C: workspace [C + E][C]: T (lower) then the extra rows [Vc_i (21); Lc (C); c^T]
+// stage C workspace [C + E][C]: T (lower) then the extra rows [Vc_i (21); Lc (C); c^T]
 template <typename T>
-__global__ void __launch_bounds__(256) k_kal_gc(DevState<T> st, UpdWs<T> ws) {
-    const int b = blockIdx.x;
-    if (ws.info[4 * b] == 0 || ws.info[4 * b + 3] < 0) return;
-    const int C = 6 * st.ncams[b], E = 21 + C + 1, Cpw = ws.Cp, ldt = ws.Cmax + 1;
-    KT* A = ws.Wk + (size_t)b * ws.wk_stride;
+__global__ void __launch_bounds__(256) k_gchol_c_load(DevState<T> st, UpdWs<T> ws) {
+    const int b = blockIdx.y;
+    KT* A;
+    int nrow, C, nelim;
+    if (!gdims<1>(st, ws, b, A, nrow, C, nelim)) return;
+    const int Cpw = ws.Cp, ldt = ws.Cmax + 1;
     const KT* Tm = ws.Tm + (size_t)b * ws.Cmax * ldt;
     const KT* Lc = ws.Lc + (size_t)b * Cpw * Cpw;
     const KT* Vi = ws.Vi + (size_t)b * KW * Cpw;
-    for (int e = threadIdx.x; e < (C + E) * C; e += blockDim.x) {
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < nrow * C; e += gridDim.x * 256) {
         const int i = e / C, j = e - i * C;
         KT v = 0;
         if (i < C) v = j <= i ? Tm[(size_t)i * ldt + j] : KT(0);
@@ -589,17 +656,26 @@ __global__ void __launch_bounds__(256) k_kal_gc(DevState<T> st, UpdWs<T> ws) {
         }
         A[(size_t)i * C + j] = v;
     }
-    __syncthreads();
-    if (!gchol_core(A, C, C + E, C, C)) {
-        if (threadIdx.x == 0) ws.info[4 * b + 3] = -1;
-        return;
-    }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_gchol_c_store(DevState<T> st, UpdWs<T> ws) {
+    const int b = blockIdx.y;
+    KT* A;
+    int nrow, C, nelim;
+    if (!gdims<1>(st, ws, b, A, nrow, C, nelim)) return;
+    const int E = nrow - C, Cpw = ws.Cp;
     KT* W = ws.W + (size_t)b * (st.Dmax + 1) * Cpw;
-    for (int e = threadIdx.x; e < E * C; e += blockDim.x) {
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < E * C; e += gridDim.x * 256) {
         const int x = e / C, j = e - x * C;
         W[(size_t)x * Cpw + j] = A[(size_t)(C + x) * C + j];
     }
 }
+
+// 3. trailing update A[i][j] -= sum_p W[i][p] W[j][p], p in [k, k+nb), for the
+// lower part j <= i, j in [k+nb, ncol), i in [k+nb, nrow): 64 x 64 MFMA tiles
+template <int STAGE, typename T>
+__global__ void __launch_bounds__(256) k_gchol_update(DevState<T> st, UpdWs<T> ws, int k);
 
 size_t kalman_global_ws_doubles(int Cmax) {   // per filter, 0 when the register-tile stages fit
     if (kalman_chol_supported(Cmax)) return 0;
@@ -668,6 +744,23 @@ __device__ __forceinline__ void gemm64(int m, int n, int kb, int ke, int i0, int
                 const int i = i0 + 32 * wr + 16 * mi + lr + 4 * r, j = j0 + 32 * wc + 16 * ni + lc;
                 if (i < m && j < n) store(i, j, acc[mi][ni][r]);
             }
+}
+
+template <int STAGE, typename T>
+__global__ void __launch_bounds__(256) k_gchol_update(DevState<T> st, UpdWs<T> ws, int k) {
+    const int b = blockIdx.z;
+    KT* A;
+    int nrow, ncol, nelim;
+    if (!gdims<STAGE>(st, ws, b, A, nrow, ncol, nelim) || k >= nelim) return;
+    const int ld = ncol, k1 = k + (nelim - k < GNB ? nelim - k : GNB);
+    const int i0 = k1 + blockIdx.y * GT, j0 = k1 + blockIdx.x * GT;
+    if (i0 >= nrow || j0 >= ncol || i0 + GT - 1 < j0) return;   // outside, or entirely above the diagonal
+    gemm64<true, true>(nrow, ncol, k, k1, i0, j0,
+                       [&](int i, int p) { return A[(size_t)i * ld + p]; },
+                       [&](int p, int j) { return A[(size_t)j * ld + p]; },
+                       [&](int i, int j, double v) {
+                           if (j <= i) A[(size_t)i * ld + j] -= v;
+                       });
 }
 
 // ---- stage B1: G = A Lc (C x C) ----
@@ -1052,6 +1145,28 @@ static bool pick_mfma(int tiles, MfmaCfg& c) {
     return false;
 }
 
+
+// Host side of the blocked global-memory factorisation (large windows).
+template <int STAGE, typename T>
+static void launch_gchol(hipStream_t s, const DevState<T>& st, const UpdWs<T>& ws) {
+    const int Cmax = ws.Cmax;
+    const int nrow = STAGE == 0 ? Cmax + 21 : 2 * Cmax + 22, ncol = STAGE == 0 ? Cmax + 21 : Cmax;
+    const int ld_chunks = (nrow * ncol + 256 * 64 - 1) / (256 * 64);
+    if (STAGE == 0) hipLaunchKernelGGL(k_gchol_a_load<T>, dim3(ld_chunks, st.B), dim3(256), 0, s, st, ws);
+    else hipLaunchKernelGGL(k_gchol_c_load<T>, dim3(ld_chunks, st.B), dim3(256), 0, s, st, ws);
+    for (int k = 0; k < Cmax; k += GNB) {
+        hipLaunchKernelGGL((k_gchol_diag<STAGE, T>), dim3(st.B), dim3(64), 0, s, st, ws, k);
+        const int rows = nrow - k - GNB;
+        if (rows > 0)
+            hipLaunchKernelGGL((k_gchol_trsm<STAGE, T>), dim3((rows + 255) / 256, st.B), dim3(256), 0, s, st, ws, k);
+        const int ti = (rows + GT - 1) / GT, tj = (ncol - k - GNB + GT - 1) / GT;
+        if (rows > 0 && tj > 0)
+            hipLaunchKernelGGL((k_gchol_update<STAGE, T>), dim3(tj, ti, st.B), dim3(256), 0, s, st, ws, k);
+    }
+    if (STAGE == 0) hipLaunchKernelGGL(k_gchol_a_store<T>, dim3(ld_chunks, st.B), dim3(256), 0, s, st, ws);
+    else hipLaunchKernelGGL(k_gchol_c_store<T>, dim3(ld_chunks, st.B), dim3(256), 0, s, st, ws);
+}
+
 static bool mfma_kalman(int Cmax) {
     static int mode = -1;   // MSCKF_KALMAN_TILE=16 selects the experimental MFMA tiles (A/B runs)
     if (mode < 0) {
@@ -1150,7 +1265,7 @@ void launch_kalman_chol(hipStream_t s, const DevState<T>& st, const Params<T>& p
     const int Cq = (Cmax + 15) & ~15;
     if (glob) {
         kt->begin(s, "kalman_a");
-        hipLaunchKernelGGL(k_kal_ga<T>, dim3(st.B), dim3(256), 0, s, st, ws);
+        launch_gchol<0, T>(s, st, ws);
         kt->end(s);
     } else if (mf) {   // stage A, MFMA tiles
         const int nrow = (Cq + 32) / 16;
@@ -1189,7 +1304,7 @@ void launch_kalman_chol(hipStream_t s, const DevState<T>& st, const Params<T>& p
     const bool split = csplit && !glob && !mf && Cq <= 16 * 12;
     if (glob) {
         kt->begin(s, "kalman_c");
-        hipLaunchKernelGGL(k_kal_gc<T>, dim3(st.B), dim3(256), 0, s, st, ws);
+        launch_gchol<1, T>(s, st, ws);
         kt->end(s);
     } else if (split) {
         const int nTc = Cp / 4;

@@ -1585,29 +1585,79 @@ __global__ void __launch_bounds__(NT) k_gate_big(DevState<T> st, Params<T> prm, 
     const T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
     const int ldp = st.Dmax;
     const double s2 = (double)prm.sigma2;
-    auto load = [&](int i, int j) -> double {
-        if (i < j) { const int t = i; i = j; j = t; }
-        if (i >= n3) {   // B row [H_f~^T ; r~^T], zero corner
-            if (j >= n3 || j >= M3) return 0.0;
-            const int x = i - n3, o = j / 3, c = j - 3 * o;
-            return x < 3 ? -ht[18 * o + 6 * c + 3 + x] : rr[4 * o + c];
+    // whole-tile loader: a 4x4 tile of the compact rows spans at most two
+    // observations each way; every P block (row obs, col obs) it needs is read
+    // once (6 rows of 6, wide loads) and shared by the tile's entries
+    auto load = [&](int i0, int j0, double (&t)[4][4]) {
+        if (i0 >= n3) {   // B row [H_f~^T ; r~^T] (zero corner tile)
+            if (j0 >= n3) return;
+#pragma unroll
+            for (int y = 0; y < 4; ++y) {
+                const int j = j0 + y;
+                if (j >= M3) continue;
+                const int o = j / 3, c = j - 3 * o;
+#pragma unroll
+                for (int x = 0; x < 3; ++x) t[x][y] = -ht[18 * o + 6 * c + 3 + x];
+                t[3][y] = rr[4 * o + c];
+            }
+            return;
         }
-        if (i >= M3 || j >= M3) return i == j ? 1.0 : 0.0;   // padding rows: unit pivots
-        const int oi = i / 3, oj = j / 3;
-        const double* hi = ht + 18 * oi + 6 * (i - 3 * oi);
-        const double* hj = ht + 18 * oj + 6 * (j - 3 * oj);
-        const T* Pb = P + (size_t)(21 + 6 * slot[oi]) * ldp + 21 + 6 * slot[oj];
-        double y = i == j ? s2 : 0.0;
-        for (int u = 0; u < 6; ++u) {
-            double t = 0;
-            for (int v = 0; v < 6; ++v) t += (double)Pb[(size_t)u * ldp + v] * hj[v];
-            y += hi[u] * t;
-        }
-        return y;
+        const int oa0 = i0 / 3, ob0 = j0 / 3;
+#pragma unroll
+        for (int da = 0; da < 2; ++da)
+#pragma unroll
+            for (int db = 0; db < 2; ++db) {
+                const int oa = oa0 + da, ob = ob0 + db;
+                if (oa >= M || ob >= M) continue;
+                // rows x of the tile on observation oa, columns y on ob
+                int xs = 0, ys = 0;
+#pragma unroll
+                for (int x = 0; x < 4; ++x) xs |= ((i0 + x) / 3 == oa && i0 + x < M3) << x;
+#pragma unroll
+                for (int y = 0; y < 4; ++y) ys |= ((j0 + y) / 3 == ob && j0 + y < M3) << y;
+                if (!xs || !ys) continue;
+                const T* Pb = P + (size_t)(21 + 6 * slot[oa]) * ldp + 21 + 6 * slot[ob];
+                double t1[4][6];
+#pragma unroll
+                for (int x = 0; x < 4; ++x)
+#pragma unroll
+                    for (int v = 0; v < 6; ++v) t1[x][v] = 0.0;
+#pragma unroll
+                for (int u = 0; u < 6; ++u) {
+                    T prow[6];
+                    __builtin_memcpy(prow, Pb + (size_t)u * ldp, 6 * sizeof(T));
+#pragma unroll
+                    for (int x = 0; x < 4; ++x) {
+                        if (!((xs >> x) & 1)) continue;
+                        const double h = ht[18 * oa + 6 * (i0 + x - 3 * oa) + u];
+#pragma unroll
+                        for (int v = 0; v < 6; ++v) t1[x][v] += h * (double)prow[v];
+                    }
+                }
+#pragma unroll
+                for (int x = 0; x < 4; ++x) {
+                    if (!((xs >> x) & 1)) continue;
+#pragma unroll
+                    for (int y = 0; y < 4; ++y) {
+                        if (!((ys >> y) & 1)) continue;
+                        const double* hj = ht + 18 * ob + 6 * (j0 + y - 3 * ob);
+                        double acc = 0.0;
+#pragma unroll
+                        for (int v = 0; v < 6; ++v) acc += t1[x][v] * hj[v];
+                        t[x][y] = acc;
+                    }
+                }
+            }
+#pragma unroll
+        for (int x = 0; x < 4; ++x)   // s2 on the diagonal, unit pivots on the padding rows
+#pragma unroll
+            for (int y = 0; y < 4; ++y)
+                if (i0 + x == j0 + y) t[x][y] += i0 + x < M3 ? s2 : 1.0;
     };
     auto panel = [](int, int, double, double, double, double) {};
     auto trail = [&](int i, int j, double v) { corner[(i - n3) * 4 + (j - n3)] = v; };
-    const bool ok = rchol_core<NT, TPL>(nrow, nrow, nrow - 1, lds, load, panel, trail);
+    const bool ok = rchol_core<NT, TPL, decltype(load), decltype(panel), decltype(trail), true>(nrow, nrow, nrow - 1,
+                                                                                              lds, load, panel, trail);
     __syncthreads();
     if (threadIdx.x == 0) {
         double rsum = 0;

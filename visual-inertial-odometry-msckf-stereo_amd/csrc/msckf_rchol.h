@@ -23,7 +23,9 @@ namespace msckf {
 // ===========================================================================
 constexpr int RB = 18;   // doubles per 4-row block of the LDS column buffer
 
-template <int NT, int TPL, class Load, class Panel, class Trail>
+// TILE_LOAD: load(i0, j0, tile) fills a whole 4x4 tile (rows i0.., cols j0..)
+// instead of being called per element (lets a loader share operands).
+template <int NT, int TPL, class Load, class Panel, class Trail, bool TILE_LOAD = false>
 __device__ __forceinline__ bool rchol_core(int nrow, int ncol, int nelim, double* lds, Load load, Panel panel,
                                            Trail trail) {
     const int tid = threadIdx.x;
@@ -45,10 +47,18 @@ __device__ __forceinline__ bool rchol_core(int nrow, int ncol, int nelim, double
 #pragma unroll
     for (int s = 0; s < TPL; ++s) {
         const int i0 = 4 * RTI(s), j0 = 4 * RTL(s);
+        if constexpr (TILE_LOAD) {
 #pragma unroll
-        for (int x = 0; x < 4; ++x)
+            for (int x = 0; x < 4; ++x)
 #pragma unroll
-            for (int y = 0; y < 4; ++y) a[s][x][y] = ROK(s) ? load(i0 + x, j0 + y) : 0.0;
+                for (int y = 0; y < 4; ++y) a[s][x][y] = 0.0;
+            if (ROK(s)) load(i0, j0, a[s]);
+        } else {
+#pragma unroll
+            for (int x = 0; x < 4; ++x)
+#pragma unroll
+                for (int y = 0; y < 4; ++y) a[s][x][y] = ROK(s) ? load(i0 + x, j0 + y) : 0.0;
+        }
     }
     bool fail = false;
     for (int tj = 0; tj < nelim; ++tj) {
