@@ -129,30 +129,51 @@ def pmc_traffic(stage, dtype, workload):
     return summ.get("stages", {}).get(stage, {}).get("bytes_per_step")
 
 
-def cpu_baseline(args, probs):
-    """Oracle (numpy restatement of the reference, 1 BLAS thread) on a bounded
-    sample of the same workload."""
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
+def _oracle_worker(payload):
+    """One CPU worker of the all-cores baseline: oracle updates on 1 BLAS
+    thread for about ``seconds``; returns (updates, elapsed)."""
+    probs, seconds, tests_dir = payload
+    sys.path.insert(0, tests_dir)
     from helpers import problem_to_dict, oracle_update
     try:
         from threadpoolctl import threadpool_limits
-        lim = threadpool_limits(1)
+        threadpool_limits(1)
     except Exception:
-        lim = None
-    done, t0 = 0, time.perf_counter()
+        pass
     oracle_update(problem_to_dict(probs[0]))          # warm-up
-    t0 = time.perf_counter()
+    done, t0 = 0, time.perf_counter()
     while True:
         oracle_update(problem_to_dict(probs[done % len(probs)]))
         done += 1
         el = time.perf_counter() - t0
-        if el > args.cpu_seconds or done >= 20:
-            break
-    if lim is not None:
-        lim.unregister() if hasattr(lim, "unregister") else None
-    return {"value": done / el, "unit": "updates/s", "cores": 1, "kind": "port",
-            "sample": "%d synthetic %dx%d updates (triangulation + jacobian + gating + QR + Kalman as in the reference), "
-                      "numpy/OpenBLAS 1 thread, oracle/msckf_oracle.py" % (done, args.N, args.F)}
+        if el > seconds:
+            return done, el
+
+
+def cpu_baseline(args, probs):
+    """Oracle (numpy restatement of the reference) on a bounded sample of the
+    same workload: 1 BLAS thread in this process, and -- SURVEY.md 8(d) asks
+    for both -- one single-threaded worker per host core of this job's CPU
+    share (forked before this process touches the GPU)."""
+    tests_dir = os.path.join(ROOT, "tests")
+    done, el = _oracle_worker((probs, args.cpu_seconds, tests_dir))
+    out = {"value": done / el, "unit": "updates/s", "cores": 1, "kind": "port",
+           "sample": "%d synthetic %dx%d updates (triangulation + jacobian + gating + QR + Kalman as in the reference), "
+                     "numpy/OpenBLAS 1 thread, oracle/msckf_oracle.py" % (done, args.N, args.F)}
+    try:
+        ncpu = len(os.sched_getaffinity(0))
+    except Exception:
+        ncpu = os.cpu_count() or 1
+    workers = max(1, min(16, ncpu))
+    if workers > 1 and args.cpu_seconds > 0:
+        import multiprocessing as mp
+        with mp.get_context("fork").Pool(workers) as pool:
+            res = pool.map(_oracle_worker, [(probs[w % len(probs):] + probs[:w % len(probs)],
+                                             args.cpu_seconds / 2, tests_dir) for w in range(workers)])
+        out["all_cores"] = {"value": sum(d for d, _ in res) / max(e for _, e in res), "unit": "updates/s",
+                            "cores": workers, "sample": "%d updates over %d single-threaded worker processes"
+                                                        % (sum(d for d, _ in res), workers)}
+    return out
 
 
 def propagation_leg(ctx, args, n_samples=10, steps=5):
@@ -221,6 +242,10 @@ def main():
     args = parse()
     grp = replicas.init("nccl")      # replicas only: RCCL carries the barriers and the max of the timing
     world, rank = grp.world, grp.rank
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:   # before this process initialises the GPU
+        cpu = cpu_baseline(args, [synth.make_update_problem(args.N, args.F, seed=sd)
+                                  for sd in replicas.problem_seeds(rank, min(args.unique, 4))])
     ctx, probs = build_batch(args, rank, grp.local_rank)
     barrier = grp.barrier
 
@@ -276,8 +301,8 @@ def main():
         "kernel_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in sorted(times.items(), key=lambda kv: -kv[1][0])},
         "canonical_gflop_per_update": round(fl["canonical"] / args.batch / 1e9, 4),
     }
-    if rank == 0 and world == 1 and not args.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(args, probs)
+    if cpu is not None:
+        out["cpu_baseline"] = cpu
     if not args.no_prop:
         out["propagation"] = propagation_leg(ctx, args)
     if rank == 0 and not args.no_ate:
