@@ -26,101 +26,116 @@
 namespace msckf {
 
 // ===========================================================================
-// IMU propagation: one 256-thread workgroup per listed filter (batched over
-// filters: workgroup w propagates filters[w] with samples
-// [smp_off[w], smp_off[w+1])), the samples of the frame applied in order.  The 21x21 recursion lives in LDS; the IMU x cam
-// cross block is updated once with the product Phi_n...Phi_1 (the per-sample
-// full-P symmetrisation of msckf.py:362-363 is a no-op on the cam x cam
-// block and only re-rounds the cross block).
+// IMU propagation (process_model, msckf.py:291-368; jit_utils.py:6-135): one
+// wavefront per listed filter, four filters per 256-thread workgroup, no
+// workgroup barriers.  Filter filters[w] takes samples [smp_off[w],
+// smp_off[w+1]) in order.  The 21x21 recursion lives in the wave's LDS
+// (products: 7 outputs per lane); lane 0 runs the serial state prediction
+// (RK4, quirk Q1) and the Phi edits.  The IMU x cam cross block is updated
+// once with the product Phi_n ... Phi_1 (the per-sample full-P symmetrisation
+// of msckf.py:362-363 is a no-op on the cam x cam block and only re-rounds
+// the cross block).
 // ===========================================================================
 template <typename T>
-__device__ void mm21(const T* A, const T* B, T* C, int tid) {   // C = A B (21x21)
-    for (int e = tid; e < 441; e += blockDim.x) {
-        int i = e / 21, j = e % 21;
+__device__ __forceinline__ void mm21w(const T* A, const T* B, T* C, int lane) {   // C = A B (21x21), one wave
+    for (int e = lane; e < 441; e += 64) {
+        const int i = e / 21, j = e - 21 * (e / 21);
         T s = 0;
+#pragma unroll 7
         for (int k = 0; k < 21; ++k) s += A[i * 21 + k] * B[k * 21 + j];
         C[e] = s;
     }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
 template <typename T>
-__global__ void __launch_bounds__(256) k_propagate(DevState<T> st, Params<T> prm,
+__device__ __forceinline__ T skew_el(const T* w, int r, int c) {   // [w]x[r][c]
+    return r == c ? T(0)
+                  : (r == 0 ? (c == 1 ? -w[2] : w[1]) : (r == 1 ? (c == 0 ? w[2] : -w[0]) : (c == 0 ? -w[1] : w[0])));
+}
+
+constexpr int PROP_LDS = 7 * 441 + 2 * 252 + 9 + 3 + 3 + 1 + IMU_STRIDE;   // T per wave
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_propagate(DevState<T> st, Params<T> prm, int nfilt,
                                                    const int* __restrict__ filters,
                                                    const int* __restrict__ smp_off,
                                                    const T* __restrict__ samples_all) {
-    __shared__ T F[441], Phi[441], Fdt2[441], Fdt3[441], A[441], Bm[441], P11[441], PhiT[441];
-    __shared__ T G[21 * 12], PG[21 * 12];
-    __shared__ T s_R[9], s_gyro[3], s_acc[3], s_dt;
-    __shared__ T s_imu[IMU_STRIDE];
-    const int tid = threadIdx.x;
-    const int b = filters[blockIdx.x];
-    const int n = smp_off[blockIdx.x + 1] - smp_off[blockIdx.x];
-    const T* samples = samples_all + 7 * (size_t)smp_off[blockIdx.x];
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int w = blockIdx.x * 4 + wv;
+    if (w >= nfilt) return;
+    const int b = filters[w];
+    const int n = smp_off[w + 1] - smp_off[w];
+    const T* samples = samples_all + 7 * (size_t)smp_off[w];
     if (n <= 0) return;
+    T* F = reinterpret_cast<T*>(smem_raw) + (size_t)wv * PROP_LDS;   // Fdt
+    T* Phi = F + 441;
+    T* Fdt2 = Phi + 441;
+    T* Fdt3 = Fdt2 + 441;
+    T* A = Fdt3 + 441;
+    T* P11 = A + 441;
+    T* PhiT = P11 + 441;                 // cumulative Phi
+    T* G = PhiT + 441;                   // 21 x 12
+    T* PG = G + 252;
+    T* s_R = PG + 252;
+    T* s_gyro = s_R + 9;
+    T* s_acc = s_gyro + 3;
+    T* s_dt = s_acc + 3;
+    T* s_imu = s_dt + 1;
     T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
     const int ld = st.Dmax;
     T* imu = st.imu + (size_t)b * IMU_STRIDE;
     const int D = 21 + 6 * st.ncams[b];
-    for (int e = tid; e < IMU_STRIDE; e += blockDim.x) s_imu[e] = imu[e];
-    for (int e = tid; e < 441; e += blockDim.x) {
+    for (int e = lane; e < IMU_STRIDE; e += 64) s_imu[e] = imu[e];
+    for (int e = lane; e < 441; e += 64) {
         P11[e] = P[(e / 21) * ld + e % 21];
         PhiT[e] = (e / 21 == e % 21) ? T(1) : T(0);
     }
-    __syncthreads();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     for (int k = 0; k < n; ++k) {
         const T* smp = samples + 7 * k;
-        if (tid == 0) {
-            s_dt = smp[0];
+        if (lane == 0) {
+            s_dt[0] = smp[0];
             for (int i = 0; i < 3; ++i) {
                 s_gyro[i] = smp[1 + i] - s_imu[I_BG + i];
                 s_acc[i] = smp[4 + i] - s_imu[I_BA + i];
             }
             quat_to_rot(s_imu + I_Q, s_R);
         }
-        __syncthreads();
-        const T dt = s_dt;
-        // F, G  (jit_utils.py:25-34); R = R_w_i
-        for (int e = tid; e < 441; e += blockDim.x) {
-            int i = e / 21, j = e % 21;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const T dt = s_dt[0];
+        // F dt, G  (jit_utils.py:25-34); R = R_w_i
+        for (int e = lane; e < 441; e += 64) {
+            const int i = e / 21, j = e - 21 * (e / 21);
+            const int bi = i / 3, bj = j / 3, r = i - 3 * bi, c = j - 3 * bj;
             T f = 0;
-            if (i < 3 && j < 3) {   // -skew(gyro)
-                const T* w = s_gyro;
-                T sk[9] = {0, -w[2], w[1], w[2], 0, -w[0], -w[1], w[0], 0};
-                f = -sk[3 * i + j];
-            } else if (i < 3 && j >= 3 && j < 6) {
-                f = (i == j - 3) ? T(-1) : T(0);
-            } else if (i >= 6 && i < 9 && j < 3) {   // -R^T skew(acc)
-                const T* a = s_acc;
-                T sk[9] = {0, -a[2], a[1], a[2], 0, -a[0], -a[1], a[0], 0};
-                int r = i - 6;
-                f = -s_R[r] * sk[j] + -s_R[3 + r] * sk[3 + j] + -s_R[6 + r] * sk[6 + j];
-            } else if (i >= 6 && i < 9 && j >= 9 && j < 12) {
-                f = -s_R[3 * (j - 9) + (i - 6)];
-            } else if (i >= 12 && i < 15 && j >= 6 && j < 9) {
-                f = (i - 12 == j - 6) ? T(1) : T(0);
-            }
-            F[e] = f * dt;   // Fdt
+            if (bi == 0 && bj == 0) f = -skew_el(s_gyro, r, c);
+            else if (bi == 0 && bj == 1) f = r == c ? T(-1) : T(0);
+            else if (bi == 2 && bj == 0)   // -R^T [a]x
+                f = -s_R[r] * skew_el(s_acc, 0, c) + -s_R[3 + r] * skew_el(s_acc, 1, c) + -s_R[6 + r] * skew_el(s_acc, 2, c);
+            else if (bi == 2 && bj == 3) f = -s_R[3 * c + r];
+            else if (bi == 4 && bj == 2) f = r == c ? T(1) : T(0);
+            F[e] = f * dt;
         }
-        for (int e = tid; e < 252; e += blockDim.x) {
-            int i = e / 12, j = e % 12;
+        for (int e = lane; e < 252; e += 64) {
+            const int i = e / 12, j = e - 12 * (e / 12);
+            const int bi = i / 3, bj = j / 3, r = i - 3 * bi, c = j - 3 * bj;
             T g = 0;
-            if (i < 3 && j < 3) g = (i == j) ? T(-1) : T(0);
-            else if (i >= 3 && i < 6 && j >= 3 && j < 6) g = (i - 3 == j - 3) ? T(1) : T(0);
-            else if (i >= 6 && i < 9 && j >= 6 && j < 9) g = -s_R[3 * (j - 6) + (i - 6)];
-            else if (i >= 9 && i < 12 && j >= 9 && j < 12) g = (i - 9 == j - 9) ? T(1) : T(0);
+            if (bi == bj && (bi == 0)) g = r == c ? T(-1) : T(0);
+            else if (bi == bj && (bi == 1 || bi == 3)) g = r == c ? T(1) : T(0);
+            else if (bi == 2 && bj == 2) g = -s_R[3 * c + r];
             G[e] = g;
         }
-        __syncthreads();
-        mm21(F, F, Fdt2, tid);
-        __syncthreads();
-        mm21(Fdt2, F, Fdt3, tid);
-        __syncthreads();
-        for (int e = tid; e < 441; e += blockDim.x) {
-            T id = (e / 21 == e % 21) ? T(1) : T(0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        mm21w(F, F, Fdt2, lane);
+        mm21w(Fdt2, F, Fdt3, lane);
+        for (int e = lane; e < 441; e += 64) {
+            const T id = (e / 21 == e % 21) ? T(1) : T(0);
             Phi[e] = id + F[e] + Fdt2[e] / T(2) + Fdt3[e] / T(6);
         }
-        __syncthreads();
-        if (tid == 0) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) {
             // ---- _predict_new_state (jit_utils.py:46-128), quirk Q1 ----
             T* q = s_imu + I_Q;
             T* v = s_imu + I_V;
@@ -247,62 +262,55 @@ __global__ void __launch_bounds__(256) k_propagate(DevState<T> st, Params<T> prm
             for (int i = 0; i < 3; ++i) { s_imu[I_VN + i] = v[i]; s_imu[I_PN + i] = p[i]; }
             s_imu[I_ALIAS] = T(1);
         }
-        __syncthreads();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         // ---- Q = Phi G Qc G^T Phi^T dt ; P11 = Phi P11 Phi^T + Q (jit_utils.py:130-135)
-        for (int e = tid; e < 252; e += blockDim.x) {
-            int i = e / 12, j = e % 12;
+        for (int e = lane; e < 252; e += 64) {
+            const int i = e / 12, j = e - 12 * (e / 12);
             T sacc = 0;
             for (int k2 = 0; k2 < 21; ++k2) sacc += Phi[i * 21 + k2] * G[k2 * 12 + j];
-            T qc = j < 3 ? prm.qc_gyro : (j < 6 ? prm.qc_gbias : (j < 9 ? prm.qc_acc : prm.qc_abias));
+            const T qc = j < 3 ? prm.qc_gyro : (j < 6 ? prm.qc_gbias : (j < 9 ? prm.qc_acc : prm.qc_abias));
             PG[e] = sacc * qc;
         }
-        for (int e = tid; e < 441; e += blockDim.x) {   // A = Phi P11
-            int i = e / 21, j = e % 21;
-            T sacc = 0;
-            for (int k2 = 0; k2 < 21; ++k2) sacc += Phi[i * 21 + k2] * P11[k2 * 21 + j];
-            A[e] = sacc;
-        }
-        __syncthreads();
-        for (int e = tid; e < 441; e += blockDim.x) {   // Bm = (Phi G Qc) G^T ; Fdt2 = A Phi^T
-            int i = e / 21, j = e % 21;
+        mm21w(Phi, P11, A, lane);   // A = Phi P11 (the mm's waitcnt also covers PG)
+        for (int e = lane; e < 441; e += 64) {   // Fdt2 = (Phi G Qc) G^T ; Fdt3 = A Phi^T
+            const int i = e / 21, j = e - 21 * (e / 21);
             T s1 = 0, s2 = 0;
             for (int k2 = 0; k2 < 12; ++k2) s1 += PG[i * 12 + k2] * G[j * 12 + k2];
+#pragma unroll 7
             for (int k2 = 0; k2 < 21; ++k2) s2 += A[i * 21 + k2] * Phi[j * 21 + k2];
-            Bm[e] = s1;
-            Fdt2[e] = s2;
+            Fdt2[e] = s1;
+            Fdt3[e] = s2;
         }
-        __syncthreads();
-        for (int e = tid; e < 441; e += blockDim.x) {   // Q = Bm Phi^T dt ; P11' = A Phi^T + Q
-            int i = e / 21, j = e % 21;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        for (int e = lane; e < 441; e += 64) {   // Q = Bm Phi^T dt ; P11' = A Phi^T + Q (into A)
+            const int i = e / 21, j = e - 21 * (e / 21);
             T s1 = 0;
-            for (int k2 = 0; k2 < 21; ++k2) s1 += Bm[i * 21 + k2] * Phi[j * 21 + k2];
-            Fdt3[e] = Fdt2[e] + s1 * dt;
+#pragma unroll 7
+            for (int k2 = 0; k2 < 21; ++k2) s1 += Fdt2[i * 21 + k2] * Phi[j * 21 + k2];
+            A[e] = Fdt3[e] + s1 * dt;
         }
-        mm21(Phi, PhiT, A, tid);   // cumulative Phi
-        __syncthreads();
-        for (int e = tid; e < 441; e += blockDim.x) {
-            int i = e / 21, j = e % 21;
-            P11[e] = (Fdt3[e] + Fdt3[j * 21 + i]) / T(2);
-            PhiT[e] = A[e];
+        mm21w(Phi, PhiT, Fdt2, lane);   // cumulative Phi (into Fdt2)
+        for (int e = lane; e < 441; e += 64) {
+            const int i = e / 21, j = e - 21 * (e / 21);
+            P11[e] = (A[e] + A[j * 21 + i]) / T(2);
+            PhiT[e] = Fdt2[e];
         }
-        __syncthreads();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
     // write back P11, IMU record; cross blocks with the cumulative Phi
-    for (int e = tid; e < 441; e += blockDim.x) P[(e / 21) * ld + e % 21] = P11[e];
-    for (int e = tid; e < IMU_STRIDE; e += blockDim.x) imu[e] = s_imu[e];
-    if (n > 0) {
-        for (int j = 21 + tid; j < D; j += blockDim.x) {
-            T col[21], out[21];
-            for (int m = 0; m < 21; ++m) col[m] = P[m * ld + j];
-            for (int i = 0; i < 21; ++i) {
-                T sacc = 0;
-                for (int m = 0; m < 21; ++m) sacc += PhiT[i * 21 + m] * col[m];
-                out[i] = sacc;
-            }
-            for (int i = 0; i < 21; ++i) {
-                P[i * ld + j] = out[i];
-                P[(size_t)j * ld + i] = out[i];
-            }
+    for (int e = lane; e < 441; e += 64) P[(e / 21) * ld + e % 21] = P11[e];
+    for (int e = lane; e < IMU_STRIDE; e += 64) imu[e] = s_imu[e];
+    for (int j = 21 + lane; j < D; j += 64) {
+        T col[21];
+#pragma unroll
+        for (int m = 0; m < 21; ++m) col[m] = P[m * ld + j];
+#pragma unroll 1
+        for (int i = 0; i < 21; ++i) {   // not unrolled: keeps the 441 Phi entries out of registers
+            T sacc = 0;
+#pragma unroll
+            for (int m = 0; m < 21; ++m) sacc += PhiT[i * 21 + m] * col[m];
+            P[i * ld + j] = sacc;
+            P[(size_t)j * ld + i] = sacc;
         }
     }
 }
@@ -2239,7 +2247,14 @@ template <typename T>
 void launch_propagate(hipStream_t s, const DevState<T>& st, const Params<T>& prm, int nfilt, const int* filters,
                       const int* smp_off, const T* samples) {
     if (nfilt <= 0) return;
-    hipLaunchKernelGGL(k_propagate<T>, dim3(nfilt), dim3(256), 0, s, st, prm, filters, smp_off, samples);
+    const size_t lds = 4 * (size_t)PROP_LDS * sizeof(T);
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_propagate<T>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr = true;
+    }
+    hipLaunchKernelGGL(k_propagate<T>, dim3((nfilt + 3) / 4), dim3(256), lds, s, st, prm, nfilt, filters, smp_off,
+                       samples);
 }
 template <typename T>
 void launch_augment(hipStream_t s, const DevState<T>& st, int nfilt, const int* filters) {
