@@ -339,7 +339,7 @@ int run_update_chain(msckf_ctx* c, int row_cap, bool triangulate) {
     UpdWs<T> ws = upd_ws<T>(c);
     if (triangulate) {
         c->timer.begin(s, "triangulate");
-        launch_triangulate<T>(s, st, prm, fb);
+        launch_triangulate<T>(s, st, prm, fb, c->sc);
         c->timer.end(s);
     }
     c->timer.begin(s, "feature_jacobian");
@@ -646,7 +646,7 @@ int do_get_states_batch(msckf_ctx* c, int nfilt, const int32_t* filters, double*
 template <typename T>
 int run_triangulate_only(msckf_ctx* c) {
     c->timer.begin(c->stream, "triangulate");
-    launch_triangulate<T>(c->stream, dev_state<T>(c), make_params<T>(c), feat_batch<T>(c));
+    launch_triangulate<T>(c->stream, dev_state<T>(c), make_params<T>(c), feat_batch<T>(c), c->sc);
     c->timer.end(c->stream);
     HIPC(hipGetLastError());
     return 0;
@@ -659,7 +659,7 @@ int do_triangulate(msckf_ctx* c, int f, int nf, const int32_t* obs_off, const in
     int r = load_features<T>(c, nf, nullptr, f, obs_off, obs_cam, obs_z, nullptr, nullptr);
     if (r) return r;
     c->timer.begin(c->stream, "triangulate");
-    launch_triangulate<T>(c->stream, dev_state<T>(c), make_params<T>(c), feat_batch<T>(c));
+    launch_triangulate<T>(c->stream, dev_state<T>(c), make_params<T>(c), feat_batch<T>(c), c->sc);
     c->timer.end(c->stream);
     HIPC(hipGetLastError());
     HIPC(hipStreamSynchronize(c->stream));

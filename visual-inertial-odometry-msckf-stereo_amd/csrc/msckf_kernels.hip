@@ -440,7 +440,18 @@ __global__ void k_cov_diag(DevState<T> st, const int* __restrict__ filters, int 
 // lanes (<= 4 per lane), LM sums reduced with xor-shuffles so every lane holds
 // bit-identical totals and runs the (scalar) LM control flow redundantly.
 // ===========================================================================
-constexpr int TRI_VPL = 4;   // views per lane -> up to 128 observations
+// Sum over aligned S-lane segments of the wavefront (xor shuffles stay inside
+// a segment for offsets < S).
+template <int S, typename T>
+__device__ __forceinline__ T seg_sum(T x) {
+#pragma unroll
+    for (int m = S >> 1; m >= 1; m >>= 1) x += __shfl_xor(x, m, 64);
+    return x;
+}
+
+// views per lane: S lanes per feature (the k_feature segment classes, M <= S
+// for S < 128) hold 2M views, VPL = 2 (VPL = 4 in the 64-lane class that
+// takes 64 < M <= 128)
 
 template <typename T>
 __device__ __forceinline__ void lu3_solve(T A[9], T b[3], T x[3]) {
@@ -470,12 +481,18 @@ __device__ __forceinline__ void lu3_solve(T A[9], T b[3], T x[3]) {
     }
 }
 
-template <typename T>
+template <typename T, int S, int TRI_VPL>
 __global__ void __launch_bounds__(256) k_triangulate(DevState<T> st, Params<T> prm, FeatBatch<T> fb,
-                                                     int f0, int nfeat) {
-    const int lane = threadIdx.x & 63;
-    const int f = f0 + blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    if (f >= f0 + nfeat) return;
+                                                     const int* __restrict__ flist, int cnt) {
+    // S-lane segment per feature, 64 / S features per wavefront; every lane of
+    // a segment runs the (scalar) LM control flow on bit-identical segment sums
+    constexpr int PER = 64 / S;
+    const int lane = threadIdx.x & 63, sl0 = lane & ~(S - 1);
+    const int wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (wid * PER >= cnt) return;
+    const int li = wid * PER + lane / S;
+    const bool active = li < cnt;
+    const int f = flist[active ? li : cnt - 1];
     const int b = fb.feat_filter[f];
     const int o0 = fb.obs_off[f], M = fb.obs_off[f + 1] - o0;
     const int nv = 2 * M;
@@ -513,7 +530,7 @@ __global__ void __launch_bounds__(256) k_triangulate(DevState<T> st, Params<T> p
     T VR[TRI_VPL][9], Vt[TRI_VPL][3], Vz[TRI_VPL][2];
 #pragma unroll
     for (int s = 0; s < TRI_VPL; ++s) {
-        int v = lane + 64 * s;
+        int v = (lane & (S - 1)) + S * s;
         if (v < nv) {
             T R[9], t[3];
             view_pose(v, R, t);
@@ -537,7 +554,7 @@ __global__ void __launch_bounds__(256) k_triangulate(DevState<T> st, Params<T> p
     // initial guess from view 0 and the LAST cam0 view (nv-2)  (feature.py:99-122, 216-218)
     T x[3];
     {
-        int vl = nv - 2, sl = vl >> 6, ll = vl & 63;
+        int vl = nv - 2, sl = vl / S, ll = sl0 + (vl & (S - 1));
         T R12[9], t12[3], z2[2], z1[2];
         // broadcast view vl's transform from its lane (static slot index)
         for (int e = 0; e < 9; ++e) {
@@ -557,7 +574,7 @@ __global__ void __launch_bounds__(256) k_triangulate(DevState<T> st, Params<T> p
 #pragma unroll
             for (int s = 1; s < TRI_VPL; ++s) val = (sl == s) ? Vz[s][i] : val;
             z2[i] = __shfl(val, ll, 64);
-            z1[i] = __shfl(Vz[0][i], 0, 64);
+            z1[i] = __shfl(Vz[0][i], sl0, 64);
         }
         T z1h[3] = {z1[0], z1[1], T(1)};
         T m[3];
@@ -574,7 +591,7 @@ __global__ void __launch_bounds__(256) k_triangulate(DevState<T> st, Params<T> p
         T c = 0;
 #pragma unroll
         for (int s = 0; s < TRI_VPL; ++s) {
-            if (lane + 64 * s < nv) {
+            if ((lane & (S - 1)) + S * s < nv) {
                 T h[3];
                 for (int i = 0; i < 3; ++i)
                     h[i] = VR[s][3 * i] * xx[0] + VR[s][3 * i + 1] * xx[1] + VR[s][3 * i + 2] + xx[2] * Vt[s][i];
@@ -582,7 +599,7 @@ __global__ void __launch_bounds__(256) k_triangulate(DevState<T> st, Params<T> p
                 c += e0 * e0 + e1 * e1;
             }
         }
-        return wave_sum(c);
+        return seg_sum<S>(c);
     };
     T lam = prm.damping;
     T cost = total_cost(x);
@@ -596,7 +613,7 @@ __global__ void __launch_bounds__(256) k_triangulate(DevState<T> st, Params<T> p
         T A[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, bb[3] = {0, 0, 0};
 #pragma unroll
         for (int s = 0; s < TRI_VPL; ++s) {
-            if (lane + 64 * s < nv) {
+            if ((lane & (S - 1)) + S * s < nv) {
                 T h[3];
                 for (int i = 0; i < 3; ++i)
                     h[i] = VR[s][3 * i] * x[0] + VR[s][3 * i + 1] * x[1] + VR[s][3 * i + 2] + x[2] * Vt[s][i];
@@ -617,8 +634,8 @@ __global__ void __launch_bounds__(256) k_triangulate(DevState<T> st, Params<T> p
                 }
             }
         }
-        for (int e = 0; e < 9; ++e) A[e] = wave_sum(A[e]);
-        for (int e = 0; e < 3; ++e) bb[e] = wave_sum(bb[e]);
+        for (int e = 0; e < 9; ++e) A[e] = seg_sum<S>(A[e]);
+        for (int e = 0; e < 3; ++e) bb[e] = seg_sum<S>(bb[e]);
         int inner = 0;
         while (inner < prm.inner_max && !reduced) {
             T Al[9], bl[3], delta[3];
@@ -646,13 +663,17 @@ __global__ void __launch_bounds__(256) k_triangulate(DevState<T> st, Params<T> p
     bool ok = true;
 #pragma unroll
     for (int s = 0; s < TRI_VPL; ++s) {
-        if (lane + 64 * s < nv) {
+        if ((lane & (S - 1)) + S * s < nv) {
             T z = VR[s][6] * pf[0] + VR[s][7] * pf[1] + VR[s][8] * pf[2] + Vt[s][2];
             if (z <= 0) ok = false;
         }
     }
-    ok = __all(ok);
-    if (lane == 0) {
+    {   // every view of the segment in front of the camera
+        const unsigned long long bad = __ballot(!ok);
+        const unsigned long long segmask = S == 64 ? ~0ull : (((1ull << S) - 1) << sl0);
+        ok = (bad & segmask) == 0;
+    }
+    if ((lane & (S - 1)) == 0 && active) {
         T pw[3];
         mat3_vec(R0w, pf, pw);
         for (int i = 0; i < 3; ++i) fb.p_w[3 * f + i] = pw[i] + t0w[i];
@@ -679,14 +700,6 @@ __global__ void __launch_bounds__(256) k_triangulate(DevState<T> st, Params<T> p
 // The nullspace basis differs from the reference's SVD basis by an orthogonal
 // transform, to which gating and the update are invariant (quirk Q4).
 // ===========================================================================
-// Sum over aligned S-lane segments of the wavefront (xor shuffles stay inside
-// a segment for offsets < S).
-template <int S, typename T>
-__device__ __forceinline__ T seg_sum(T x) {
-#pragma unroll
-    for (int m = S >> 1; m >= 1; m >>= 1) x += __shfl_xor(x, m, 64);
-    return x;
-}
 
 // Store n (even) values as 2-element vectors (8-byte float2 / 16-byte double2
 // stores; rows of obs_ws / obs_g keep that alignment).
@@ -2278,9 +2291,23 @@ void launch_cov_diag(hipStream_t s, const DevState<T>& st, int nfilt, const int*
                        out);
 }
 template <typename T>
-void launch_triangulate(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const FeatBatch<T>& fb) {
+void launch_triangulate(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const FeatBatch<T>& fb,
+                        const SegClasses& sc) {
     if (fb.nf == 0) return;
-    hipLaunchKernelGGL(k_triangulate<T>, dim3((fb.nf + 3) / 4), dim3(256), 0, s, st, prm, fb, 0, fb.nf);
+    for (int c = 0; c < SegClasses::NC; ++c) {   // the k_feature classes: S lanes, 2 views per lane
+        const int cnt = sc.off[c + 1] - sc.off[c];
+        if (cnt == 0) continue;
+        const int* list = sc.list + sc.off[c];
+        const int lanes = SegClasses::S[c] < 64 ? SegClasses::S[c] : 64;
+        const int waves = (cnt * lanes + 63) / 64, blocks = (waves + 3) / 4;
+        switch (SegClasses::S[c]) {
+            case 8: hipLaunchKernelGGL((k_triangulate<T, 8, 2>), dim3(blocks), dim3(256), 0, s, st, prm, fb, list, cnt); break;
+            case 16: hipLaunchKernelGGL((k_triangulate<T, 16, 2>), dim3(blocks), dim3(256), 0, s, st, prm, fb, list, cnt); break;
+            case 32: hipLaunchKernelGGL((k_triangulate<T, 32, 2>), dim3(blocks), dim3(256), 0, s, st, prm, fb, list, cnt); break;
+            case 64: hipLaunchKernelGGL((k_triangulate<T, 64, 2>), dim3(blocks), dim3(256), 0, s, st, prm, fb, list, cnt); break;
+            default: hipLaunchKernelGGL((k_triangulate<T, 64, 4>), dim3(blocks), dim3(256), 0, s, st, prm, fb, list, cnt); break;
+        }
+    }
 }
 template <typename T>
 void launch_feature(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const FeatBatch<T>& fb,
@@ -2524,7 +2551,8 @@ void launch_kalman(hipStream_t s, const DevState<T>& st, const Params<T>& prm, c
     template void launch_prune<T>(hipStream_t, const DevState<T>&, int, const int*, const int*, const int*,  \
                                   const int*, const int*);                                                 \
     template void launch_cov_diag<T>(hipStream_t, const DevState<T>&, int, const int*, int, int, T*);      \
-    template void launch_triangulate<T>(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&); \
+    template void launch_triangulate<T>(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&,  \
+                                        const SegClasses&);                                                 \
     template void launch_feature<T>(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&, const SegClasses&); \
     template void launch_gate<T>(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&, const GateClasses&); \
     template void launch_select<T>(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const UpdWs<T>&, int); \

@@ -71,8 +71,6 @@ void launch_prune(hipStream_t, const DevState<T>&, int nfilt, const int* filters
                   const int* keep, const int* kcam_off, const int* keep_cams);
 template <typename T>
 void launch_cov_diag(hipStream_t, const DevState<T>&, int nfilt, const int* filters, int i0, int n, T* out);
-template <typename T>
-void launch_triangulate(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&);
 // Per-feature kernels packed S lanes per feature: features listed by class
 // (M <= S), 64/S features per wavefront.
 struct SegClasses {
@@ -82,13 +80,14 @@ struct SegClasses {
     int off[NC + 1] = {};
 };
 template <typename T>
+void launch_triangulate(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&, const SegClasses&);
+template <typename T>
 void launch_feature(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&, const SegClasses&);
 // Feature index lists per gating size class (device pointer + host offsets).
 // Gating size classes by observation count M.  Class c < NC-2 runs the
-// one-wave register-tile kernel with TPL[c] 4x4 tiles per lane (enough for the
-// (M+1)(M+2)/2 tiles of the augmented 4M+4 matrix); class NC-2 (M <= 62) the
-// workgroup register-tile kernel k_gate_big; the last class the workgroup LDS
-// kernel (or its global-memory variant).
+// one-wave register-tile kernel with TPL[c] 4x4 tiles per lane; class NC-2
+// (M <= 82) the workgroup register-tile kernel k_gate_big; the last class the
+// workgroup LDS kernel (or its global-memory variant).
 struct GateClasses {
     // one-wave classes by the tiles of the reduced (3M + 4)-square matrix,
     // ceil((gate_nt(M) (gate_nt(M) + 1) / 2) / 64) per lane; then the
