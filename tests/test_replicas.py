@@ -34,8 +34,10 @@ def _worker(rank, world, port, q):
         el = 0.5 + grp.rank            # rank 1 is the slow one
         mx = grp.max_over_ranks(el)
         rate = replicas.whole_job_rate(64, grp.world, 10, mx)
+        mine = replicas.shard(list(range(11)), grp.rank, grp.world)   # 11 sequences over the ranks
+        total = grp.sum_over_ranks(len(mine))
         grp.barrier()
-        q.put((grp.rank, grp.world, seeds, float(prob.P.sum()), mx, rate))
+        q.put((grp.rank, grp.world, seeds, float(prob.P.sum()), mx, rate, mine, total))
         grp.close()
     except Exception as e:   # surface the failure in the parent
         q.put((rank, "error", repr(e)))
@@ -54,6 +56,12 @@ def test_single_process_needs_no_group(monkeypatch):
 def test_problem_seeds_disjoint():
     a, b = set(replicas.problem_seeds(0, 32)), set(replicas.problem_seeds(1, 32))
     assert len(a) == 32 and not (a & b)
+
+
+def test_shard_round_robin():
+    parts = [replicas.shard(list(range(11)), r, 8) for r in range(8)]
+    assert sorted(sum(parts, [])) == list(range(11))
+    assert [len(p) for p in parts] == [2, 2, 2, 1, 1, 1, 1, 1]
 
 
 def test_whole_job_rate():
@@ -76,7 +84,9 @@ def test_gloo_world2_replicas():
     for r in res:
         assert r[1] != "error", r
     res.sort()
-    (r0, w0, s0, p0, m0, v0), (r1, w1, s1, p1, m1, v1) = res
+    (r0, w0, s0, p0, m0, v0, sh0, t0), (r1, w1, s1, p1, m1, v1, sh1, t1) = res
+    assert sorted(sh0 + sh1) == list(range(11)) and not (set(sh0) & set(sh1))   # each sequence on one rank
+    assert t0 == t1 == 11
     assert (r0, r1) == (0, 1) and w0 == w1 == 2
     assert not (set(s0) & set(s1))          # different problems per replica
     assert p0 != p1

@@ -37,6 +37,15 @@ class ReplicaGroup:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
+    def sum_over_ranks(self, x: float) -> float:
+        """SUM all-reduce of one float (e.g. frames processed by every rank)."""
+        if self.dist is None:
+            return float(x)
+        import torch
+        t = torch.tensor([float(x)], dtype=torch.float64, device=self.device)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return float(t.item())
+
     def close(self):
         if self.dist is not None:
             self.dist.destroy_process_group()
@@ -65,6 +74,13 @@ def problem_seeds(rank: int, unique: int) -> List[int]:
     """Seeds of the distinct synthetic problems a replica tiles over its
     batch: disjoint across ranks, so N replicas process N different batches."""
     return [1000 * rank + u for u in range(unique)]
+
+
+def shard(items: list, rank: int, world: int) -> list:
+    """The independent units (sequences, filter batches) a rank owns:
+    round-robin, so every unit runs on exactly one rank (SURVEY config 4:
+    sequences one per GPU, no cross-GPU state)."""
+    return list(items[rank::world])
 
 
 def whole_job_rate(filters_per_rank: int, world: int, steps: int, max_elapsed_s: float) -> float:
