@@ -1707,33 +1707,47 @@ size_t gate_big_lds_bytes(int maxM) {
 }
 
 // ===========================================================================
-// Stacking in feature order with the row cap (msckf.py:671-679): one thread
-// per filter walks its features; decides the compression (msckf.py:549).
+// Stacking in feature order with the row cap (msckf.py:671-679): one
+// wavefront per filter scans its features; decides the compression (msckf.py:549).
 // ===========================================================================
 template <typename T>
-__global__ void k_select(DevState<T> st, FeatBatch<T> fb, UpdWs<T> ws, int row_cap) {
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ void __launch_bounds__(256) k_select(DevState<T> st, FeatBatch<T> fb, UpdWs<T> ws, int row_cap) {
+    // one wavefront per filter: 64 features at a time, the accepted row counts
+    // prefix-summed across the wave.  Feature f is stacked iff it is valid,
+    // accepted and the rows stacked before it do not exceed the cap yet (the
+    // reference breaks after the count first exceeds it, msckf.py:676-679).
+    const int lane = threadIdx.x & 63;
+    const int b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (b >= st.B) return;
-    int count = 0;
-    bool capped = false;
-    for (int f = fb.feat_off[b]; f < fb.feat_off[b + 1]; ++f) {
-        fb.include[f] = 0;
-        fb.row_off[f] = 0;
-        if (capped || !fb.valid[f]) continue;
-        if (fb.accept[f]) {
-            const int M = fb.obs_off[f + 1] - fb.obs_off[f];
-            fb.include[f] = 1;
-            fb.row_off[f] = count;
-            count += 4 * M - 3;
+    int carry = 0, count = 0;
+    for (int f0 = fb.feat_off[b]; f0 < fb.feat_off[b + 1]; f0 += 64) {
+        const int f = f0 + lane;
+        const bool in = f < fb.feat_off[b + 1];
+        int v = 0;
+        if (in && fb.valid[f] && fb.accept[f]) v = 4 * (fb.obs_off[f + 1] - fb.obs_off[f]) - 3;
+        int incl = v;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int t = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += t;
         }
-        if (row_cap > 0 && count > row_cap) capped = true;
+        const int excl = carry + incl - v;
+        const bool take = v > 0 && (row_cap <= 0 || excl <= row_cap);
+        if (in) {
+            fb.include[f] = take ? 1 : 0;
+            fb.row_off[f] = take ? excl : 0;
+        }
+        count += wave_sum(take ? v : 0);
+        carry += __shfl(incl, 63, 64);
     }
-    const int C = 6 * st.ncams[b];
-    int* info = ws.info + 4 * b;
-    info[0] = count;
-    info[1] = count > C ? C : count;
-    info[2] = count > C ? 1 : 0;
-    info[3] = 0;
+    if (lane == 0) {
+        const int C = 6 * st.ncams[b];
+        int* info = ws.info + 4 * b;
+        info[0] = count;
+        info[1] = count > C ? C : count;
+        info[2] = count > C ? 1 : 0;
+        info[3] = 0;
+    }
 }
 
 // ===========================================================================
@@ -2450,7 +2464,7 @@ void launch_gate(hipStream_t s, const DevState<T>& st, const Params<T>& prm, con
 template <typename T>
 void launch_select(hipStream_t s, const DevState<T>& st, const FeatBatch<T>& fb, const UpdWs<T>& ws,
                    int row_cap) {
-    hipLaunchKernelGGL(k_select<T>, dim3((st.B + 63) / 64), dim3(64), 0, s, st, fb, ws, row_cap);
+    hipLaunchKernelGGL(k_select<T>, dim3((st.B + 3) / 4), dim3(256), 0, s, st, fb, ws, row_cap);
 }
 
 // Numerical-rank threshold of the pivoted Cholesky, relative to max diag(A).
