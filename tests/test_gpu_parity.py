@@ -234,6 +234,27 @@ def test_batched_fp32_vs_oracle(cap):
             assert rel(dp, dp_o) < 1e-3
 
 
+def test_gate_fp32_gamma_vs_oracle():
+    """fp32 gating (MFMA tiles, every size class up to M = 40: 1..8 16-row
+    blocks, single- and multi-pass Y staging) against the oracle's fp64 gamma
+    (msckf.py:606-614).  Tolerance: fp32 with the saddle point's conditioning
+    (~1e3) -- median relative error <= 1e-4, 99th percentile <= 1e-2."""
+    problems = [synth.make_update_problem(40, 150, seed=300 + b) for b in range(2)]
+    ctx, ds, feat_off, acc, gam, pw, valid, rows = _batched(problems, np.float32)
+    errs = []
+    for b, d in enumerate(ds):
+        st, acc_o, tri_p, tri_ok, gam_o = oracle_update(d)
+        sl = slice(feat_off[b], feat_off[b + 1])
+        ok = valid[sl] & tri_ok
+        g, go = gam[sl][ok], gam_o[ok]
+        assert np.isfinite(g).all()
+        errs.append(np.abs(g - go) / np.maximum(np.abs(go), 1e-6))
+    e = np.concatenate(errs)
+    assert e.size > 250
+    assert np.median(e) < 1e-4, np.median(e)
+    assert np.quantile(e, 0.99) < 1e-2, np.quantile(e, 0.99)
+
+
 def test_restore_repeats_identically():
     problems = [synth.make_update_problem(20, 60, seed=7 + b) for b in range(2)]
     ds = [problem_to_dict(p) for p in problems]

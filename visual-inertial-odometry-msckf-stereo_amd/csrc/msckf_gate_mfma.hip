@@ -1,0 +1,369 @@
+// msckf_gate_mfma.hip -- chi^2 gating of the fp32 contexts (msckf.py:606-614)
+// on fp32 MFMA tiles, one wavefront per feature (M <= 40).
+//
+// Same mathematics as k_gate_wave (msckf_kernels.hip): gamma = r0^T S^-1 r0
+// is read off an LDL^T elimination of the rank-3 reduced saddle-point matrix
+//     [[Y~, H_f~, r~], [H_f~^T, 0, 0], [r~^T, 0, 0]],   Y~ = Ht P Ht^T + s2 I,
+// (3M range rows, the null rows adding |r_n|^2 / s2), with no projection
+// formed.  What changes is the layout of the elimination:
+//   * the matrix is held as 16x16 blocks in the C/D layout of
+//     v_mfma_f32_16x16x4_f32 (lane l: column 16 cb + (l & 15), rows
+//     16 rb + 4 (l >> 4) + i, i = 0..3), lower block triangle only;
+//   * rows: the 3M range rows, unit padding pivots, and the four B rows
+//     [H_f~^T ; r~^T] as the last four rows of the last block;
+//   * each 4-pivot step, the owners of the four pivot columns dump them to a
+//     row-major LDS panel, every lane factors the 4x4 diagonal (one reciprocal
+//     per pivot), forms its MFMA operands (lane l: row 16 rb + (l & 15), pivot
+//     column l >> 4 of W = A L_d^-T and of -W D^-1; rows of finished pivots
+//     zeroed), and the whole trailing lower block triangle takes the rank-4
+//     update as one v_mfma_f32_16x16x4_f32 per block;
+//   * the Schur complement left in the B rows' 4x4 gives gamma as before.
+// One MFMA replaces the 16 packed FMAs + operand fetches a 4x4 register tile
+// needed, and no lanes idle on finished tiles of a triangular tile order.
+// fp32 MFMA is exact f32 (an fmaf chain) on gfx950.
+#include "msckf_common.h"
+#include "msckf_launch.h"
+
+#include <stdlib.h>
+
+namespace msckf {
+
+namespace {
+
+using F4 = float __attribute__((ext_vector_type(4)));
+using F2 = float __attribute__((ext_vector_type(2)));
+
+__host__ __device__ constexpr int gm_nb(int M) { return (3 * M + 4 + 15) / 16; }
+__host__ __device__ constexpr int gm_head(int Mmax) { return (22 * Mmax + 3) & ~3; }   // Ht rows + [r~ | r_n]
+__host__ __device__ constexpr int gm_area(int Mmax, int capb) {                         // Y staging / panel
+    return 9 * capb > 64 * gm_nb(Mmax) ? ((9 * capb + 3) & ~3) : 64 * gm_nb(Mmax);
+}
+__host__ __device__ constexpr int gm_wave_floats(int Mmax, int capb) {
+    return gm_head(Mmax) + gm_area(Mmax, capb) + ((Mmax + 3) & ~3);
+}
+__host__ __device__ constexpr int bidx(int rb, int cb) { return rb * (rb + 1) / 2 + cb; }
+
+template <int NB, bool MP>
+__global__ void __launch_bounds__(256) k_gate_mfma(DevState<float> st, Params<float> prm, FeatBatch<float> fb,
+                                                   const int* __restrict__ flist, int nlist, int Mmax, int capb,
+                                                   int phases) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wpb = blockDim.x >> 6;
+    // wave-uniform by construction; readfirstlane tells the compiler, so every
+    // size test below is a scalar branch instead of an exec-mask region
+    const int li = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x) * wpb + wv);
+    if (li >= nlist) return;
+    const int f = __builtin_amdgcn_readfirstlane(flist[li]);
+    if (!fb.valid[f]) {
+        if (lane == 0) { fb.gamma[f] = NAN; fb.accept[f] = 0; }
+        return;
+    }
+    const int b = __builtin_amdgcn_readfirstlane(fb.feat_filter[f]);
+    const int o0 = __builtin_amdgcn_readfirstlane(fb.obs_off[f]);
+    const int M = __builtin_amdgcn_readfirstlane(fb.obs_off[f + 1]) - o0, M3 = 3 * M;
+    const int nY = (M3 + 3) >> 2;          // elimination steps, 4 pivots each
+    const int nb = gm_nb(M);               // 16-row blocks in use (<= NB)
+    const int nB = 16 * nb - 4;            // first B row
+    float* ht = reinterpret_cast<float*>(smem_raw) + (size_t)wv * gm_wave_floats(Mmax, capb);
+    float* rt = ht + 18 * Mmax;            // [Mmax][4]: r~ (3), r_n
+    float* area = ht + gm_head(Mmax);
+    float* stage = area;                   // [capb][9] Y blocks of one pass (row-major lower block order)
+    float* pan = area;                     // [16 NB][4] panel rows (after the Y phase)
+    int* slot = reinterpret_cast<int*>(area + gm_area(Mmax, capb));
+    const float* ws = fb.obs_ws + (size_t)o0 * OBS_WS;
+    for (int e = lane; e < 18 * M; e += 64) {
+        const int o = e / 18;
+        ht[e] = ws[(size_t)o * OBS_WS + OBS_HT + (e - 18 * o)];
+    }
+    float rn2 = 0;
+    for (int e = lane; e < 4 * M; e += 64) {
+        const float v = ws[(size_t)(e >> 2) * OBS_WS + OBS_RT + (e & 3)];
+        rt[e] = v;
+        if ((e & 3) == 3) rn2 += v * v;
+    }
+    rn2 = wave_sum(rn2);
+    for (int i = lane; i < M; i += 64) slot[i] = fb.obs_cam[o0 + i];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+
+    const int col_l = lane & 15, rg = lane >> 4;
+    constexpr int NBLK = NB * (NB + 1) / 2;
+    F4 acc[NBLK];
+    // B rows [H_f~^T ; r~^T] (H_f~ = -Ht[:, 3:6]), unit padding pivots, zeros
+    // (phases: profiling aid, bit0 Y, bit2 elimination; without the Y phase the
+    // range rows get unit pivots so that the elimination still runs in full)
+    const int pad_lo = (phases & 1) ? M3 : 0;
+    auto init_acc = [&]() {
+#pragma unroll
+        for (int RB = 0; RB < NB; ++RB)
+#pragma unroll
+            for (int CB = 0; CB <= RB; ++CB) {
+                const int p = 16 * CB + col_l;
+                const int o = p / 3, c = p - 3 * o;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int q = 16 * RB + 4 * rg + i;
+                    float x = 0;
+                    if (q >= nB && q < nB + 4 && p < M3) {
+                        const int xq = q - nB;
+                        x = xq < 3 ? -ht[18 * o + 6 * c + 3 + xq] : rt[4 * o + c];
+                    } else if (q == p && q >= pad_lo && q < nB) {
+                        x = 1;
+                    }
+                    acc[bidx(RB, CB)][i] = x;
+                }
+            }
+    };
+
+    // ---- Y: observation-pair blocks Ht_a P_ab Ht_b^T (a >= b, 3x3) into LDS in
+    // row-major lower order k = a (a + 1) / 2 + b -- consecutive lanes take
+    // consecutive b of one row a, so a load instruction reads consecutive 24-byte
+    // row segments of P (cams of a track are usually consecutive slots) instead
+    // of 64 scattered blocks -- in passes over observation rows [c0, c1) when
+    // capb < M (M + 1) / 2; each pass fills the lower Y entries of rows [3 c0, 3 c1).
+    const float* P = st.P + (size_t)b * st.Dmax * st.Dmax;
+    const int ldp = st.Dmax;
+    const float s2 = prm.sigma2;
+    constexpr int BIF = MP ? 1 : 2;   // blocks per lane in flight
+    if (MP || !(phases & 1)) init_acc();
+    for (int c0 = 0; c0 < ((phases & 1) ? M : 0);) {
+        int c1 = c0, nbp = 0;
+        while (c1 < M && (c1 == c0 || nbp + (c1 + 1) <= capb)) { nbp += c1 + 1; ++c1; }
+        const int kbase = c0 * (c0 + 1) / 2;
+        for (int k0 = 0; k0 < nbp; k0 += 64 * BIF) {
+            float Pl[BIF][36];
+            int oa[BIF], ob[BIF];
+#pragma unroll
+            for (int j = 0; j < BIF; ++j) {
+                const int kk = k0 + 64 * j + lane;
+                const int k = kbase + (kk < nbp ? kk : 0);
+                int a = (int)((sqrtf(8.0f * (float)k + 1.0f) - 1.0f) * 0.5f);
+                if (a * (a + 1) / 2 > k) --a;
+                if ((a + 1) * (a + 2) / 2 <= k) ++a;
+                oa[j] = a;
+                ob[j] = k - a * (a + 1) / 2;
+                const float* Pb = P + (size_t)(21 + 6 * slot[oa[j]]) * ldp + 21 + 6 * slot[ob[j]];
+#pragma unroll
+                for (int u = 0; u < 6; ++u) {
+                    if (kk < nbp) {
+                        __builtin_memcpy(Pl[j] + 6 * u, Pb + (size_t)u * ldp, 6 * sizeof(float));
+                    } else {
+#pragma unroll
+                        for (int c2 = 0; c2 < 6; ++c2) Pl[j][6 * u + c2] = 0.f;
+                    }
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < BIF; ++j) {
+                const int kk = k0 + 64 * j + lane;
+                if (kk >= nbp) continue;
+                const float* Ha = ht + 18 * oa[j];
+                const float* Hb = ht + 18 * ob[j];
+                float* dst = stage + 9 * kk;
+                F2 hb01[6];   // (Hb[0][u], Hb[1][u])
+#pragma unroll
+                for (int u = 0; u < 6; ++u) hb01[u] = F2{Hb[u], Hb[6 + u]};
+#pragma unroll
+                for (int x = 0; x < 3; ++x) {
+                    F2 t2[3] = {F2{0, 0}, F2{0, 0}, F2{0, 0}};   // Ha[x] P as three column pairs
+#pragma unroll
+                    for (int u = 0; u < 6; ++u) {
+                        const float h = Ha[6 * x + u];
+#pragma unroll
+                        for (int c = 0; c < 3; ++c)
+                            t2[c] = __builtin_elementwise_fma(F2{h, h}, F2{Pl[j][6 * u + 2 * c], Pl[j][6 * u + 2 * c + 1]},
+                                                              t2[c]);
+                    }
+                    const float t1[6] = {t2[0].x, t2[0].y, t2[1].x, t2[1].y, t2[2].x, t2[2].y};
+                    F2 y01 = {0, 0};
+                    float y2 = 0;
+#pragma unroll
+                    for (int u = 0; u < 6; ++u) {
+                        y01 = __builtin_elementwise_fma(F2{t1[u], t1[u]}, hb01[u], y01);
+                        y2 = fmaf(t1[u], Hb[12 + u], y2);
+                    }
+                    dst[3 * x] = y01.x;
+                    dst[3 * x + 1] = y01.y;
+                    dst[3 * x + 2] = y2;
+                }
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // one wave: its stores are visible to all lanes
+        if (!MP) init_acc();
+        const int plo = 3 * c0, phi = 3 * c1;
+#pragma unroll
+        for (int RB = 0; RB < NB; ++RB)
+#pragma unroll
+            for (int CB = 0; CB <= RB; ++CB) {
+                if (16 * RB >= phi || 16 * RB + 16 <= plo || 16 * CB >= phi) continue;   // uniform
+                const int p = 16 * CB + col_l;
+                const int ob_ = p / 3, cb_ = p - 3 * ob_;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int q = 16 * RB + 4 * rg + i;
+                    if (q >= plo && q < phi && q >= p) {
+                        const int oa_ = q / 3, ca_ = q - 3 * oa_;
+                        float v = stage[9 * (oa_ * (oa_ + 1) / 2 + ob_ - kbase) + 3 * ca_ + cb_];
+                        if (q == p) v += s2;
+                        acc[bidx(RB, CB)][i] = v;
+                    }
+                }
+            }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads done before the next pass / the panel reuse
+        c0 = c1;
+        if (!MP) break;
+    }
+
+    // ---- blocked LDL^T, 4 pivots per step, MFMA trailing updates ----
+    bool fail = false;
+    const int csel = rg;   // pivot column of this lane's operands
+#pragma unroll
+    for (int KB = 0; KB < NB; ++KB) {
+        if (4 * KB >= nY || fail || !(phases & 4)) break;
+        for (int sc = 0; sc < 4; ++sc) {
+            const int j = 4 * KB + sc;
+            if (j >= nY) break;
+            const int p0 = 4 * j;
+            // 1. owners of columns p0 .. p0 + 3 dump them (rows of blocks KB..NB-1;
+            //    blocks past nb carry stale rows that step 3 masks)
+            if ((col_l >> 2) == sc) {
+                float* d = pan + 4 * (16 * KB + 4 * rg) + (col_l & 3);
+#pragma unroll
+                for (int RB = KB; RB < NB; ++RB) {
+                    const F4 v = acc[bidx(RB, KB)];
+                    float* dd = d + 64 * (RB - KB);
+                    dd[0] = v[0]; dd[4] = v[1]; dd[8] = v[2]; dd[12] = v[3];
+                }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            // 2. every lane factors the diagonal 4x4 (lower entries only)
+            const F4 r0 = *reinterpret_cast<const F4*>(pan + 4 * p0);
+            const F4 r1 = *reinterpret_cast<const F4*>(pan + 4 * p0 + 4);
+            const F4 r2 = *reinterpret_cast<const F4*>(pan + 4 * p0 + 8);
+            const F4 r3 = *reinterpret_cast<const F4*>(pan + 4 * p0 + 12);
+            F4 xr[NB];   // this lane's panel row of every block row
+#pragma unroll
+            for (int RB = KB; RB < NB; ++RB) xr[RB] = *reinterpret_cast<const F4*>(pan + 4 * (16 * RB + col_l));
+            const float d0 = r0.x, e0 = pivot_rcp(d0);
+            const float l10 = r1.x * e0, l20 = r2.x * e0, l30 = r3.x * e0;
+            const float d1 = r1.y - l10 * r1.x, e1 = pivot_rcp(d1);
+            const float m21 = r2.y - l20 * r1.x, m31 = r3.y - l30 * r1.x;
+            const float l21 = m21 * e1, l31 = m31 * e1;
+            const float d2 = r2.z - l20 * r2.x - l21 * m21, e2 = pivot_rcp(d2);
+            const float m32 = r3.z - l30 * r2.x - l31 * m21;
+            const float l32 = m32 * e2;
+            const float d3 = r3.w - l30 * r3.x - l31 * m31 - l32 * m32;
+            if (!(d0 > 0.f) || !(d1 > 0.f) || !(d2 > 0.f) || !(d3 > 0.f)) { fail = true; break; }
+            const float e3 = pivot_rcp(d3);
+            const float esel = csel == 0 ? e0 : (csel == 1 ? e1 : (csel == 2 ? e2 : e3));
+            // 3. operands: lane l holds row 16 RB + (l & 15), pivot column l >> 4;
+            //    rows of finished pivots and of blocks past nb are zero
+            float av[NB], bv[NB];
+#pragma unroll
+            for (int RB = KB; RB < NB; ++RB) {
+                const int r = 16 * RB + col_l;
+                const F4 x = xr[RB];
+                const float w0 = x.x;
+                const float w1 = x.y - w0 * l10;
+                const float w2 = x.z - w0 * l20 - w1 * l21;
+                const float w3 = x.w - w0 * l30 - w1 * l31 - w2 * l32;
+                float w = csel == 0 ? w0 : (csel == 1 ? w1 : (csel == 2 ? w2 : w3));
+                w = (r <= p0 + 3 || RB >= nb) ? 0.f : w;
+                bv[RB] = w;
+                av[RB] = -w * esel;
+            }
+            // 4. trailing rank-4 update of the lower block triangle right of the panel
+#pragma unroll
+            for (int CB = KB; CB < NB; ++CB)
+#pragma unroll
+                for (int RB = CB; RB < NB; ++RB)
+                    acc[bidx(RB, CB)] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[RB], bv[CB], acc[bidx(RB, CB)], 0, 0, 0);
+        }
+    }
+    // the B rows' 4x4 Schur block (negated [[H_f~^T Y~^-1 H_f~, .], [., r~^T Y~^-1 r~]]):
+    // rows / cols 12..15 of block (nb-1, nb-1) sit in lanes 60..63
+#pragma unroll
+    for (int RB = 0; RB < NB; ++RB)
+        if (RB == nb - 1 && rg == 3 && col_l >= 12) {
+            const F4 v = acc[bidx(RB, RB)];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) pan[4 * i + (col_l - 12)] = v[i];
+        }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) {
+        const float* a = pan;
+        const float d0 = a[0];
+        const float l10 = a[4] / d0, l20 = a[8] / d0, l30 = a[12] / d0;
+        const float d1 = a[5] - l10 * l10 * d0;
+        const float l21 = (a[9] - l20 * l10 * d0) / d1;
+        const float l31 = (a[13] - l30 * l10 * d0) / d1;
+        const float d2 = a[10] - l20 * l20 * d0 - l21 * l21 * d1;
+        const float l32 = (a[14] - l30 * l20 * d0 - l31 * l21 * d1) / d2;
+        const float d3 = a[15] - l30 * l30 * d0 - l31 * l31 * d1 - l32 * l32 * d2;
+        float gam = -d3 + rn2 / s2;
+        if (fail || !(d0 < 0.f) || !(d1 < 0.f) || !(d2 < 0.f) || !(gam == gam)) gam = INFINITY;
+        fb.gamma[f] = gam;
+        fb.accept[f] = (gam < fb.chi2[f]) ? 1 : 0;
+    }
+}
+
+template <int NB, bool MP>
+void launch_cfg(hipStream_t s, const DevState<float>& st, const Params<float>& prm, const FeatBatch<float>& fb,
+                const int* list, int cnt, int Mmax, int capb, int wpb, size_t lds) {
+    static size_t attr = 64 * 1024;
+    if (lds > attr) {
+        (void)hipFuncSetAttribute((const void*)k_gate_mfma<NB, MP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds);
+        attr = lds;
+    }
+    static int phases = -1;   // MSCKF_GATE_PHASES: profiling aid (bit0 Y blocks, bit2 elimination)
+    if (phases < 0) {
+        const char* e = getenv("MSCKF_GATE_PHASES");
+        phases = e ? atoi(e) : 7;
+    }
+    hipLaunchKernelGGL((k_gate_mfma<NB, MP>), dim3((cnt + wpb - 1) / wpb), dim3(64 * wpb), lds, s, st, prm, fb, list,
+                       cnt, Mmax, capb, phases);
+}
+
+template <int NB>
+void launch_nb(hipStream_t s, const DevState<float>& st, const Params<float>& prm, const FeatBatch<float>& fb,
+               const int* list, int cnt, int Mmax) {
+    // Y staging capacity: all M (M + 1) / 2 pair blocks in one pass unless four
+    // waves would then need more than MSCKF_GATE_SPKB KB (default 80: two
+    // workgroups per CU); otherwise passes sized for half of that.
+    static int single_kb = -1;
+    if (single_kb < 0) {
+        const char* e = getenv("MSCKF_GATE_SPKB");
+        single_kb = e ? atoi(e) : 80;
+    }
+    const int nbk = Mmax * (Mmax + 1) / 2;
+    auto per_wave = [&](int cb) { return (size_t)gm_wave_floats(Mmax, cb) * sizeof(float); };
+    int capb = nbk;
+    if (4 * per_wave(capb) > (size_t)single_kb * 1024)
+        for (int parts = 2; 4 * per_wave(capb) > (size_t)single_kb * 512 && capb > Mmax; ++parts)
+            capb = (nbk + parts - 1) / parts > Mmax ? (nbk + parts - 1) / parts : Mmax;
+    const size_t pw = per_wave(capb);
+    const int wpb = 4 * pw <= 160 * 1024 ? 4 : (2 * pw <= 160 * 1024 ? 2 : 1);
+    if (capb < nbk) launch_cfg<NB, true>(s, st, prm, fb, list, cnt, Mmax, capb, wpb, wpb * pw);
+    else launch_cfg<NB, false>(s, st, prm, fb, list, cnt, Mmax, capb, wpb, wpb * pw);
+}
+
+}  // namespace
+
+bool gate_mfma_fits(int maxM) { return maxM >= 1 && gm_nb(maxM) <= 8; }
+
+void launch_gate_mfma(hipStream_t s, const DevState<float>& st, const Params<float>& prm, const FeatBatch<float>& fb,
+                      const int* list, int cnt, int maxM) {
+    if (cnt <= 0) return;
+    switch (gm_nb(maxM)) {
+        case 1: launch_nb<1>(s, st, prm, fb, list, cnt, maxM); break;
+        case 2: launch_nb<2>(s, st, prm, fb, list, cnt, maxM); break;
+        case 3: launch_nb<3>(s, st, prm, fb, list, cnt, maxM); break;
+        case 4: launch_nb<4>(s, st, prm, fb, list, cnt, maxM); break;
+        case 5: launch_nb<5>(s, st, prm, fb, list, cnt, maxM); break;
+        case 6: launch_nb<6>(s, st, prm, fb, list, cnt, maxM); break;
+        case 7: launch_nb<7>(s, st, prm, fb, list, cnt, maxM); break;
+        default: launch_nb<8>(s, st, prm, fb, list, cnt, maxM); break;
+    }
+}
+
+}  // namespace msckf

@@ -2396,11 +2396,11 @@ static void launch_gate_wave(hipStream_t s, const DevState<T>& st, const Params<
 // time): the register-tile wave kernel sized for the class, or for the
 // largest features the workgroup LDS kernel (global-memory kernel if even
 // that does not fit).
-static int gate_mode() {   // MSCKF_GATE=lds forces the workgroup kernel for every class (A/B runs)
-    static int mode = -1;
+static int gate_mode() {   // MSCKF_GATE=lds forces the workgroup kernel for every class, =wave the
+    static int mode = -1;     // 4x4 register-tile wave kernel for fp32 too (A/B runs)
     if (mode < 0) {
         const char* e = getenv("MSCKF_GATE");
-        mode = (e && e[0] == 'l') ? 1 : 0;
+        mode = (e && e[0] == 'l') ? 1 : ((e && e[0] == 'w') ? 2 : 0);
     }
     return mode;
 }
@@ -2426,7 +2426,13 @@ void launch_gate(hipStream_t s, const DevState<T>& st, const Params<T>& prm, con
         if (cnt == 0) continue;
         const int maxM = gc.maxM[c];
         const int* list = gc.list + gc.off[c];
-        if (mode == 0 && c == GateClasses::NC - 2) {   // 40 < M <= 82: register tiles, one workgroup per feature
+        if constexpr (sizeof(T) == 4) {   // fp32: MFMA tiles (msckf_gate_mfma.hip)
+            if (mode == 0 && c < GateClasses::NC - 2 && gate_mfma_fits(maxM)) {
+                launch_gate_mfma(s, st, prm, fb, list, cnt, maxM);
+                continue;
+            }
+        }
+        if (mode != 1 && c == GateClasses::NC - 2) {   // 40 < M <= 82: register tiles, one workgroup per feature
             const int nrow = gate_nt(maxM), tiles = nrow * (nrow + 1) / 2;
             const size_t lds = gate_big_lds_bytes(maxM);
             if (tiles <= 256 * 4) {
@@ -2440,7 +2446,7 @@ void launch_gate(hipStream_t s, const DevState<T>& st, const Params<T>& prm, con
             }
             continue;
         }
-        if (mode == 0 && c < GateClasses::NC - 2) {
+        if (mode != 1 && c < GateClasses::NC - 2) {
             switch (GateClasses::TPL[c]) {
                 case 1: launch_gate_wave<T, 1>(s, st, prm, fb, list, cnt, maxM); break;
                 case 2: launch_gate_wave<T, 2>(s, st, prm, fb, list, cnt, maxM); break;
@@ -2448,6 +2454,7 @@ void launch_gate(hipStream_t s, const DevState<T>& st, const Params<T>& prm, con
                 case 4: launch_gate_wave<T, 4>(s, st, prm, fb, list, cnt, maxM); break;
                 case 5: launch_gate_wave<T, 5>(s, st, prm, fb, list, cnt, maxM); break;
                 case 6: launch_gate_wave<T, 6>(s, st, prm, fb, list, cnt, maxM); break;
+                case 7: launch_gate_wave<T, 7>(s, st, prm, fb, list, cnt, maxM); break;
                 default: launch_gate_wave<T, 8>(s, st, prm, fb, list, cnt, maxM); break;
             }
             continue;

@@ -92,15 +92,21 @@ struct GateClasses {
     // one-wave classes by the tiles of the reduced (3M + 4)-square matrix,
     // ceil((gate_nt(M) (gate_nt(M) + 1) / 2) / 64) per lane; then the
     // register-tile workgroup kernel (nT <= 63) and the global-memory kernel
-    static constexpr int NC = 9;
-    static constexpr int LIM[NC] = {12, 18, 24, 28, 30, 34, 40, 82, 1 << 30};
-    static constexpr int TPL[NC - 2] = {1, 2, 3, 4, 5, 6, 8};
+    // (the one-wave class limits are also the fp32 MFMA kernel's 16-row block
+    // boundaries: ceil((3M + 4) / 16) = 1..8 for M <= 4, 9, 14, 20, 25, 30, 36, 40)
+    static constexpr int NC = 10;
+    static constexpr int LIM[NC] = {4, 9, 14, 20, 25, 30, 36, 40, 82, 1 << 30};
+    static constexpr int TPL[NC - 2] = {1, 1, 2, 3, 4, 5, 7, 8};
     const int* list = nullptr;
     int off[NC + 1] = {};
     int maxM[NC] = {};
 };
 template <typename T>
 void launch_gate(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&, const GateClasses&);
+// fp32 gating on MFMA tiles (msckf_gate_mfma.hip), one wavefront per feature, M <= 40.
+bool gate_mfma_fits(int maxM);
+void launch_gate_mfma(hipStream_t, const DevState<float>&, const Params<float>&, const FeatBatch<float>&,
+                      const int* list, int cnt, int maxM);
 template <typename T>
 void launch_select(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const UpdWs<T>&, int row_cap);
 template <typename T>
