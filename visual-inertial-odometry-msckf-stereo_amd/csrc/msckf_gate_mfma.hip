@@ -88,30 +88,57 @@ __global__ void __launch_bounds__(256) k_gate_mfma(DevState<float> st, Params<fl
     const int col_l = lane & 15, rg = lane >> 4;
     constexpr int NBLK = NB * (NB + 1) / 2;
     F4 acc[NBLK];
-    // B rows [H_f~^T ; r~^T] (H_f~ = -Ht[:, 3:6]), unit padding pivots, zeros
-    // (phases: profiling aid, bit0 Y, bit2 elimination; without the Y phase the
-    // range rows get unit pivots so that the elimination still runs in full)
+    // Matrix assembly into the C-layout blocks.  Every element is written once
+    // per call: Y entries of rows [plo, phi) from the pair-block stage (lower
+    // entries, s2 on the diagonal), and on the first call the rest -- B rows
+    // [H_f~^T ; r~^T] (H_f~ = -Ht[:, 3:6]) in rows 12..15 of block nb - 1, unit
+    // padding pivots, zeros.  The stage offset of Y[q][p] separates into a row
+    // part and a column part: 9 (a (a + 1) / 2 + b) + 3 c_q + c_p with a = q / 3,
+    // b = p / 3.  (phases: profiling aid, bit0 Y, bit2 elimination; without the
+    // Y phase the range rows get unit pivots so that the elimination still runs.)
     const int pad_lo = (phases & 1) ? M3 : 0;
-    auto init_acc = [&]() {
+    const float s2 = prm.sigma2;
+    auto assemble = [&](int plo, int phi, int kbase, bool first) {
 #pragma unroll
-        for (int RB = 0; RB < NB; ++RB)
+        for (int RB = 0; RB < NB; ++RB) {
+            if (!first && (16 * RB >= phi || 16 * RB + 16 <= plo)) continue;   // uniform
+            const bool brow = RB == nb - 1 && rg == 3;   // this lane's 4 rows are the B rows
+            int rofs[4];
+            bool qy[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int q = 16 * RB + 4 * rg + i, oa = q / 3;
+                rofs[i] = 9 * (oa * (oa + 1) / 2 - kbase) + 3 * (q - 3 * oa);
+                qy[i] = q >= plo && q < phi;
+            }
 #pragma unroll
             for (int CB = 0; CB <= RB; ++CB) {
-                const int p = 16 * CB + col_l;
-                const int o = p / 3, c = p - 3 * o;
+                const int p = 16 * CB + col_l, ob = p / 3, cp = p - 3 * ob;
+                float bval[4] = {0.f, 0.f, 0.f, 0.f};
+                if (first && RB == nb - 1) {   // uniform
+                    const bool pv = brow && p < M3;
+                    const int o = pv ? ob : 0;
+#pragma unroll
+                    for (int i = 0; i < 3; ++i) bval[i] = pv ? -ht[18 * o + 6 * cp + 3 + i] : 0.f;
+                    bval[3] = pv ? rt[4 * o + cp] : 0.f;
+                }
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     const int q = 16 * RB + 4 * rg + i;
-                    float x = 0;
-                    if (q >= nB && q < nB + 4 && p < M3) {
-                        const int xq = q - nB;
-                        x = xq < 3 ? -ht[18 * o + 6 * c + 3 + xq] : rt[4 * o + c];
-                    } else if (q == p && q >= pad_lo && q < nB) {
-                        x = 1;
+                    const bool take = qy[i] && (RB > CB || q >= p);
+                    const float y = stage[take ? rofs[i] + 9 * ob + cp : 0];
+                    float v = acc[bidx(RB, CB)][i];
+                    if (first) {
+                        v = bval[i];
+                        if (RB == CB) v = (q == p && q >= pad_lo && q < nB) ? 1.f : v;
                     }
-                    acc[bidx(RB, CB)][i] = x;
+                    if (RB == CB) v = take ? y + (q == p ? s2 : 0.f) : v;
+                    else v = take ? y : v;
+                    acc[bidx(RB, CB)][i] = v;
                 }
+                asm volatile("" : "+a"(acc[bidx(RB, CB)]));   // finished block -> AGPRs now (VGPR budget)
             }
+        }
     };
 
     // ---- Y: observation-pair blocks Ht_a P_ab Ht_b^T (a >= b, 3x3) into LDS in
@@ -122,9 +149,8 @@ __global__ void __launch_bounds__(256) k_gate_mfma(DevState<float> st, Params<fl
     // capb < M (M + 1) / 2; each pass fills the lower Y entries of rows [3 c0, 3 c1).
     const float* P = st.P + (size_t)b * st.Dmax * st.Dmax;
     const int ldp = st.Dmax;
-    const float s2 = prm.sigma2;
     constexpr int BIF = MP ? 1 : 2;   // blocks per lane in flight
-    if (MP || !(phases & 1)) init_acc();
+    if (MP || !(phases & 1)) assemble(0, 0, 0, true);
     for (int c0 = 0; c0 < ((phases & 1) ? M : 0);) {
         int c1 = c0, nbp = 0;
         while (c1 < M && (c1 == c0 || nbp + (c1 + 1) <= capb)) { nbp += c1 + 1; ++c1; }
@@ -188,26 +214,7 @@ __global__ void __launch_bounds__(256) k_gate_mfma(DevState<float> st, Params<fl
             }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // one wave: its stores are visible to all lanes
-        if (!MP) init_acc();
-        const int plo = 3 * c0, phi = 3 * c1;
-#pragma unroll
-        for (int RB = 0; RB < NB; ++RB)
-#pragma unroll
-            for (int CB = 0; CB <= RB; ++CB) {
-                if (16 * RB >= phi || 16 * RB + 16 <= plo || 16 * CB >= phi) continue;   // uniform
-                const int p = 16 * CB + col_l;
-                const int ob_ = p / 3, cb_ = p - 3 * ob_;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int q = 16 * RB + 4 * rg + i;
-                    if (q >= plo && q < phi && q >= p) {
-                        const int oa_ = q / 3, ca_ = q - 3 * oa_;
-                        float v = stage[9 * (oa_ * (oa_ + 1) / 2 + ob_ - kbase) + 3 * ca_ + cb_];
-                        if (q == p) v += s2;
-                        acc[bidx(RB, CB)][i] = v;
-                    }
-                }
-            }
+        assemble(3 * c0, 3 * c1, kbase, !MP);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads done before the next pass / the panel reuse
         c0 = c1;
         if (!MP) break;
@@ -254,22 +261,27 @@ __global__ void __launch_bounds__(256) k_gate_mfma(DevState<float> st, Params<fl
             const float d3 = r3.w - l30 * r3.x - l31 * m31 - l32 * m32;
             if (!(d0 > 0.f) || !(d1 > 0.f) || !(d2 > 0.f) || !(d3 > 0.f)) { fail = true; break; }
             const float e3 = pivot_rcp(d3);
-            const float esel = csel == 0 ? e0 : (csel == 1 ? e1 : (csel == 2 ? e2 : e3));
-            // 3. operands: lane l holds row 16 RB + (l & 15), pivot column l >> 4;
-            //    rows of finished pivots and of blocks past nb are zero
+            // 3. operands: lane l holds row 16 RB + (l & 15), pivot column c = l >> 4:
+            //    W[r][c] = (x L_d^-T)[c] = sum_k x_k (L_d^-1)[c][k] -- this lane's row
+            //    of L_d^-1 is chosen once per step; rows of finished pivots and of
+            //    blocks past nb are zero
+            const float i10 = -l10, i21 = -l21, i32 = -l32;
+            const float i20 = -l20 - l21 * i10, i31 = -l31 - l32 * i21;
+            const float i30 = -l30 - l31 * i10 - l32 * i20;
+            const float g0 = csel == 0 ? 1.f : (csel == 1 ? i10 : (csel == 2 ? i20 : i30));
+            const float g1 = csel == 0 ? 0.f : (csel == 1 ? 1.f : (csel == 2 ? i21 : i31));
+            const float g2 = csel <= 1 ? 0.f : (csel == 2 ? 1.f : i32);
+            const float g3 = csel == 3 ? 1.f : 0.f;
+            const float esel = -(csel == 0 ? e0 : (csel == 1 ? e1 : (csel == 2 ? e2 : e3)));
             float av[NB], bv[NB];
 #pragma unroll
             for (int RB = KB; RB < NB; ++RB) {
                 const int r = 16 * RB + col_l;
                 const F4 x = xr[RB];
-                const float w0 = x.x;
-                const float w1 = x.y - w0 * l10;
-                const float w2 = x.z - w0 * l20 - w1 * l21;
-                const float w3 = x.w - w0 * l30 - w1 * l31 - w2 * l32;
-                float w = csel == 0 ? w0 : (csel == 1 ? w1 : (csel == 2 ? w2 : w3));
+                float w = fmaf(x.w, g3, fmaf(x.z, g2, fmaf(x.y, g1, x.x * g0)));
                 w = (r <= p0 + 3 || RB >= nb) ? 0.f : w;
                 bv[RB] = w;
-                av[RB] = -w * esel;
+                av[RB] = w * esel;
             }
             // 4. trailing rank-4 update of the lower block triangle right of the panel
 #pragma unroll
