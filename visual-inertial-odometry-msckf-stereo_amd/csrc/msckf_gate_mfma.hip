@@ -41,6 +41,9 @@ __host__ __device__ constexpr int gm_area(int Mmax, int capb) {                 
 __host__ __device__ constexpr int gm_wave_floats(int Mmax, int capb) {
     return gm_head(Mmax) + gm_area(Mmax, capb) + ((Mmax + 3) & ~3);
 }
+#ifndef GATE_BIF_BIG
+#define GATE_BIF_BIG 3
+#endif
 __host__ __device__ constexpr int bidx(int rb, int cb) { return rb * (rb + 1) / 2 + cb; }
 
 template <int NB, bool MP>
@@ -149,7 +152,9 @@ __global__ void __launch_bounds__(256) k_gate_mfma(DevState<float> st, Params<fl
     // capb < M (M + 1) / 2; each pass fills the lower Y entries of rows [3 c0, 3 c1).
     const float* P = st.P + (size_t)b * st.Dmax * st.Dmax;
     const int ldp = st.Dmax;
-    constexpr int BIF = MP ? 1 : 2;   // blocks per lane in flight
+    // pair blocks per lane in flight: the Y phase's VGPRs are free up to the
+    // elimination's peak once the accumulators outgrow them (NB >= 5)
+    constexpr int BIF = MP ? 1 : (NB >= 5 ? GATE_BIF_BIG : 2);
     if (MP || !(phases & 1)) assemble(0, 0, 0, true);
     for (int c0 = 0; c0 < ((phases & 1) ? M : 0);) {
         int c1 = c0, nbp = 0;
