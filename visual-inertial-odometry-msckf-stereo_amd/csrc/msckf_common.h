@@ -38,7 +38,8 @@ constexpr int OBS_HX = 0, OBS_V = 24, OBS_W = 36, OBS_QR = 54, OBS_R = 58, OBS_H
 //   UB  6    Hx_i^T r_i - G_i^T g
 // so that the projected block H0 = (Q^T Hx)[3:] satisfies
 //   H0^T H0 = blockdiag_i(Hx_i^T Hx_i) - G^T G,   H0^T r0 = sum_i UB_i.
-constexpr int OBG_G = 0, OBG_DS = 18, OBG_UB = 39, OBG_STRIDE = 48;
+//   CAM  1   the observation's cam slot (exact in fp64)
+constexpr int OBG_G = 0, OBG_DS = 18, OBG_UB = 39, OBG_CAM = 45, OBG_STRIDE = 48;
 
 template <typename T>
 struct Params {

@@ -941,6 +941,7 @@ __global__ void __launch_bounds__(256) k_feature(DevState<T> st, Params<T> prm, 
         for (int c = 0; c < 6; ++c)
             rec[OBG_UB + c] = u6[s][c] - (rec[OBG_G + c] * gr[0] + rec[OBG_G + 6 + c] * gr[1] + rec[OBG_G + 12 + c] * gr[2]);
         for (int e = OBG_UB + 6; e < OBG_STRIDE; ++e) rec[e] = 0;
+        rec[OBG_CAM] = (CT)fb.obs_cam[o0 + i];
         store_pairs(fb.obs_g + (size_t)(o0 + i) * OBG_STRIDE, rec, OBG_STRIDE);
     }
 }
@@ -2523,6 +2524,10 @@ template <typename T>
 void launch_compress(hipStream_t s, const DevState<T>& st, const FeatBatch<T>& fb, const UpdWs<T>& ws) {
     if (update_mode(ws.Cmax) == UPD_QR) {
         launch_compress_qr<T>(s, st, fb, ws);
+        return;
+    }
+    if (update_mode(ws.Cmax) == UPD_CHOL && info_mfma_enabled(st.Nmax)) {
+        launch_info_mfma<T>(s, st, fb, ws);
         return;
     }
     const int nblk = st.Nmax * (st.Nmax + 1) / 2;   // 6x6 cam-pair blocks of A (lower triangle)

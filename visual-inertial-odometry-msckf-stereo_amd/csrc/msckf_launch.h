@@ -111,6 +111,10 @@ template <typename T>
 void launch_select(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const UpdWs<T>&, int row_cap);
 template <typename T>
 void launch_compress(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const UpdWs<T>&);
+// [A | b] assembly on fp64 MFMA tiles (msckf_info_mfma.hip), Cholesky-form update path
+bool info_mfma_enabled(int Nmax);
+template <typename T>
+void launch_info_mfma(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const UpdWs<T>&);
 template <typename T>
 void launch_compress_qr(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const UpdWs<T>&);
 enum UpdateMode { UPD_CHOL = 0, UPD_PCHOL = 1, UPD_QR = 2 };
