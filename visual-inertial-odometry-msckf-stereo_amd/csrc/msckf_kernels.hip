@@ -715,8 +715,9 @@ __device__ __forceinline__ void store_pairs(T* dst, const S* src, int n) {
     }
 }
 
+// (one observation per lane: three waves per SIMD -- 168 VGPRs, a 12-byte spill)
 template <typename T, int S, int OPL>
-__global__ void __launch_bounds__(256) k_feature(DevState<T> st, Params<T> prm, FeatBatch<T> fb,
+__global__ void __launch_bounds__(256, OPL == 1 ? 3 : 1) k_feature(DevState<T> st, Params<T> prm, FeatBatch<T> fb,
                                                  const int* __restrict__ flist, int cnt) {
     using CT = double;
     constexpr int PER = 64 / S;   // features per wavefront, one S-lane segment each
