@@ -62,6 +62,8 @@ struct DBuf {   // grow-only device buffer
 struct msckf_ctx {
     int device = 0, scalar = 8, B = 1, Nmax = 0, Dmax = 0, Cmax = 0;
     hipStream_t stream = nullptr;
+    hipStream_t side = nullptr;                          // Kalman stage A ahead of the feature kernels
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     msckf_config_t cfg{};
     std::vector<int> h_ncams;
     // state
@@ -69,7 +71,7 @@ struct msckf_ctx {
     DBuf<int> ncams, ncams_snap;
     // update workspace
     DBuf<unsigned char> Hthin, Hqr, HP, S, dx, Lc, Vi, Sii, G, Tm, W, Wk;
-    DBuf<int> info;
+    DBuf<int> info, afail;
     // feature batch
     int nf = 0, maxM = 0;
     std::vector<int> h_feat_off;
@@ -133,6 +135,7 @@ UpdWs<T> upd_ws(msckf_ctx* c) {
     w.Cmax = c->Cmax;
     w.Cp = (c->Cmax + 15) & ~15;   // leading dim of Lc / Vi / W (MFMA path pads C to 16)
     w.Lc = reinterpret_cast<KT*>(c->Lc.p);
+    w.afail = c->afail.p;
     w.Vi = reinterpret_cast<KT*>(c->Vi.p);
     w.Sii = reinterpret_cast<KT*>(c->Sii.p);
     w.G = reinterpret_cast<KT*>(c->G.p);
@@ -337,6 +340,17 @@ int run_update_chain(msckf_ctx* c, int row_cap, bool triangulate) {
     Params<T> prm = make_params<T>(c);
     FeatBatch<T> fb = feat_batch<T>(c);
     UpdWs<T> ws = upd_ws<T>(c);
+    // Kalman stage A depends on P only: fork it onto the side stream now, join
+    // before stage B (it overlaps triangulation .. information assembly)
+    const bool a_early = kalman_a_early(c->Cmax);
+    if (a_early) {
+        HIPC(hipEventRecord(c->ev_fork, s));
+        HIPC(hipStreamWaitEvent(c->side, c->ev_fork, 0));
+        c->timer.begin(c->side, "kalman_a");
+        launch_kalman_a_early<T>(c->side, st, ws);
+        c->timer.end(c->side);
+        HIPC(hipEventRecord(c->ev_join, c->side));
+    }
     if (triangulate) {
         c->timer.begin(s, "triangulate");
         launch_triangulate<T>(s, st, prm, fb, c->sc);
@@ -354,7 +368,8 @@ int run_update_chain(msckf_ctx* c, int row_cap, bool triangulate) {
     c->timer.begin(s, "compress");
     launch_compress<T>(s, st, fb, ws);
     c->timer.end(s);
-    launch_kalman<T>(s, st, prm, ws, &c->timer);
+    if (a_early) HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
+    launch_kalman<T>(s, st, prm, ws, &c->timer, a_early);
     HIPC(hipGetLastError());
     return 0;
 }
@@ -397,6 +412,8 @@ int do_create(msckf_ctx* c) {
     HIPC(c->S.ensure(B * c->Cmax * c->Cmax * sizeof(KT)));
     HIPC(c->dx.ensure(B * (c->Dmax + c->Cmax) * sizeof(KT)));
     HIPC(c->info.ensure(4 * B));
+    HIPC(c->afail.ensure(B));
+    HIPC(hipMemset(c->afail.p, 0, B * sizeof(int)));
     if (update_mode(c->Cmax) == UPD_CHOL) {   // Cholesky-form Kalman workspace
         const size_t Cp = (c->Cmax + 15) & ~15, kb = sizeof(KT);
         HIPC(c->Lc.ensure(B * Cp * Cp * kb));
@@ -719,6 +736,13 @@ int msckf_create(const msckf_config_t* cfg, int hip_device, int scalar_bytes, in
         delete c;
         FAIL(-2, "hipStreamCreate: %s", hipGetErrorString(e));
     }
+    e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming);
+    if (e != hipSuccess) {
+        msckf_destroy(c);
+        FAIL(-2, "hipStreamCreate / hipEventCreate: %s", hipGetErrorString(e));
+    }
     int r = DISPATCH(c, do_create, c);
     if (r) {
         msckf_destroy(c);
@@ -732,16 +756,20 @@ int msckf_destroy(msckf_ctx_t* c) {
     if (!c) return 0;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->side) (void)hipStreamSynchronize(c->side);
     for (auto* b : {&c->P, &c->imu, &c->cams, &c->P_snap, &c->imu_snap, &c->cams_snap, &c->Hthin, &c->Hqr, &c->HP, &c->S, &c->Lc, &c->Vi, &c->Sii, &c->G, &c->Tm, &c->W, &c->Wk,
                     &c->dx, &c->obs_z, &c->chi2, &c->p_w, &c->obs_ws, &c->obs_g, &c->tau, &c->ysq, &c->gamma, &c->scratch})
         b->release();
-    for (auto* b : {&c->ncams, &c->ncams_snap, &c->info, &c->feat_filter, &c->feat_off, &c->obs_off, &c->obs_cam,
+    for (auto* b : {&c->ncams, &c->ncams_snap, &c->info, &c->afail, &c->feat_filter, &c->feat_off, &c->obs_off, &c->obs_cam,
                     &c->row_off, &c->iscratch, &c->gate_list, &c->seg_list})
         b->release();
     c->ysq_off.release();
     c->valid.release();
     c->accept.release();
     c->include.release();
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+    if (c->side) (void)hipStreamDestroy(c->side);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return 0;

@@ -106,6 +106,7 @@ struct UpdWs {
     KT* Tm;      // [B][Cmax][Cmax+1]    (s2 I + Lc^T A Lc | Lc^T b), lower
     KT* W;       // [B][Dmax+1][Cp]      rows [Vi ; Lc ; c^T] L_T^-T
     KT* Wk;      // [B][wk_stride]       global-memory factorisation workspace (large windows only)
+    int* afail;  // [B]                  stage A status (1: P_cc not PD), written by every k_kal_a run
     size_t wk_stride;
     int Cp;
 };

@@ -282,11 +282,13 @@ __global__ void __launch_bounds__(64 * NW) k_kal_c16(DevState<T> st, UpdWs<T> ws
 
 // ---- stage A: [P_cc P_ci; P_ic P_ii] in index space [cams (Cp) | IMU (24)] ----
 template <typename T, int NT, int TPL>
-__global__ void __launch_bounds__(NT) k_kal_a(DevState<T> st, UpdWs<T> ws) {
+__global__ void __launch_bounds__(NT) k_kal_a(DevState<T> st, UpdWs<T> ws, int early) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int b = blockIdx.x;
     const int* info = ws.info + 4 * b;
-    if (info[0] == 0) return;
+    // early: launched on the side stream while the feature kernels run, before
+    // k_select has written info -- stage A depends on P only
+    if (!early && info[0] == 0) return;
     const int C = 6 * st.ncams[b], Cp = round4(C);
     const int nrow = (Cp + KW) / 4;
     const T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
@@ -306,7 +308,10 @@ __global__ void __launch_bounds__(NT) k_kal_a(DevState<T> st, UpdWs<T> ws) {
     };
     auto trail = [&](int i, int j, double v) { Sii[(i - Cp) * KW + (j - Cp)] = v; };
     const bool ok = rchol_core<NT, TPL>(nrow, nrow, Cp / 4, reinterpret_cast<double*>(smem_raw), load, panel, trail);
-    if (!ok && threadIdx.x == 0) ws.info[4 * b + 3] = -1;
+    if (threadIdx.x == 0) {
+        ws.afail[b] = ok ? 0 : 1;   // read by k_kal_c1 (info[3] may not exist yet when early)
+        if (!ok && !early) ws.info[4 * b + 3] = -1;
+    }
 }
 
 // ---- stage C: Cholesky of T (Cp) with extra rows [Vc_i (21); Lc (C); c^T] ----
@@ -369,6 +374,10 @@ __global__ void __launch_bounds__(NT) k_kal_c1(DevState<T> st, UpdWs<T> ws) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int b = blockIdx.x;
     if (ws.info[4 * b] == 0) return;
+    if (ws.afail[b]) {   // stage A failed (P_cc not PD): no update for this filter
+        if (threadIdx.x == 0) ws.info[4 * b + 3] = -1;
+        return;
+    }
     const int C = 6 * st.ncams[b], Cp = round4(C), nTc = Cp / 4;
     const int ldt = ws.Cmax + 1;
     const KT* Tm = ws.Tm + (size_t)b * ws.Cmax * ldt;
@@ -1126,8 +1135,8 @@ static bool pick_rchol(int tiles, RcholCfg& c) {
 }
 
 template <typename T, int NT, int TPL>
-static void launch_a_cfg(hipStream_t s, const DevState<T>& st, const UpdWs<T>& ws, size_t lds) {
-    hipLaunchKernelGGL((k_kal_a<T, NT, TPL>), dim3(st.B), dim3(NT), lds, s, st, ws);
+static void launch_a_cfg(hipStream_t s, const DevState<T>& st, const UpdWs<T>& ws, size_t lds, int early = 0) {
+    hipLaunchKernelGGL((k_kal_a<T, NT, TPL>), dim3(st.B), dim3(NT), lds, s, st, ws, early);
 }
 template <typename T, int NT, int TPL>
 static void launch_c_cfg(hipStream_t s, const DevState<T>& st, const UpdWs<T>& ws, int groups, int ner, size_t lds) {
@@ -1256,14 +1265,41 @@ static void launch_b(hipStream_t s, const DevState<T>& st, const Params<T>& prm,
     hipLaunchKernelGGL((k_kal_b<T, NW, WR, WC, NTM>), dim3(st.B), dim3(64 * NW), lds, s, st, prm, ws);
 }
 
+// Stage A (4x4-tile path) can run before the update's feature kernels finish:
+// it reads P only.  With MSCKF_KALMAN_A_EARLY=1 the context forks it onto a
+// side stream at the start of the update chain and joins before stage B.  Off
+// by default: at 2048 x 30x200 the chip is already full -- stage A stretched
+// from 0.82 to 2.8 ms and the gating from 3.5 to 3.7 ms, no net change.
+bool kalman_a_early(int Cmax) {
+    static int en = -1;
+    if (en < 0) {
+        const char* e = getenv("MSCKF_KALMAN_A_EARLY");
+        en = e ? atoi(e) : 0;
+    }
+    return en && update_mode(Cmax) == UPD_CHOL && kalman_chol_supported(Cmax) && !mfma_kalman(Cmax);
+}
+
+template <typename T>
+void launch_kalman_a_early(hipStream_t s, const DevState<T>& st, const UpdWs<T>& ws) {
+    const int Cp = (ws.Cmax + 3) & ~3;
+    const int nrow = (Cp + KW) / 4;
+    RcholCfg c;
+    pick_rchol(nrow * (nrow + 1) / 2, c);
+    const size_t lds = rchol_lds_doubles(nrow) * sizeof(double);
+    if (c.nt == 256) launch_a_cfg<T, 256, 4>(s, st, ws, lds, 1);
+    else launch_a_cfg<T, 512, 4>(s, st, ws, lds, 1);
+}
+
 template <typename T>
 void launch_kalman_chol(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const UpdWs<T>& ws,
-                        KernelTimer* kt) {
+                        KernelTimer* kt, bool a_done) {
     const int Cp = (ws.Cmax + 3) & ~3, Cmax = ws.Cmax;
     const bool mf = mfma_kalman(Cmax);
     const bool glob = !kalman_chol_supported(Cmax);   // large window: global-memory stages A and C
     const int Cq = (Cmax + 15) & ~15;
-    if (glob) {
+    if (a_done) {
+        // stage A already ran on the side stream (launch_kalman_a_early)
+    } else if (glob) {
         kt->begin(s, "kalman_a");
         launch_gchol<0, T>(s, st, ws);
         kt->end(s);
@@ -1364,8 +1400,10 @@ void launch_kalman_chol(hipStream_t s, const DevState<T>& st, const Params<T>& p
 }
 
 template void launch_kalman_chol<float>(hipStream_t, const DevState<float>&, const Params<float>&,
-                                        const UpdWs<float>&, KernelTimer*);
+                                        const UpdWs<float>&, KernelTimer*, bool);
 template void launch_kalman_chol<double>(hipStream_t, const DevState<double>&, const Params<double>&,
-                                         const UpdWs<double>&, KernelTimer*);
+                                         const UpdWs<double>&, KernelTimer*, bool);
+template void launch_kalman_a_early<float>(hipStream_t, const DevState<float>&, const UpdWs<float>&);
+template void launch_kalman_a_early<double>(hipStream_t, const DevState<double>&, const UpdWs<double>&);
 
 }  // namespace msckf

@@ -2539,9 +2539,9 @@ void launch_compress(hipStream_t s, const DevState<T>& st, const FeatBatch<T>& f
 
 template <typename T>
 void launch_kalman(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const UpdWs<T>& ws,
-                   KernelTimer* kt) {
+                   KernelTimer* kt, bool a_done) {
     if (update_mode(ws.Cmax) == UPD_CHOL) {
-        launch_kalman_chol<T>(s, st, prm, ws, kt);
+        launch_kalman_chol<T>(s, st, prm, ws, kt, a_done);
         kt->begin(s, "kalman_correct");
         hipLaunchKernelGGL(k_correct<T>, dim3(st.B), dim3(64), 0, s, st, ws);
         kt->end(s);
@@ -2584,7 +2584,7 @@ void launch_kalman(hipStream_t s, const DevState<T>& st, const Params<T>& prm, c
     template void launch_gate<T>(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&, const GateClasses&); \
     template void launch_select<T>(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const UpdWs<T>&, int); \
     template void launch_compress<T>(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const UpdWs<T>&); \
-    template void launch_kalman<T>(hipStream_t, const DevState<T>&, const Params<T>&, const UpdWs<T>&, KernelTimer*);
+    template void launch_kalman<T>(hipStream_t, const DevState<T>&, const Params<T>&, const UpdWs<T>&, KernelTimer*, bool);
 INSTANTIATE(float)
 INSTANTIATE(double)
 

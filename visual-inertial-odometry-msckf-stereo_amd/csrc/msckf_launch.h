@@ -123,8 +123,14 @@ bool feature_needs_compact(int maxM, int Cmax);
 bool kalman_chol_supported(int Cmax);
 size_t kalman_global_ws_doubles(int Cmax);
 template <typename T>
-void launch_kalman_chol(hipStream_t, const DevState<T>&, const Params<T>&, const UpdWs<T>&, KernelTimer*);
+void launch_kalman_chol(hipStream_t, const DevState<T>&, const Params<T>&, const UpdWs<T>&, KernelTimer*,
+                        bool a_done = false);
 template <typename T>
-void launch_kalman(hipStream_t, const DevState<T>&, const Params<T>&, const UpdWs<T>&, KernelTimer*);
+void launch_kalman(hipStream_t, const DevState<T>&, const Params<T>&, const UpdWs<T>&, KernelTimer*,
+                   bool a_done = false);
+// Kalman stage A ahead of the feature kernels on a side stream (msckf_kalman.hip)
+bool kalman_a_early(int Cmax);
+template <typename T>
+void launch_kalman_a_early(hipStream_t, const DevState<T>&, const UpdWs<T>&);
 
 }  // namespace msckf
