@@ -14,6 +14,6 @@ for line in sys.stdin:
         k, v = line.rsplit(":", 1); cur[k.strip()] = v.strip()
 names = subprocess.run(["c++filt"], input="\n".join(r["name"] for r in rows), capture_output=True, text=True).stdout.split("\n")
 for r, n in zip(rows, names):
-    n = re.sub(r"\(.*", "", n).replace("msckf::", "").replace("void ", "")
+    n = re.sub(r"\(.*", "", n.replace("(anonymous namespace)::", "")).replace("msckf::", "").replace("void ", "")
     print("%-26s vgpr=%-4s agpr=%-4s scratch=%-5s lds=%-6s occ=%s" % (n, r.get("VGPRs"), r.get("AGPRs"), r.get("ScratchSize [bytes/lane]"), r.get("LDS Size [bytes/block]"), r.get("Occupancy [waves/SIMD]")))
 '

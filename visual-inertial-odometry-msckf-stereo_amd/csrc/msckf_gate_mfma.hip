@@ -323,6 +323,252 @@ __global__ void __launch_bounds__(256) k_gate_mfma(DevState<float> st, Params<fl
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// Large tracks (40 < M <= 82, nb <= 16 blocks): the same MFMA elimination on a
+// workgroup of four waves per feature.  Wave w owns block rows RB = w + 4 i
+// (i < 4) -- at most 40 accumulator blocks (acc row i holds blocks 0..4 i + 3).
+// Per 4-pivot step the owners of the pivot columns dump them to a
+// double-buffered LDS panel, one barrier, then every wave factors the 4x4
+// diagonal, forms the B operands of every block row and the A operands of its
+// own rows, and updates its blocks.  The Y pairs are staged in passes over
+// observation rows by all 256 threads, each pass followed by the owners'
+// assembly.  (Replaces k_gate_big's fp64 register tiles in the fp32 contexts.)
+constexpr int GW_NB = 16;
+__host__ __device__ constexpr int gw_off(int i) { return 2 * i * (i + 1); }
+__host__ __device__ constexpr int gw_pan() { return 2 * 16 * GW_NB * 4; }   // floats, double-buffered
+__host__ __device__ constexpr int gw_floats(int Mmax, int capb) {
+    return gm_head(Mmax) + gw_pan() + ((9 * capb + 3) & ~3) + ((Mmax + 3) & ~3);
+}
+
+__global__ void __launch_bounds__(256) k_gate_mfma_wg(DevState<float> st, Params<float> prm, FeatBatch<float> fb,
+                                                      const int* __restrict__ flist, int Mmax, int capb) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int f = __builtin_amdgcn_readfirstlane(flist[blockIdx.x]);
+    if (!fb.valid[f]) {
+        if (tid == 0) { fb.gamma[f] = NAN; fb.accept[f] = 0; }
+        return;
+    }
+    const int b = __builtin_amdgcn_readfirstlane(fb.feat_filter[f]);
+    const int o0 = __builtin_amdgcn_readfirstlane(fb.obs_off[f]);
+    const int M = __builtin_amdgcn_readfirstlane(fb.obs_off[f + 1]) - o0, M3 = 3 * M;
+    const int nY = (M3 + 3) >> 2;
+    const int nb = gm_nb(M);
+    const int nB = 16 * nb - 4;
+    float* ht = reinterpret_cast<float*>(smem_raw);
+    float* rt = ht + 18 * Mmax;
+    float* pan = ht + gm_head(Mmax);               // [2][16 GW_NB][4]
+    float* stage = pan + gw_pan();                 // [capb][9]
+    int* slot = reinterpret_cast<int*>(stage + ((9 * capb + 3) & ~3));
+    const float* ws = fb.obs_ws + (size_t)o0 * OBS_WS;
+    for (int e = tid; e < 18 * M; e += 256) {
+        const int o = e / 18;
+        ht[e] = ws[(size_t)o * OBS_WS + OBS_HT + (e - 18 * o)];
+    }
+    for (int e = tid; e < 4 * M; e += 256) rt[e] = ws[(size_t)(e >> 2) * OBS_WS + OBS_RT + (e & 3)];
+    for (int i = tid; i < M; i += 256) slot[i] = fb.obs_cam[o0 + i];
+    __syncthreads();
+    float rn2 = 0;
+    for (int e = 4 * lane + 3; e < 4 * M; e += 256) rn2 += rt[e] * rt[e];
+    rn2 = wave_sum(rn2);
+
+    const int col_l = lane & 15, rg = lane >> 4;
+    F4 acc[gw_off(4)];
+    const float s2 = prm.sigma2;
+    // as k_gate_mfma's assemble, over this wave's blocks (RB = w + 4 i, CB = c <= RB)
+    auto assemble = [&](int plo, int phi, int kbase, bool first) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int RB = w + 4 * i;
+            if (RB >= nb) continue;
+            if (!first && (16 * RB >= phi || 16 * RB + 16 <= plo)) continue;
+            const bool brow = RB == nb - 1 && rg == 3;
+            int rofs[4];
+            bool qy[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int q = 16 * RB + 4 * rg + r, oa = q / 3;
+                rofs[r] = 9 * (oa * (oa + 1) / 2 - kbase) + 3 * (q - 3 * oa);
+                qy[r] = q >= plo && q < phi;
+            }
+#pragma unroll
+            for (int c = 0; c < 4 * i + 4; ++c) {
+                if (c > RB) continue;
+                const int p = 16 * c + col_l, ob = p / 3, cp = p - 3 * ob;
+                float bval[4] = {0.f, 0.f, 0.f, 0.f};
+                if (first && RB == nb - 1) {
+                    const bool pv = brow && p < M3;
+                    const int o = pv ? ob : 0;
+#pragma unroll
+                    for (int r = 0; r < 3; ++r) bval[r] = pv ? -ht[18 * o + 6 * cp + 3 + r] : 0.f;
+                    bval[3] = pv ? rt[4 * o + cp] : 0.f;
+                }
+                F4& a = acc[gw_off(i) + c];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int q = 16 * RB + 4 * rg + r;
+                    const bool take = qy[r] && q >= p;
+                    const float y = stage[take ? rofs[r] + 9 * ob + cp : 0];
+                    float v = first ? bval[r] : a[r];
+                    if (first && q == p && q >= M3 && q < nB) v = 1.f;
+                    v = take ? y + (q == p ? s2 : 0.f) : v;
+                    a[r] = v;
+                }
+                asm volatile("" : "+a"(a));
+            }
+        }
+    };
+
+    assemble(0, 0, 0, true);
+    const float* P = st.P + (size_t)b * st.Dmax * st.Dmax;
+    const int ldp = st.Dmax;
+    for (int c0 = 0; c0 < M;) {
+        int c1 = c0, nbp = 0;
+        while (c1 < M && (c1 == c0 || nbp + (c1 + 1) <= capb)) { nbp += c1 + 1; ++c1; }
+        const int kbase = c0 * (c0 + 1) / 2;
+        for (int kk = tid; kk < nbp; kk += 256) {
+            const int k = kbase + kk;
+            int a = (int)((sqrtf(8.0f * (float)k + 1.0f) - 1.0f) * 0.5f);
+            if (a * (a + 1) / 2 > k) --a;
+            if ((a + 1) * (a + 2) / 2 <= k) ++a;
+            const int bo = k - a * (a + 1) / 2;
+            const float* Pb = P + (size_t)(21 + 6 * slot[a]) * ldp + 21 + 6 * slot[bo];
+            float Pl[36];
+#pragma unroll
+            for (int u = 0; u < 6; ++u) __builtin_memcpy(Pl + 6 * u, Pb + (size_t)u * ldp, 6 * sizeof(float));
+            const float* Ha = ht + 18 * a;
+            const float* Hb = ht + 18 * bo;
+            float* dst = stage + 9 * kk;
+#pragma unroll
+            for (int x = 0; x < 3; ++x) {
+                F2 t2[3] = {F2{0, 0}, F2{0, 0}, F2{0, 0}};
+#pragma unroll
+                for (int u = 0; u < 6; ++u) {
+                    const float h = Ha[6 * x + u];
+#pragma unroll
+                    for (int c = 0; c < 3; ++c)
+                        t2[c] = __builtin_elementwise_fma(F2{h, h}, F2{Pl[6 * u + 2 * c], Pl[6 * u + 2 * c + 1]}, t2[c]);
+                }
+                const float t1[6] = {t2[0].x, t2[0].y, t2[1].x, t2[1].y, t2[2].x, t2[2].y};
+#pragma unroll
+                for (int y = 0; y < 3; ++y) {
+                    float acc_y = 0;
+#pragma unroll
+                    for (int u = 0; u < 6; ++u) acc_y = fmaf(t1[u], Hb[6 * y + u], acc_y);
+                    dst[3 * x + y] = acc_y;
+                }
+            }
+        }
+        __syncthreads();
+        assemble(3 * c0, 3 * c1, kbase, false);
+        __syncthreads();
+        c0 = c1;
+    }
+
+    bool fail = false;
+    const int csel = rg;
+#pragma unroll
+    for (int KB = 0; KB < GW_NB; ++KB) {
+        if (4 * KB >= nY || fail) break;
+        for (int sc = 0; sc < 4; ++sc) {
+            const int j = 4 * KB + sc;
+            if (j >= nY) break;
+            const int p0 = 4 * j;
+            float* pb = pan + (j & 1) * (16 * GW_NB * 4);
+            if ((col_l >> 2) == sc) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    if (KB >= 4 * i + 4) continue;   // no block (RB, KB) in acc row i (compile time)
+                    const int RB = w + 4 * i;
+                    if (RB < KB || RB >= nb) continue;
+                    const F4 v = acc[gw_off(i) + KB];
+                    float* dd = pb + 4 * (16 * RB + 4 * rg) + (col_l & 3);
+                    dd[0] = v[0]; dd[4] = v[1]; dd[8] = v[2]; dd[12] = v[3];
+                }
+            }
+            LDS_BARRIER();
+            const F4 r0 = *reinterpret_cast<const F4*>(pb + 4 * p0);
+            const F4 r1 = *reinterpret_cast<const F4*>(pb + 4 * p0 + 4);
+            const F4 r2 = *reinterpret_cast<const F4*>(pb + 4 * p0 + 8);
+            const F4 r3 = *reinterpret_cast<const F4*>(pb + 4 * p0 + 12);
+            F4 xr[GW_NB];
+#pragma unroll
+            for (int CB = KB; CB < GW_NB; ++CB) xr[CB] = *reinterpret_cast<const F4*>(pb + 4 * (16 * CB + col_l));
+            F4 xo[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) xo[i] = *reinterpret_cast<const F4*>(pb + 4 * (16 * (w + 4 * i) + col_l));
+            const float d0 = r0.x, e0 = pivot_rcp(d0);
+            const float l10 = r1.x * e0, l20 = r2.x * e0, l30 = r3.x * e0;
+            const float d1 = r1.y - l10 * r1.x, e1 = pivot_rcp(d1);
+            const float m21 = r2.y - l20 * r1.x, m31 = r3.y - l30 * r1.x;
+            const float l21 = m21 * e1, l31 = m31 * e1;
+            const float d2 = r2.z - l20 * r2.x - l21 * m21, e2 = pivot_rcp(d2);
+            const float m32 = r3.z - l30 * r2.x - l31 * m21;
+            const float l32 = m32 * e2;
+            const float d3 = r3.w - l30 * r3.x - l31 * m31 - l32 * m32;
+            if (!(d0 > 0.f) || !(d1 > 0.f) || !(d2 > 0.f) || !(d3 > 0.f)) { fail = true; break; }   // same in every wave
+            const float e3 = pivot_rcp(d3);
+            const float i10 = -l10, i21 = -l21, i32 = -l32;
+            const float i20 = -l20 - l21 * i10, i31 = -l31 - l32 * i21;
+            const float i30 = -l30 - l31 * i10 - l32 * i20;
+            const float g0 = csel == 0 ? 1.f : (csel == 1 ? i10 : (csel == 2 ? i20 : i30));
+            const float g1 = csel == 0 ? 0.f : (csel == 1 ? 1.f : (csel == 2 ? i21 : i31));
+            const float g2 = csel <= 1 ? 0.f : (csel == 2 ? 1.f : i32);
+            const float g3 = csel == 3 ? 1.f : 0.f;
+            const float esel = -(csel == 0 ? e0 : (csel == 1 ? e1 : (csel == 2 ? e2 : e3)));
+            float bv[GW_NB];
+#pragma unroll
+            for (int CB = KB; CB < GW_NB; ++CB) {
+                const F4 x = xr[CB];
+                const float wv = fmaf(x.w, g3, fmaf(x.z, g2, fmaf(x.y, g1, x.x * g0)));
+                bv[CB] = (16 * CB + col_l <= p0 + 3 || CB >= nb) ? 0.f : wv;
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int RB = w + 4 * i;
+                if (RB < KB || RB >= nb) continue;   // uniform
+                const F4 x = xo[i];
+                const float wv = fmaf(x.w, g3, fmaf(x.z, g2, fmaf(x.y, g1, x.x * g0)));
+                const float av = (16 * RB + col_l <= p0 + 3) ? 0.f : wv * esel;
+#pragma unroll
+                for (int c = KB; c < 4 * i + 4; ++c)
+                    if (c <= RB)
+                        acc[gw_off(i) + c] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[c], acc[gw_off(i) + c], 0, 0, 0);
+            }
+        }
+    }
+    // the B rows' 4x4 Schur block: block (nb-1, nb-1), owned by wave (nb-1) % 4
+    float* fin = pan;
+    LDS_BARRIER();
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int c = 0; c < 4 * i + 4; ++c)
+            if (w + 4 * i == nb - 1 && c == nb - 1 && rg == 3 && col_l >= 12) {
+                const F4 v = acc[gw_off(i) + c];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) fin[4 * r + (col_l - 12)] = v[r];
+            }
+    LDS_BARRIER();
+    if (tid == 0) {
+        const float* a = fin;
+        const float d0 = a[0];
+        const float l10 = a[4] / d0, l20 = a[8] / d0, l30 = a[12] / d0;
+        const float d1 = a[5] - l10 * l10 * d0;
+        const float l21 = (a[9] - l20 * l10 * d0) / d1;
+        const float l31 = (a[13] - l30 * l10 * d0) / d1;
+        const float d2 = a[10] - l20 * l20 * d0 - l21 * l21 * d1;
+        const float l32 = (a[14] - l30 * l20 * d0 - l31 * l21 * d1) / d2;
+        const float d3 = a[15] - l30 * l30 * d0 - l31 * l31 * d1 - l32 * l32 * d2;
+        float gam = -d3 + rn2 / s2;
+        if (fail || !(d0 < 0.f) || !(d1 < 0.f) || !(d2 < 0.f) || !(gam == gam)) gam = INFINITY;
+        fb.gamma[f] = gam;
+        fb.accept[f] = (gam < fb.chi2[f]) ? 1 : 0;
+    }
+}
+
 template <int NB, bool MP>
 void launch_cfg(hipStream_t s, const DevState<float>& st, const Params<float>& prm, const FeatBatch<float>& fb,
                 const int* list, int cnt, int Mmax, int capb, int wpb, size_t lds) {
@@ -367,6 +613,25 @@ void launch_nb(hipStream_t s, const DevState<float>& st, const Params<float>& pr
 }  // namespace
 
 bool gate_mfma_fits(int maxM) { return maxM >= 1 && gm_nb(maxM) <= 8; }
+bool gate_mfma_wg_fits(int maxM) { return maxM >= 1 && gm_nb(maxM) <= GW_NB; }
+
+void launch_gate_mfma_wg(hipStream_t s, const DevState<float>& st, const Params<float>& prm,
+                         const FeatBatch<float>& fb, const int* list, int cnt, int maxM) {
+    if (cnt <= 0) return;
+    // LDS for two workgroups per CU: the Y pairs staged in as many passes as that needs
+    const int fixed = gm_head(maxM) + gw_pan() + ((maxM + 3) & ~3) + 4;
+    int capb = ((78 * 1024) / (int)sizeof(float) - fixed) / 9;
+    const int nbk = maxM * (maxM + 1) / 2;
+    if (capb > nbk) capb = nbk;
+    if (capb < maxM) capb = maxM;
+    const size_t lds = (size_t)gw_floats(maxM, capb) * sizeof(float);
+    static size_t attr = 64 * 1024;
+    if (lds > attr) {
+        (void)hipFuncSetAttribute((const void*)k_gate_mfma_wg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr = lds;
+    }
+    hipLaunchKernelGGL(k_gate_mfma_wg, dim3(cnt), dim3(256), lds, s, st, prm, fb, list, maxM, capb);
+}
 
 void launch_gate_mfma(hipStream_t s, const DevState<float>& st, const Params<float>& prm, const FeatBatch<float>& fb,
                       const int* list, int cnt, int maxM) {

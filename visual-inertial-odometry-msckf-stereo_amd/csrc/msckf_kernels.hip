@@ -2433,6 +2433,10 @@ void launch_gate(hipStream_t s, const DevState<T>& st, const Params<T>& prm, con
                 launch_gate_mfma(s, st, prm, fb, list, cnt, maxM);
                 continue;
             }
+            if (mode == 0 && c == GateClasses::NC - 2 && gate_mfma_wg_fits(maxM)) {
+                launch_gate_mfma_wg(s, st, prm, fb, list, cnt, maxM);
+                continue;
+            }
         }
         if (mode != 1 && c == GateClasses::NC - 2) {   // 40 < M <= 82: register tiles, one workgroup per feature
             const int nrow = gate_nt(maxM), tiles = nrow * (nrow + 1) / 2;

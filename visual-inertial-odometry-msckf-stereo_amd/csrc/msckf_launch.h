@@ -107,6 +107,10 @@ void launch_gate(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBa
 bool gate_mfma_fits(int maxM);
 void launch_gate_mfma(hipStream_t, const DevState<float>&, const Params<float>&, const FeatBatch<float>&,
                       const int* list, int cnt, int maxM);
+// fp32 gating of large tracks (40 < M <= 82) on MFMA tiles, one 4-wave workgroup per feature
+bool gate_mfma_wg_fits(int maxM);
+void launch_gate_mfma_wg(hipStream_t, const DevState<float>&, const Params<float>&, const FeatBatch<float>&,
+                         const int* list, int cnt, int maxM);
 template <typename T>
 void launch_select(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const UpdWs<T>&, int row_cap);
 template <typename T>
