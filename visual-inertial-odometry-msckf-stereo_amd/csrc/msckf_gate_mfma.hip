@@ -377,57 +377,71 @@ __global__ void __launch_bounds__(256) k_gate_mfma_wg(DevState<float> st, Params
     const int col_l = lane & 15, rg = lane >> 4;
     F4 acc[gw_off(4)];
     const float s2 = prm.sigma2;
-    // as k_gate_mfma's assemble, over this wave's blocks (RB = w + 4 i, CB = c <= RB)
-    auto assemble = [&](int plo, int phi, int kbase, bool first) {
+    // Assembly of this wave's blocks (RB = w + 4 i, CB = c <= RB) whose block
+    // row lies in [R0, R1): every element written once, as in k_gate_mfma --
+    // Y entries from the pass's pair stage (kbase = its first pair), B rows,
+    // unit padding pivots, zeros.  The Y passes are aligned to block rows, so
+    // no accumulator is ever read back (a read-modify-write kept ~100 of them
+    // live in VGPRs across the pass loop).
+    auto assemble = [&](int R0, int R1, int kbase) {
+        // opaque copies: the index arithmetic stays inside the pass loop
+        int col_l = lane & 15, rg = lane >> 4;
+        asm volatile("" : "+v"(col_l), "+v"(rg));
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int RB = w + 4 * i;
-            if (RB >= nb) continue;
-            if (!first && (16 * RB >= phi || 16 * RB + 16 <= plo)) continue;
+            if (RB >= nb || RB < R0 || RB >= R1) continue;
             const bool brow = RB == nb - 1 && rg == 3;
             int rofs[4];
-            bool qy[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int q = 16 * RB + 4 * rg + r, oa = q / 3;
                 rofs[r] = 9 * (oa * (oa + 1) / 2 - kbase) + 3 * (q - 3 * oa);
-                qy[r] = q >= plo && q < phi;
             }
 #pragma unroll
             for (int c = 0; c < 4 * i + 4; ++c) {
                 if (c > RB) continue;
                 const int p = 16 * c + col_l, ob = p / 3, cp = p - 3 * ob;
                 float bval[4] = {0.f, 0.f, 0.f, 0.f};
-                if (first && RB == nb - 1) {
+                if (RB == nb - 1) {
                     const bool pv = brow && p < M3;
                     const int o = pv ? ob : 0;
 #pragma unroll
                     for (int r = 0; r < 3; ++r) bval[r] = pv ? -ht[18 * o + 6 * cp + 3 + r] : 0.f;
                     bval[3] = pv ? rt[4 * o + cp] : 0.f;
                 }
-                F4& a = acc[gw_off(i) + c];
+                F4 a;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int q = 16 * RB + 4 * rg + r;
-                    const bool take = qy[r] && q >= p;
+                    const bool take = q < M3 && q >= p;
                     const float y = stage[take ? rofs[r] + 9 * ob + cp : 0];
-                    float v = first ? bval[r] : a[r];
-                    if (first && q == p && q >= M3 && q < nB) v = 1.f;
-                    v = take ? y + (q == p ? s2 : 0.f) : v;
-                    a[r] = v;
+                    float v = bval[r];
+                    if (q == p && q >= M3 && q < nB) v = 1.f;
+                    a[r] = take ? y + (q == p ? s2 : 0.f) : v;
                 }
-                asm volatile("" : "+a"(a));
+                acc[gw_off(i) + c] = a;
+                asm volatile("" : "+a"(acc[gw_off(i) + c]));
             }
         }
     };
 
-    assemble(0, 0, 0, true);
     const float* P = st.P + (size_t)b * st.Dmax * st.Dmax;
     const int ldp = st.Dmax;
-    for (int c0 = 0; c0 < M;) {
-        int c1 = c0, nbp = 0;
-        while (c1 < M && (c1 == c0 || nbp + (c1 + 1) <= capb)) { nbp += c1 + 1; ++c1; }
-        const int kbase = c0 * (c0 + 1) / 2;
+    // Y passes over block rows [R0, R1): the pairs of observation rows
+    // [16 R0 / 3, (16 R1 - 1) / 3] (rows straddling a pass boundary twice)
+    for (int R0 = 0; R0 < nb;) {
+        const int alo = (16 * R0) / 3;
+        int R1 = R0 + 1, ahi = min(M - 1, (16 * R1 - 1) / 3);
+        auto npairs = [&](int lo, int hi) { return hi < lo ? 0 : (hi * (hi + 1) / 2 + hi + 1) - lo * (lo + 1) / 2; };
+        while (R1 < nb) {
+            const int ah2 = min(M - 1, (16 * (R1 + 1) - 1) / 3);
+            if (npairs(alo, ah2) > capb) break;
+            ++R1;
+            ahi = ah2;
+        }
+        const int kbase = alo * (alo + 1) / 2, nbp = npairs(alo, ahi);
+#pragma unroll 1
         for (int kk = tid; kk < nbp; kk += 256) {
             const int k = kbase + kk;
             int a = (int)((sqrtf(8.0f * (float)k + 1.0f) - 1.0f) * 0.5f);
@@ -462,9 +476,9 @@ __global__ void __launch_bounds__(256) k_gate_mfma_wg(DevState<float> st, Params
             }
         }
         __syncthreads();
-        assemble(3 * c0, 3 * c1, kbase, false);
+        assemble(R0, R1, kbase);
         __syncthreads();
-        c0 = c1;
+        R0 = R1;
     }
 
     bool fail = false;
@@ -493,12 +507,6 @@ __global__ void __launch_bounds__(256) k_gate_mfma_wg(DevState<float> st, Params
             const F4 r1 = *reinterpret_cast<const F4*>(pb + 4 * p0 + 4);
             const F4 r2 = *reinterpret_cast<const F4*>(pb + 4 * p0 + 8);
             const F4 r3 = *reinterpret_cast<const F4*>(pb + 4 * p0 + 12);
-            F4 xr[GW_NB];
-#pragma unroll
-            for (int CB = KB; CB < GW_NB; ++CB) xr[CB] = *reinterpret_cast<const F4*>(pb + 4 * (16 * CB + col_l));
-            F4 xo[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) xo[i] = *reinterpret_cast<const F4*>(pb + 4 * (16 * (w + 4 * i) + col_l));
             const float d0 = r0.x, e0 = pivot_rcp(d0);
             const float l10 = r1.x * e0, l20 = r2.x * e0, l30 = r3.x * e0;
             const float d1 = r1.y - l10 * r1.x, e1 = pivot_rcp(d1);
@@ -518,18 +526,20 @@ __global__ void __launch_bounds__(256) k_gate_mfma_wg(DevState<float> st, Params
             const float g2 = csel <= 1 ? 0.f : (csel == 2 ? 1.f : i32);
             const float g3 = csel == 3 ? 1.f : 0.f;
             const float esel = -(csel == 0 ? e0 : (csel == 1 ? e1 : (csel == 2 ? e2 : e3)));
+            // B operands of every block row, four panel rows in flight at a time (VGPR budget)
             float bv[GW_NB];
 #pragma unroll
             for (int CB = KB; CB < GW_NB; ++CB) {
-                const F4 x = xr[CB];
+                const F4 x = *reinterpret_cast<const F4*>(pb + 4 * (16 * CB + col_l));
                 const float wv = fmaf(x.w, g3, fmaf(x.z, g2, fmaf(x.y, g1, x.x * g0)));
                 bv[CB] = (16 * CB + col_l <= p0 + 3 || CB >= nb) ? 0.f : wv;
+                if ((CB & 3) == 3) __builtin_amdgcn_sched_barrier(0);
             }
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int RB = w + 4 * i;
                 if (RB < KB || RB >= nb) continue;   // uniform
-                const F4 x = xo[i];
+                const F4 x = *reinterpret_cast<const F4*>(pb + 4 * (16 * RB + col_l));
                 const float wv = fmaf(x.w, g3, fmaf(x.z, g2, fmaf(x.y, g1, x.x * g0)));
                 const float av = (16 * RB + col_l <= p0 + 3) ? 0.f : wv * esel;
 #pragma unroll
@@ -623,7 +633,7 @@ void launch_gate_mfma_wg(hipStream_t s, const DevState<float>& st, const Params<
     int capb = ((78 * 1024) / (int)sizeof(float) - fixed) / 9;
     const int nbk = maxM * (maxM + 1) / 2;
     if (capb > nbk) capb = nbk;
-    if (capb < maxM) capb = maxM;
+    if (capb < 6 * maxM) capb = 6 * maxM;   // one block row (up to six observation rows) per pass at least
     const size_t lds = (size_t)gw_floats(maxM, capb) * sizeof(float);
     static size_t attr = 64 * 1024;
     if (lds > attr) {
