@@ -91,54 +91,56 @@ __global__ void __launch_bounds__(256) k_gate_mfma(DevState<float> st, Params<fl
     const int col_l = lane & 15, rg = lane >> 4;
     constexpr int NBLK = NB * (NB + 1) / 2;
     F4 acc[NBLK];
-    // Matrix assembly into the C-layout blocks.  Every element is written once
-    // per call: Y entries of rows [plo, phi) from the pair-block stage (lower
-    // entries, s2 on the diagonal), and on the first call the rest -- B rows
-    // [H_f~^T ; r~^T] (H_f~ = -Ht[:, 3:6]) in rows 12..15 of block nb - 1, unit
-    // padding pivots, zeros.  The stage offset of Y[q][p] separates into a row
-    // part and a column part: 9 (a (a + 1) / 2 + b) + 3 c_q + c_p with a = q / 3,
-    // b = p / 3.  (phases: profiling aid, bit0 Y, bit2 elimination; without the
-    // Y phase the range rows get unit pivots so that the elimination still runs.)
+    // Matrix assembly into the C-layout blocks of block rows [R0, R1): every
+    // element written exactly once -- Y entries (lower, s2 on the diagonal) from
+    // the pass's pair stage (kbase = its first pair), B rows [H_f~^T ; r~^T]
+    // (H_f~ = -Ht[:, 3:6]) in rows 12..15 of block nb - 1, unit padding pivots,
+    // zeros.  The stage offset of Y[q][p] separates into a row part and a
+    // column part: 9 (a (a + 1) / 2 + b) + 3 c_q + c_p with a = q / 3, b = p / 3.
+    // (phases: profiling aid, bit0 Y, bit2 elimination; without the Y phase the
+    // range rows get unit pivots so that the elimination still runs.)
     const int pad_lo = (phases & 1) ? M3 : 0;
     const float s2 = prm.sigma2;
-    auto assemble = [&](int plo, int phi, int kbase, bool first) {
+    auto assemble = [&](int R0, int R1, int kbase) {
+        int col_l = lane & 15, rg = lane >> 4;   // opaque copies: index math stays in the pass loop
+        asm volatile("" : "+v"(col_l), "+v"(rg));
 #pragma unroll
         for (int RB = 0; RB < NB; ++RB) {
-            if (!first && (16 * RB >= phi || 16 * RB + 16 <= plo)) continue;   // uniform
+            if (RB < R0 || RB >= R1) continue;   // uniform
             const bool brow = RB == nb - 1 && rg == 3;   // this lane's 4 rows are the B rows
             int rofs[4];
-            bool qy[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int q = 16 * RB + 4 * rg + i, oa = q / 3;
                 rofs[i] = 9 * (oa * (oa + 1) / 2 - kbase) + 3 * (q - 3 * oa);
-                qy[i] = q >= plo && q < phi;
             }
 #pragma unroll
             for (int CB = 0; CB <= RB; ++CB) {
                 const int p = 16 * CB + col_l, ob = p / 3, cp = p - 3 * ob;
                 float bval[4] = {0.f, 0.f, 0.f, 0.f};
-                if (first && RB == nb - 1) {   // uniform
+                if (RB == nb - 1) {   // uniform
                     const bool pv = brow && p < M3;
                     const int o = pv ? ob : 0;
 #pragma unroll
                     for (int i = 0; i < 3; ++i) bval[i] = pv ? -ht[18 * o + 6 * cp + 3 + i] : 0.f;
                     bval[3] = pv ? rt[4 * o + cp] : 0.f;
                 }
+                F4 a;
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     const int q = 16 * RB + 4 * rg + i;
-                    const bool take = qy[i] && (RB > CB || q >= p);
+                    const bool take = q < pad_lo && (RB > CB || q >= p);
                     const float y = stage[take ? rofs[i] + 9 * ob + cp : 0];
-                    float v = acc[bidx(RB, CB)][i];
-                    if (first) {
-                        v = bval[i];
-                        if (RB == CB) v = (q == p && q >= pad_lo && q < nB) ? 1.f : v;
+                    float v = bval[i];
+                    if (RB == CB) {
+                        v = (q == p && q >= pad_lo && q < nB) ? 1.f : v;
+                        v = take ? y + (q == p ? s2 : 0.f) : v;
+                    } else {
+                        v = take ? y : v;
                     }
-                    if (RB == CB) v = take ? y + (q == p ? s2 : 0.f) : v;
-                    else v = take ? y : v;
-                    acc[bidx(RB, CB)][i] = v;
+                    a[i] = v;
                 }
+                acc[bidx(RB, CB)] = a;
                 asm volatile("" : "+a"(acc[bidx(RB, CB)]));   // finished block -> AGPRs now (VGPR budget)
             }
         }
@@ -148,18 +150,26 @@ __global__ void __launch_bounds__(256) k_gate_mfma(DevState<float> st, Params<fl
     // row-major lower order k = a (a + 1) / 2 + b -- consecutive lanes take
     // consecutive b of one row a, so a load instruction reads consecutive 24-byte
     // row segments of P (cams of a track are usually consecutive slots) instead
-    // of 64 scattered blocks -- in passes over observation rows [c0, c1) when
-    // capb < M (M + 1) / 2; each pass fills the lower Y entries of rows [3 c0, 3 c1).
+    // of 64 scattered blocks.  When capb < M (M + 1) / 2 the pairs are staged in
+    // passes aligned to block rows [R0, R1) (observation rows [16 R0 / 3,
+    // (16 R1 - 1) / 3], those straddling a boundary twice), so that every
+    // accumulator block is assembled once, never read back.
     const float* P = st.P + (size_t)b * st.Dmax * st.Dmax;
     const int ldp = st.Dmax;
     // pair blocks per lane in flight: the Y phase's VGPRs are free up to the
     // elimination's peak once the accumulators outgrow them (NB >= 5)
     constexpr int BIF = MP ? 1 : (NB >= 5 ? GATE_BIF_BIG : 2);
-    if (MP || !(phases & 1)) assemble(0, 0, 0, true);
-    for (int c0 = 0; c0 < ((phases & 1) ? M : 0);) {
-        int c1 = c0, nbp = 0;
-        while (c1 < M && (c1 == c0 || nbp + (c1 + 1) <= capb)) { nbp += c1 + 1; ++c1; }
-        const int kbase = c0 * (c0 + 1) / 2;
+    auto npairs = [&](int lo, int hi) { return hi < lo ? 0 : (hi + 1) * (hi + 2) / 2 - lo * (lo + 1) / 2; };
+    for (int R0 = 0; R0 < nb;) {
+        const int alo = (16 * R0) / 3;
+        int R1 = R0 + 1, ahi = min(M - 1, (16 * R1 - 1) / 3);
+        while (R1 < nb) {
+            const int ah2 = min(M - 1, (16 * (R1 + 1) - 1) / 3);
+            if (npairs(alo, ah2) > capb) break;
+            ++R1;
+            ahi = ah2;
+        }
+        const int kbase = alo * (alo + 1) / 2, nbp = (phases & 1) ? npairs(alo, ahi) : 0;
         for (int k0 = 0; k0 < nbp; k0 += 64 * BIF) {
             float Pl[BIF][36];
             int oa[BIF], ob[BIF];
@@ -219,9 +229,9 @@ __global__ void __launch_bounds__(256) k_gate_mfma(DevState<float> st, Params<fl
             }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // one wave: its stores are visible to all lanes
-        assemble(3 * c0, 3 * c1, kbase, !MP);
+        assemble(R0, R1, kbase);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads done before the next pass / the panel reuse
-        c0 = c1;
+        R0 = R1;
         if (!MP) break;
     }
 
@@ -601,19 +611,23 @@ template <int NB>
 void launch_nb(hipStream_t s, const DevState<float>& st, const Params<float>& prm, const FeatBatch<float>& fb,
                const int* list, int cnt, int Mmax) {
     // Y staging capacity: all M (M + 1) / 2 pair blocks in one pass unless four
-    // waves would then need more than MSCKF_GATE_SPKB KB (default 80: two
-    // workgroups per CU); otherwise passes sized for half of that.
+    // waves would then need more than MSCKF_GATE_SPKB KB; otherwise passes (of
+    // whole block rows) sized for half of that.  Multi-pass also drops the Y
+    // phase's registers (one pair in flight per lane, 82-88 VGPRs), so the
+    // classes with nb >= 4 gain a wave per SIMD.  Measured at 30x200 (gate
+    // ms): budget 80: 3.46, 60: 3.28, 50: 3.10, 36: 3.05, 20 / 12: 3.06-3.10.
     static int single_kb = -1;
     if (single_kb < 0) {
         const char* e = getenv("MSCKF_GATE_SPKB");
-        single_kb = e ? atoi(e) : 80;
+        single_kb = e ? atoi(e) : 36;
     }
     const int nbk = Mmax * (Mmax + 1) / 2;
+    const int cmin = 6 * Mmax < nbk ? 6 * Mmax : nbk;   // one block row (up to six observation rows) per pass
     auto per_wave = [&](int cb) { return (size_t)gm_wave_floats(Mmax, cb) * sizeof(float); };
     int capb = nbk;
     if (4 * per_wave(capb) > (size_t)single_kb * 1024)
-        for (int parts = 2; 4 * per_wave(capb) > (size_t)single_kb * 512 && capb > Mmax; ++parts)
-            capb = (nbk + parts - 1) / parts > Mmax ? (nbk + parts - 1) / parts : Mmax;
+        for (int parts = 2; 4 * per_wave(capb) > (size_t)single_kb * 512 && capb > cmin; ++parts)
+            capb = (nbk + parts - 1) / parts > cmin ? (nbk + parts - 1) / parts : cmin;
     const size_t pw = per_wave(capb);
     const int wpb = 4 * pw <= 160 * 1024 ? 4 : (2 * pw <= 160 * 1024 ? 2 : 1);
     if (capb < nbk) launch_cfg<NB, true>(s, st, prm, fb, list, cnt, Mmax, capb, wpb, wpb * pw);
