@@ -299,8 +299,14 @@ __global__ void __launch_bounds__(256) k_gate_mfma(DevState<float> st, Params<fl
                 av[RB] = w * esel;
             }
             // 4. trailing rank-4 update of the lower block triangle right of the panel
+            //    (after a block's last step its own column is finished: skipped)
+            if (sc < 3) {
 #pragma unroll
-            for (int CB = KB; CB < NB; ++CB)
+                for (int RB = KB; RB < NB; ++RB)
+                    acc[bidx(RB, KB)] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[RB], bv[KB], acc[bidx(RB, KB)], 0, 0, 0);
+            }
+#pragma unroll
+            for (int CB = KB + 1; CB < NB; ++CB)
 #pragma unroll
                 for (int RB = CB; RB < NB; ++RB)
                     acc[bidx(RB, CB)] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[RB], bv[CB], acc[bidx(RB, CB)], 0, 0, 0);
@@ -554,7 +560,7 @@ __global__ void __launch_bounds__(256) k_gate_mfma_wg(DevState<float> st, Params
                 const float av = (16 * RB + col_l <= p0 + 3) ? 0.f : wv * esel;
 #pragma unroll
                 for (int c = KB; c < 4 * i + 4; ++c)
-                    if (c <= RB)
+                    if (c <= RB && (c > KB || sc < 3))   // a block's last step leaves its own column finished
                         acc[gw_off(i) + c] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[c], acc[gw_off(i) + c], 0, 0, 0);
             }
         }
