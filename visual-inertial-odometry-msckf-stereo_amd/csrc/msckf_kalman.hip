@@ -21,6 +21,7 @@
 #include "msckf_common.h"
 #include "msckf_launch.h"
 #include "msckf_rchol.h"
+#include "msckf_mchol.h"
 
 namespace msckf {
 
@@ -312,6 +313,75 @@ __global__ void __launch_bounds__(NT) k_kal_a(DevState<T> st, UpdWs<T> ws, int e
         ws.afail[b] = ok ? 0 : 1;   // read by k_kal_c1 (info[3] may not exist yet when early)
         if (!ok && !early) ws.info[4 * b + 3] = -1;
     }
+}
+
+// ---- stages A and C1 on fp64 MFMA tiles (msckf_mchol.h), n <= 208 ----
+template <typename T>
+__global__ void __launch_bounds__(64 * MC_NW) k_kal_a_m(DevState<T> st, UpdWs<T> ws, int early) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    const int b = blockIdx.x;
+    const int* info = ws.info + 4 * b;
+    if (!early && info[0] == 0) return;
+    const int C = 6 * st.ncams[b], Cp = round4(C);
+    const T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
+    const int ld = st.Dmax, Cpw = ws.Cp;
+    KT* Lc = ws.Lc + (size_t)b * Cpw * Cpw;
+    KT* Vi = ws.Vi + (size_t)b * KW * Cpw;
+    KT* Sii = ws.Sii + (size_t)b * KW * KW;
+    auto map = [&](int i) { return i < C ? 21 + i : (i < Cp ? -1 : (i < Cp + 21 ? i - Cp : -1)); };
+    auto load = [&](int i, int j) -> double {
+        const int mi = map(i), mj = map(j);
+        if (mi < 0 || mj < 0) return i == j ? 1.0 : 0.0;
+        return (double)P[(size_t)mi * ld + mj];
+    };
+    auto put = [&](int r, int c, double v) {
+        if (r < Cp) Lc[(size_t)r * Cpw + c] = v;
+        else Vi[(size_t)(r - Cp) * Cpw + c] = v;
+    };
+    auto trail = [&](int i, int j, double v) { Sii[(i - Cp) * KW + (j - Cp)] = v; };
+    const bool ok = mchol_core(Cp + KW, Cp / 4, reinterpret_cast<double*>(smem_raw), load, put, trail);
+    if (threadIdx.x == 0) {
+        ws.afail[b] = ok ? 0 : 1;
+        if (!ok && !early) ws.info[4 * b + 3] = -1;
+    }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(64 * MC_NW) k_kal_c1_m(DevState<T> st, UpdWs<T> ws) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    const int b = blockIdx.x;
+    if (ws.info[4 * b] == 0) return;
+    if (ws.afail[b]) {   // stage A failed (P_cc not PD): no update for this filter
+        if (threadIdx.x == 0) ws.info[4 * b + 3] = -1;
+        return;
+    }
+    const int C = 6 * st.ncams[b], Cp = round4(C);
+    const int ldt = ws.Cmax + 1;
+    const KT* Tm = ws.Tm + (size_t)b * ws.Cmax * ldt;
+    KT* L = ws.G + (size_t)b * ws.Cmax * ldt;
+    auto load = [&](int i, int j) -> double {
+        if (i >= C || j >= C) return i == j ? 1.0 : 0.0;
+        return i >= j ? Tm[(size_t)i * ldt + j] : Tm[(size_t)j * ldt + i];
+    };
+    auto put = [&](int r, int c, double v) {
+        if (r < C && c < C && c <= r) L[(size_t)r * ldt + c] = v;
+    };
+    auto trail = [](int, int, double) {};
+    const bool ok = mchol_core(Cp, Cp / 4, reinterpret_cast<double*>(smem_raw), load, put, trail);
+    if (!ok && threadIdx.x == 0) ws.info[4 * b + 3] = -1;
+}
+
+// MSCKF_KAL_MCHOL=1: stages A / C1 on the fp64 MFMA workgroup Cholesky.  Off by
+// default: slower than rchol_core's 4x4 VALU tiles at 30x200 (A 1.45 vs 0.82 ms,
+// C1 1.15 vs 0.73 ms) -- fp64 MFMA has no rate advantage on MI355X, and eight
+// waves with two block rows each leave the MFMA pipe waiting on the step chain.
+static bool kal_mchol() {
+    static int en = -1;
+    if (en < 0) {
+        const char* e = getenv("MSCKF_KAL_MCHOL");
+        en = e ? atoi(e) : 0;
+    }
+    return en != 0;
 }
 
 // ---- stage C: Cholesky of T (Cp) with extra rows [Vc_i (21); Lc (C); c^T] ----
@@ -1282,6 +1352,11 @@ bool kalman_a_early(int Cmax) {
 template <typename T>
 void launch_kalman_a_early(hipStream_t s, const DevState<T>& st, const UpdWs<T>& ws) {
     const int Cp = (ws.Cmax + 3) & ~3;
+    if (kal_mchol() && mchol_fits(Cp + KW)) {
+        hipLaunchKernelGGL(k_kal_a_m<T>, dim3(st.B), dim3(64 * MC_NW), mchol_lds_doubles() * sizeof(double), s, st, ws,
+                           1);
+        return;
+    }
     const int nrow = (Cp + KW) / 4;
     RcholCfg c;
     pick_rchol(nrow * (nrow + 1) / 2, c);
@@ -1311,6 +1386,11 @@ void launch_kalman_chol(hipStream_t s, const DevState<T>& st, const Params<T>& p
         kt->begin(s, "kalman_a");
         if (c.nw == 8) launch_a16<T, 8, 14>(s, st, ws, lds);
         else launch_a16<T, 16, 8>(s, st, ws, lds);
+        kt->end(s);
+    } else if (kal_mchol() && mchol_fits(Cp + KW)) {   // stage A, fp64 MFMA tiles
+        kt->begin(s, "kalman_a");
+        hipLaunchKernelGGL(k_kal_a_m<T>, dim3(st.B), dim3(64 * MC_NW), mchol_lds_doubles() * sizeof(double), s, st, ws,
+                           0);
         kt->end(s);
     } else {   // stage A, 4x4 VALU tiles
         const int nrow = (Cp + KW) / 4;
@@ -1348,7 +1428,10 @@ void launch_kalman_chol(hipStream_t s, const DevState<T>& st, const Params<T>& p
         pick_rchol(nTc * (nTc + 1) / 2, c);
         const size_t lds = rchol_lds_doubles(nTc) * sizeof(double);
         kt->begin(s, "kalman_c");
-        if (c.nt == 256) launch_c1<T, 256, 4>(s, st, ws, lds);
+        if (kal_mchol() && mchol_fits(Cp))
+            hipLaunchKernelGGL(k_kal_c1_m<T>, dim3(st.B), dim3(64 * MC_NW), mchol_lds_doubles() * sizeof(double), s, st,
+                               ws);
+        else if (c.nt == 256) launch_c1<T, 256, 4>(s, st, ws, lds);
         else launch_c1<T, 512, 4>(s, st, ws, lds);
         if (Cq <= 16 * 8) launch_c2<T, 7, 2, 8>(s, st, ws);
         else launch_c2<T, 7, 2, 12>(s, st, ws);
