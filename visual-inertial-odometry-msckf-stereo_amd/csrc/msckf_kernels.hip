@@ -1791,7 +1791,7 @@ __host__ __device__ constexpr int info_slot_doubles(int Nmax) { return (Nmax * O
 
 template <typename T, int BPT, int NT>
 __global__ void __launch_bounds__(NT) k_info(DevState<T> st, FeatBatch<T> fb, UpdWs<T> ws, double tol_rel,
-                                             int phases, int assemble_only) {
+                                             int phases, int assemble_only, int tiled) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int b = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwave = NT >> 6;
@@ -1816,14 +1816,30 @@ __global__ void __launch_bounds__(NT) k_info(DevState<T> st, FeatBatch<T> fb, Up
     bool act[BPT];
 #pragma unroll
     for (int m = 0; m < BPT; ++m) {
-        // blocks of this workgroup: part blockIdx.y of the filter's lower-triangle blocks
-        const int blk = blockIdx.y * (NT * BPT) + tid + NT * m;
-        int i = (int)((sqrtf(8.0f * (float)blk + 1.0f) - 1.0f) * 0.5f);
-        while (i * (i + 1) / 2 > blk) --i;
-        while ((i + 1) * (i + 2) / 2 <= blk) ++i;
-        I[m] = i;
-        J[m] = blk - i * (i + 1) / 2;
-        act[m] = i < nc;
+        if (tiled) {
+            // wave = one 8 x 8 tile of cam pairs (lane: I = 8 ti + lane / 8, J = 8 tj + lane % 8):
+            // a feature's contiguous cam range [s, e] activates the pairs s <= J <= I <= e,
+            // a triangle that whole tiles cover far better than the row-major block order
+            // (whose 64-block strips are mostly inactive for every feature)
+            const int tt = blockIdx.y * (NT >> 6) * BPT + (tid >> 6) + (NT >> 6) * m;
+            const int TS = (Nmax + 7) >> 3, ntl = TS * (TS + 1) / 2;
+            int ti = (int)((sqrtf(8.0f * (float)tt + 1.0f) - 1.0f) * 0.5f);
+            while (ti * (ti + 1) / 2 > tt) --ti;
+            while ((ti + 1) * (ti + 2) / 2 <= tt) ++ti;
+            const int tj = tt - ti * (ti + 1) / 2;
+            I[m] = 8 * ti + (lane >> 3);
+            J[m] = 8 * tj + (lane & 7);
+            act[m] = tt < ntl && I[m] < nc && J[m] <= I[m];
+        } else {
+            // blocks of this workgroup: part blockIdx.y of the filter's lower-triangle blocks
+            const int blk = blockIdx.y * (NT * BPT) + tid + NT * m;
+            int i = (int)((sqrtf(8.0f * (float)blk + 1.0f) - 1.0f) * 0.5f);
+            while (i * (i + 1) / 2 > blk) --i;
+            while ((i + 1) * (i + 2) / 2 <= blk) ++i;
+            I[m] = i;
+            J[m] = blk - i * (i + 1) / 2;
+            act[m] = i < nc;
+        }
 #pragma unroll
         for (int x = 0; x < 6; ++x) {
             bv[m][x] = 0;
@@ -2483,12 +2499,26 @@ void launch_select(hipStream_t s, const DevState<T>& st, const FeatBatch<T>& fb,
 // Numerical-rank threshold of the pivoted Cholesky, relative to max diag(A).
 constexpr double INFO_TOL_REL = 1e-11;
 
+// MSCKF_INFO_TILED=0: the row-major cam-pair order in k_info (A/B runs).  The
+// pivoted-Cholesky variant needs every block in one workgroup: row-major there.
+static bool info_tiled(int Cmax) {
+    static int en = -1;
+    if (en < 0) {
+        const char* e = getenv("MSCKF_INFO_TILED");
+        en = e ? atoi(e) : 1;
+    }
+    return en != 0 && update_mode(Cmax) == UPD_CHOL;
+}
+
 template <typename T, int BPT, int NT>
 static void launch_info_cfg(hipStream_t s, const DevState<T>& st, const FeatBatch<T>& fb, const UpdWs<T>& ws) {
     const int fbn = info_fb(st.Nmax);
     const size_t lds = ((size_t)2 * fbn * info_slot_doubles(st.Nmax) + 2 * (size_t)ws.Cmax + 1) * sizeof(double) +
                        4 * fbn * sizeof(unsigned long long) + ((size_t)ws.Cmax + 2 * fbn * st.Nmax) * sizeof(int);
-    const int nblk = st.Nmax * (st.Nmax + 1) / 2, parts = (nblk + NT * BPT - 1) / (NT * BPT);
+    const int TS = (st.Nmax + 7) / 8, ntl = TS * (TS + 1) / 2;
+    const int tiled = info_tiled(ws.Cmax) ? 1 : 0;
+    const int nblk = st.Nmax * (st.Nmax + 1) / 2;
+    const int parts = tiled ? (ntl + (NT / 64) * BPT - 1) / ((NT / 64) * BPT) : (nblk + NT * BPT - 1) / (NT * BPT);
     static size_t attr = 64 * 1024;   // dynamic LDS granted so far (default 64 KB)
     if (lds > attr) {
         (void)hipFuncSetAttribute((const void*)k_info<T, BPT, NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2503,7 +2533,7 @@ static void launch_info_cfg(hipStream_t s, const DevState<T>& st, const FeatBatc
     // the pivoted Cholesky needs every block in one workgroup: update_mode() only
     // selects it when parts == 1
     hipLaunchKernelGGL((k_info<T, BPT, NT>), dim3(st.B, parts), dim3(NT), lds, s, st, fb, ws, INFO_TOL_REL, phases,
-                       update_mode(ws.Cmax) == UPD_CHOL ? 1 : 0);
+                       update_mode(ws.Cmax) == UPD_CHOL ? 1 : 0, tiled);
 }
 
 // Update path (MSCKF_UPDATE env, for A/B runs):
@@ -2533,6 +2563,14 @@ void launch_compress(hipStream_t s, const DevState<T>& st, const FeatBatch<T>& f
     }
     if (update_mode(ws.Cmax) == UPD_CHOL && info_mfma_enabled(st.Nmax)) {
         launch_info_mfma<T>(s, st, fb, ws);
+        return;
+    }
+    if (info_tiled(ws.Cmax)) {   // one wave per 8 x 8 tile of cam pairs
+        const int TS = (st.Nmax + 7) / 8, ntl = TS * (TS + 1) / 2;
+        if (ntl <= 4) launch_info_cfg<T, 1, 256>(s, st, fb, ws);
+        else if (ntl <= 8) launch_info_cfg<T, 1, 512>(s, st, fb, ws);
+        else if (ntl <= 10) launch_info_cfg<T, 1, 640>(s, st, fb, ws);
+        else launch_info_cfg<T, 1, 1024>(s, st, fb, ws);   // > 10 tiles: several workgroups per filter
         return;
     }
     const int nblk = st.Nmax * (st.Nmax + 1) / 2;   // 6x6 cam-pair blocks of A (lower triangle)
