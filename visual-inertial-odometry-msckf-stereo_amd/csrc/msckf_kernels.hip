@@ -1781,9 +1781,9 @@ __global__ void __launch_bounds__(256) k_select(DevState<T> st, FeatBatch<T> fb,
 // problems) carry no information and produce no row.
 // Output: rows 0..n-1 of [F | r_F] in H_thin (KT), n = rank in info[1].
 // ===========================================================================
-// features staged per round (one staging wave each): 4, 2 or 1, as many as
+// features staged per round (one staging wave each): 5, 4, 2 or 1, as many as
 // the double-buffered slots fit in LDS
-__host__ __device__ constexpr int info_fb(int Nmax) { return Nmax <= 40 ? 4 : (Nmax <= 80 ? 2 : 1); }
+__host__ __device__ constexpr int info_fb(int Nmax) { return Nmax <= 32 ? 5 : (Nmax <= 40 ? 4 : (Nmax <= 80 ? 2 : 1)); }
 
 // Doubles per staging slot: a feature's M <= Nmax records copied contiguously,
 // rounded up to whole 1 KiB global_load_lds wave-instructions.
@@ -1791,7 +1791,7 @@ __host__ __device__ constexpr int info_slot_doubles(int Nmax) { return (Nmax * O
 
 template <typename T, int BPT, int NT>
 __global__ void __launch_bounds__(NT) k_info(DevState<T> st, FeatBatch<T> fb, UpdWs<T> ws, double tol_rel,
-                                             int phases, int assemble_only, int tiled) {
+                                             int phases, int assemble_only, int tiled, int fbn) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int b = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwave = NT >> 6;
@@ -1801,7 +1801,7 @@ __global__ void __launch_bounds__(NT) k_info(DevState<T> st, FeatBatch<T> fb, Up
         if (tid == 0) info[1] = 0;
         return;
     }
-    const int SLOT = info_slot_doubles(Nmax), INFO_FB = info_fb(Nmax);
+    const int SLOT = info_slot_doubles(Nmax), INFO_FB = fbn;
     double* rec = reinterpret_cast<double*>(smem_raw);                      // [2][FB][SLOT]
     double* fvec = rec + (size_t)2 * INFO_FB * SLOT;                         // [Cmax + 1]
     double* dval = fvec + Cmax + 1;                                          // [Cmax]
@@ -2512,7 +2512,19 @@ static bool info_tiled(int Cmax) {
 
 template <typename T, int BPT, int NT>
 static void launch_info_cfg(hipStream_t s, const DevState<T>& st, const FeatBatch<T>& fb, const UpdWs<T>& ws) {
-    const int fbn = info_fb(st.Nmax);
+    int fbn = info_fb(st.Nmax);
+    {   // MSCKF_INFO_FB: features staged per batch (as many as the double-buffered slots fit in LDS)
+        static int want = -1;
+        if (want < 0) {
+            const char* e = getenv("MSCKF_INFO_FB");
+            want = e ? atoi(e) : 0;
+        }
+        const size_t per = ((size_t)2 * info_slot_doubles(st.Nmax)) * sizeof(double) + 4 * sizeof(unsigned long long) +
+                           2 * st.Nmax * sizeof(int);
+        const size_t fixed = (2 * (size_t)ws.Cmax + 1) * sizeof(double) + (size_t)ws.Cmax * sizeof(int);
+        if (want > 0) fbn = want;
+        while (fbn > 1 && fixed + fbn * per > 160 * 1024) --fbn;
+    }
     const size_t lds = ((size_t)2 * fbn * info_slot_doubles(st.Nmax) + 2 * (size_t)ws.Cmax + 1) * sizeof(double) +
                        4 * fbn * sizeof(unsigned long long) + ((size_t)ws.Cmax + 2 * fbn * st.Nmax) * sizeof(int);
     const int TS = (st.Nmax + 7) / 8, ntl = TS * (TS + 1) / 2;
@@ -2533,7 +2545,7 @@ static void launch_info_cfg(hipStream_t s, const DevState<T>& st, const FeatBatc
     // the pivoted Cholesky needs every block in one workgroup: update_mode() only
     // selects it when parts == 1
     hipLaunchKernelGGL((k_info<T, BPT, NT>), dim3(st.B, parts), dim3(NT), lds, s, st, fb, ws, INFO_TOL_REL, phases,
-                       update_mode(ws.Cmax) == UPD_CHOL ? 1 : 0, tiled);
+                       update_mode(ws.Cmax) == UPD_CHOL ? 1 : 0, tiled, fbn);
 }
 
 // Update path (MSCKF_UPDATE env, for A/B runs):
