@@ -581,14 +581,14 @@ __global__ void __launch_bounds__(64 * NW) k_kal_c2(DevState<T> st, UpdWs<T> ws)
 // Stages A and C for windows whose tiles do not fit in one workgroup's
 // registers (Nmax > 36): the same partial Cholesky, in place on a row-major
 // global workspace (rows < ncol: the square lower part; rows >= ncol: extra
-// rows with ncol columns), right-looking and blocked by GNB = 16 pivots.  Each
+// rows with ncol columns), right-looking and blocked by GNB = 32 pivots.  Each
 // panel step is three launches over all filters: factor the 16 x 16 diagonal
 // block (one wave per filter), the panel rows below it (one row per thread,
 // many workgroups per filter), and the trailing update A -= W W^T on the
 // matrix cores (64 x 64 fp64 MFMA tiles, gemm64 below).  The trailing matrix
 // makes one round trip per 16 pivots instead of one per pivot.
 // ===========================================================================
-constexpr int GNB = 16;
+constexpr int GNB = 32;   // pivots per panel (16: 18 trailing round trips at 50x400, 3.7 ms of stage C)
 
 // stage 0 = A: [P_cc P_ci; P_ic P_ii] (N = C + 21 square, C pivots);
 // stage 1 = C: T (C square) with the extra rows [Vc_i (21); Lc (C); c^T]
