@@ -581,14 +581,14 @@ __global__ void __launch_bounds__(64 * NW) k_kal_c2(DevState<T> st, UpdWs<T> ws)
 // Stages A and C for windows whose tiles do not fit in one workgroup's
 // registers (Nmax > 36): the same partial Cholesky, in place on a row-major
 // global workspace (rows < ncol: the square lower part; rows >= ncol: extra
-// rows with ncol columns), right-looking and blocked by GNB = 32 pivots.  Each
+// rows with ncol columns), right-looking and blocked by GNB = 64 pivots.  Each
 // panel step is three launches over all filters: factor the 16 x 16 diagonal
 // block (one wave per filter), the panel rows below it (one row per thread,
 // many workgroups per filter), and the trailing update A -= W W^T on the
 // matrix cores (64 x 64 fp64 MFMA tiles, gemm64 below).  The trailing matrix
 // makes one round trip per 16 pivots instead of one per pivot.
 // ===========================================================================
-constexpr int GNB = 32;   // pivots per panel (16: 18 trailing round trips at 50x400, 3.7 ms of stage C)
+constexpr int GNB = 64;   // pivots per panel (50x400 / 80x1000 updates/s: 16: 24.1k / 4.98k, 32: 26.3k / 5.27k, 48: 26.8k / 5.21k, 64: 27.5k / 5.20k)
 
 // stage 0 = A: [P_cc P_ci; P_ic P_ii] (N = C + 21 square, C pivots);
 // stage 1 = C: T (C square) with the extra rows [Vc_i (21); Lc (C); c^T]
@@ -1235,10 +1235,13 @@ static void launch_gchol(hipStream_t s, const DevState<T>& st, const UpdWs<T>& w
     else hipLaunchKernelGGL(k_gchol_c_load<T>, dim3(ld_chunks, st.B), dim3(256), 0, s, st, ws);
     for (int k = 0; k < Cmax; k += GNB) {
         hipLaunchKernelGGL((k_gchol_diag<STAGE, T>), dim3(st.B), dim3(64), 0, s, st, ws, k);
-        const int rows = nrow - k - GNB;
+        // grids for the rows / columns below / right of the panel: a filter's last panel
+        // may hold fewer than GNB pivots (nb = min(GNB, C_b - k), C_b <= Cmax), so size
+        // them for nb >= 1; blocks past a filter's matrix exit at once
+        const int rows = nrow - k - 1;
         if (rows > 0)
             hipLaunchKernelGGL((k_gchol_trsm<STAGE, T>), dim3((rows + 255) / 256, st.B), dim3(256), 0, s, st, ws, k);
-        const int ti = (rows + GT - 1) / GT, tj = (ncol - k - GNB + GT - 1) / GT;
+        const int ti = (rows + GT - 1) / GT, tj = (ncol - k - 1 + GT - 1) / GT;
         if (rows > 0 && tj > 0)
             hipLaunchKernelGGL((k_gchol_update<STAGE, T>), dim3(tj, ti, st.B), dim3(256), 0, s, st, ws, k);
     }
