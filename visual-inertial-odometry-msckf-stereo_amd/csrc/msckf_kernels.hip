@@ -1783,7 +1783,9 @@ __global__ void __launch_bounds__(256) k_select(DevState<T> st, FeatBatch<T> fb,
 // ===========================================================================
 // features staged per round (one staging wave each): 5, 4, 2 or 1, as many as
 // the double-buffered slots fit in LDS
-__host__ __device__ constexpr int info_fb(int Nmax) { return Nmax <= 32 ? 5 : (Nmax <= 40 ? 4 : (Nmax <= 80 ? 2 : 1)); }
+// (five, or as many as fit: 2 x 5 slots at <= 40 cams, 4 at 50, 2 at 80 -- measured at 30x200
+// four / five / six: 2.17 / 2.06 / 2.11 ms; at 50x400 two / three / four: 3.0 / 2.5 / 2.18 ms)
+__host__ __device__ constexpr int info_fb(int Nmax) { return Nmax > 0 ? 5 : 1; }
 
 // Doubles per staging slot: a feature's M <= Nmax records copied contiguously,
 // rounded up to whole 1 KiB global_load_lds wave-instructions.
