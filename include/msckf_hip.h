@@ -56,7 +56,7 @@ typedef struct msckf_ctx msckf_ctx_t;
 
 /* Replaces MSCKF.__init__ (msckf.py:105-164): allocates the device state of
  * n_filters filters of capacity n_cam_capacity cam states each
- * (1 <= n_cam_capacity <= 64). */
+ * (1 <= n_cam_capacity <= 128). */
 int msckf_create(const msckf_config_t* cfg, int hip_device, int scalar_bytes,
                  int n_filters, int n_cam_capacity, msckf_ctx_t** out);
 int msckf_destroy(msckf_ctx_t* ctx);

@@ -582,6 +582,21 @@ def remove_cam_cov(st: FilterState, cam_ids: Sequence[int]):
         del st.cams[cid]
 
 
+def check_motion(obs: "OrderedDict[int, np.ndarray]", cams: Dict[int, CamState], threshold: float) -> bool:
+    """feature.py:124-165: enough translation between the first and the last
+    observing cam, orthogonal to the first observation's ray, to triangulate."""
+    if threshold < 0:
+        return True
+    ids = list(obs.keys())
+    c0, c1 = cams[ids[0]], cams[ids[-1]]
+    R0 = to_rotation(c0.q).T
+    d = np.array([*obs[ids[0]][:2], 1.0])
+    d = R0 @ (d / np.linalg.norm(d))
+    tr = c1.p - c0.p
+    orth = tr - (tr @ d) * d
+    return bool(np.linalg.norm(orth) > threshold)
+
+
 def find_redundant_cam_states(st: FilterState, tracking_rate: float):
     """msckf.py:691-727."""
     pairs = list(st.cams.items())
@@ -655,6 +670,7 @@ class OracleMSCKF:
         self.gate_log: List[tuple] = []   # (frame, dof, rows, accepted)
         self.shape_log: List[tuple] = []  # (frame, H rows, H cols)
         self.n_published = 0
+        self.resets: List[int] = []       # frames after which online_reset fired
 
     def _initial_cov(self):
         """msckf.py:820-830"""
@@ -741,6 +757,9 @@ class OracleMSCKF:
                 invalid.append(f.id)
                 continue
             if not f.is_initialized:
+                if not check_motion(f.observations, self.st.cams, self.lm.translation_threshold):
+                    invalid.append(f.id)
+                    continue
                 if not self._initialize(f):
                     invalid.append(f.id)
                     continue
@@ -789,7 +808,8 @@ class OracleMSCKF:
                 del f.observations[inv[0]]
                 continue
             if not f.is_initialized:
-                if not self._initialize(f):
+                if (not check_motion(f.observations, self.st.cams, self.lm.translation_threshold)
+                        or not self._initialize(f)):
                     for c in inv:
                         del f.observations[c]
                     continue
@@ -830,6 +850,7 @@ class OracleMSCKF:
         self.st.cams.clear()
         self.map.clear()
         self.st.P = self._initial_cov()
+        self.resets.append(self.n_published - 1)   # the frame just published
 
     def publish(self, t):
         """msckf.py:888-908 -> dict(timestamp, pose (R, t), velocity, cam0_pose)."""

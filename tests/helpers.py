@@ -36,11 +36,14 @@ def feature_obs(d, f):
     return [(int(c), d["obs_z"][r]) for r, c in zip(range(a, b), d["obs_cam"][a:b])]
 
 
-def oracle_update(d, row_cap=None, triangulate=True):
+def oracle_update(d, row_cap=None, triangulate=True, accept=None, tri=None, sigma2=0.035 ** 2):
     """Oracle restatement of the synthetic update: triangulate, jacobian,
     gate (dof = M-1, the lost-feature path), stack, EKF update.
+    ``tri = (p, ok)`` replaces the triangulation and ``accept`` (bool per
+    feature) the chi2 decisions -- to rerun the update on another path's own
+    decisions (the fp32 parity tests).
     Returns (state, accept flags, tri positions, tri ok, gammas)."""
-    st = oracle_state_from_arrays(d)
+    st = oracle_state_from_arrays(d, sigma2=sigma2)
     F = int(d["F"])
     tri_p = np.zeros((F, 3))
     tri_ok = np.zeros(F, bool)
@@ -51,7 +54,9 @@ def oracle_update(d, row_cap=None, triangulate=True):
     from msckf_amd import chi2_threshold
     for f in range(F):
         obs = feature_obs(d, f)
-        if triangulate:
+        if tri is not None:
+            p, ok = np.asarray(tri[0][f], float), bool(tri[1][f])
+        elif triangulate:
             p, ok, _ = O.triangulate(OrderedDict(obs), st.cams, st.R_cam0_cam1, st.t_cam0_cam1)
         else:
             p, ok = d["tri_p"][f], bool(d["tri_ok"][f])
@@ -59,9 +64,12 @@ def oracle_update(d, row_cap=None, triangulate=True):
         if not ok:
             continue
         H, r = O.feature_jacobian(st, p, obs)
-        g = O.gating_gamma(st, H, r)
-        gam[f] = g
-        if g < chi2_threshold(len(obs) - 1):
+        if accept is not None:      # forced decisions: no gating
+            take = bool(accept[f])
+        else:
+            gam[f] = O.gating_gamma(st, H, r)
+            take = gam[f] < chi2_threshold(len(obs) - 1)
+        if take:
             acc[f] = True
             Hs.append(H)
             rs.append(r)
@@ -71,3 +79,25 @@ def oracle_update(d, row_cap=None, triangulate=True):
     if Hs:
         O.measurement_update(st, np.vstack(Hs), np.concatenate(rs))
     return st, acc, tri_p, tri_ok, gam
+
+
+def rounded(d, dtype=np.float32):
+    """The problem as a context of scalar type ``dtype`` holds it: every
+    floating-point array rounded to ``dtype`` (and back to float64)."""
+    out = {}
+    for k, v in d.items():
+        a = np.asarray(v)
+        out[k] = a.astype(dtype).astype(np.float64) if a.dtype.kind == "f" else v
+    return out
+
+
+def sequence_config(g):
+    """FilterConfig with the config edits a sequence fixture was made with
+    (tools/gen_golden.py:gen_sequence)."""
+    from msckf_amd import FilterConfig
+    cfg = FilterConfig()
+    if "translation_threshold" in g:
+        cfg.optimization.translation_threshold = float(g["translation_threshold"])
+    if "position_std_threshold" in g:
+        cfg.position_std_threshold = float(g["position_std_threshold"])
+    return cfg

@@ -3,9 +3,10 @@ by running the reference filter itself (tools/gen_golden.py).  CPU only."""
 from collections import OrderedDict
 
 import numpy as np
+import pytest
 
 from conftest import golden, rel
-from helpers import oracle_state_from_arrays, feature_obs
+from helpers import oracle_state_from_arrays, feature_obs, sequence_config
 from oracle import msckf_oracle as O
 from msckf_amd import CHI2_05, geometry
 
@@ -128,13 +129,31 @@ def sequence_record(st, res, n_map):
         res["cam0_pose"].R.ravel(), res["cam0_pose"].t])
 
 
-def test_sequence():
-    """200-frame synthetic stereo+IMU stream through the whole filter: every
-    gating decision and stacked-H shape identical, state to 1e-9."""
-    from msckf_amd import synth, FilterConfig, chi2_threshold
-    g = golden("sequence_s1")
+def test_check_motion():
+    """feature.py:124-165 at thresholds -1 (EuRoC default), 0.2 and 0.4."""
+    g = golden("check_motion")
+    cams = OrderedDict((i, O.CamState(i, 0.0, g["cam_q"][i], g["cam_p"][i], g["cam_q"][i]))
+                       for i in range(len(g["cam_q"])))
+    for thr, key in ((-1.0, "ok_m1"), (0.2, "ok_2"), (0.4, "ok_4")):
+        res = []
+        for j in range(len(g["first"])):
+            obs = OrderedDict((c, g["z"][j] + 0.01 * (c - g["first"][j]))
+                              for c in range(int(g["first"][j]), int(g["last"][j]) + 1))
+            res.append(O.check_motion(obs, cams, thr))
+        np.testing.assert_array_equal(res, g[key])
+    assert 0 < g["ok_4"].sum() < g["ok_2"].sum() < g["ok_m1"].sum()
+
+
+@pytest.mark.parametrize("name", ["sequence_s1", "sequence_s2", "sequence_s3"])
+def test_sequence(name):
+    """Synthetic stereo+IMU streams through the whole filter: every gating
+    decision and stacked-H shape identical, state to 1e-9.  s1: EuRoC config
+    (200 frames); s2: check_motion at translation threshold 0.2; s3:
+    online_reset firing (position std threshold 0.11 m)."""
+    from msckf_amd import synth, chi2_threshold
+    g = golden(name)
     seq = synth.make_sequence(int(g["n_frames"]), int(g["seed"]))
-    orc = O.OracleMSCKF(FilterConfig(), chi2_threshold)
+    orc = O.OracleMSCKF(sequence_config(g), chi2_threshold)
     recs = []
     for kind, m in seq.events():
         if kind == 0:
@@ -149,3 +168,5 @@ def test_sequence():
     assert rec.shape == g["rec"].shape
     np.testing.assert_allclose(rec, g["rec"], rtol=1e-9, atol=1e-10)
     assert rel(orc.st.P, g["P_final"]) < 1e-9
+    if "resets" in g:
+        np.testing.assert_array_equal(orc.resets, g["resets"])

@@ -244,11 +244,54 @@ def gen_prune():
     save("prune", **problem_arrays(pr), rm=np.array(rm), P_out=R.state_server._vio_state_cov__, **out)
 
 
-def gen_sequence(name, n_frames, seed):
+def gen_check_motion():
+    """Fixture (x): Feature.check_motion feature.py:124-165 on random cam
+    windows and observations, at the config.py:10 thresholds -1 / 0.2 and
+    config.py:68's 0.4."""
+    rng = np.random.default_rng(21)
+    n_cams, n_feat = 12, 64
+    cq = np.stack([rand_quat(rng, 0.3) for _ in range(n_cams)])
+    cp = rng.standard_normal((n_cams, 3)) * 0.35
+    cams = OrderedDict()
+    for i in range(n_cams):
+        c = ref.msckf.CAMState(i)
+        c.orientation = cq[i].copy()
+        c._vio_position__ = cp[i].copy()
+        cams[i] = c
+    first = rng.integers(0, n_cams - 2, n_feat)
+    last = np.minimum(first + rng.integers(2, 8, n_feat), n_cams - 1)
+    z = rng.uniform(-0.6, 0.6, (n_feat, 4))
+    out = {}
+    for thr in (-1.0, 0.2, 0.4):
+        oc = ref.config.OptimizationConfigEuRoC()
+        oc._vio_translation_threshold__ = thr
+        res = []
+        for j in range(n_feat):
+            f = ref.feature.Feature(j, oc)
+            for c in range(first[j], last[j] + 1):
+                f.observations[c] = z[j] + 0.01 * (c - first[j])
+            res.append(bool(f.check_motion(cams)))
+        out["ok_%s" % ("m1" if thr < 0 else str(int(thr * 10)))] = np.array(res)
+    save("check_motion", cam_q=cq, cam_p=cp, first=first, last=last, z=z, **out)
+
+
+def gen_sequence(name, n_frames, seed, translation_threshold=None, position_std_threshold=None):
     """Fixture (ix): the full reference filter on a synthetic stereo+IMU stream,
     fed in strict time order.  Per frame: state, covariance norms, the gating
-    decision sequence and the stacked-H shapes."""
+    decision sequence and the stacked-H shapes.  Optional config edits: the
+    feature translation threshold (check_motion, feature.py:124-165) and the
+    position std threshold of online_reset (msckf.py:859-886)."""
     R, _ = fresh_filter(ref)
+    if translation_threshold is not None:
+        R.optimization_config._vio_translation_threshold__ = translation_threshold
+    if position_std_threshold is not None:
+        R.config._vio_position_std_threshold__ = position_std_threshold
+    resets = []
+    orig_reset = R.reset_state_cov
+
+    def reset():
+        resets.append(len(recs))
+        return orig_reset()
     seq = synth.make_sequence(n_frames, seed)
     gates, shapes = [], []
     orig_gate, orig_upd = R.gating_test, R.measurement_update
@@ -264,6 +307,7 @@ def gen_sequence(name, n_frames, seed):
 
     R.gating_test, R.measurement_update = gate, upd
     recs = []
+    R.reset_state_cov = reset
     for kind, m in seq.events():
         if kind == 0:
             R.imu_callback(m)
@@ -279,17 +323,33 @@ def gen_sequence(name, n_frames, seed):
             [np.linalg.norm(P), np.trace(P), P.shape[0], len(R.state_server._vio_cam_states__),
              len(R.map_server)], res.cam0_pose._vio_R__.ravel(), res.cam0_pose._vio_t__]))
     P = R.state_server._vio_state_cov__
+    extra = {}
+    if translation_threshold is not None:
+        extra["translation_threshold"] = translation_threshold
+    if position_std_threshold is not None:
+        extra["position_std_threshold"] = position_std_threshold
     save(name, seed=seed, n_frames=n_frames, rec=np.array(recs),
          gates=np.array(gates, dtype=np.int64), shapes=np.array(shapes, dtype=np.int64),
-         P_final=P, gravity=ref.msckf.IMUState._vio_gravity__)
+         P_final=P, gravity=ref.msckf.IMUState._vio_gravity__, resets=np.array(resets, dtype=np.int64), **extra)
 
+
+JOBS = {
+    "math": gen_math,
+    "process_model": gen_process_model,
+    "augment": gen_augment,
+    "update_n10_f40": lambda: gen_update("update_n10_f40", 10, 40, seed=3),
+    "update_n20_f100": lambda: gen_update("update_n20_f100", 20, 100, seed=4, n_inv=6),
+    "prune": gen_prune,
+    "check_motion": gen_check_motion,
+    "sequence_s1": lambda: gen_sequence("sequence_s1", 200, 1),
+    # check_motion on: threshold 0.2, the value config.py:10 comments out
+    "sequence_s2": lambda: gen_sequence("sequence_s2", 120, 2, translation_threshold=0.2),
+    # online_reset firing: position std threshold 0.11 m instead of 8 m (config.py:64)
+    "sequence_s3": lambda: gen_sequence("sequence_s3", 100, 2, position_std_threshold=0.11),
+}
 
 if __name__ == "__main__":
+    # python tools/gen_golden.py [fixture ...]   (default: all)
     os.makedirs(OUT, exist_ok=True)
-    gen_math()
-    gen_process_model()
-    gen_augment()
-    gen_update("update_n10_f40", 10, 40, seed=3)
-    gen_update("update_n20_f100", 20, 100, seed=4, n_inv=6)
-    gen_prune()
-    gen_sequence("sequence_s1", 200, 1)
+    for name in (sys.argv[1:] or list(JOBS)):
+        JOBS[name]()

@@ -62,15 +62,13 @@ struct DBuf {   // grow-only device buffer
 struct msckf_ctx {
     int device = 0, scalar = 8, B = 1, Nmax = 0, Dmax = 0, Cmax = 0;
     hipStream_t stream = nullptr;
-    hipStream_t side = nullptr;                          // Kalman stage A ahead of the feature kernels
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     msckf_config_t cfg{};
     std::vector<int> h_ncams;
     // state
     DBuf<unsigned char> P, imu, cams, P_snap, imu_snap, cams_snap;
     DBuf<int> ncams, ncams_snap;
     // update workspace
-    DBuf<unsigned char> Hthin, Hqr, HP, S, dx, Lc, Vi, Sii, G, Tm, W, Wk;
+    DBuf<unsigned char> Hthin, dx, Lc, Vi, Sii, G, Tm, W, Wk;
     DBuf<int> info, afail;
     // feature batch
     int nf = 0, maxM = 0;
@@ -127,9 +125,6 @@ template <typename T>
 UpdWs<T> upd_ws(msckf_ctx* c) {
     UpdWs<T> w;
     w.Hthin = reinterpret_cast<KT*>(c->Hthin.p);
-    w.Hqr = reinterpret_cast<T*>(c->Hqr.p);
-    w.HP = reinterpret_cast<KT*>(c->HP.p);
-    w.S = reinterpret_cast<KT*>(c->S.p);
     w.dx = reinterpret_cast<KT*>(c->dx.p);
     w.info = c->info.p;
     w.Cmax = c->Cmax;
@@ -161,7 +156,7 @@ FeatBatch<T> feat_batch(msckf_ctx* c) {
     f.valid = c->valid.p;
     f.obs_ws = reinterpret_cast<T*>(c->obs_ws.p);
     f.obs_g = reinterpret_cast<double*>(c->obs_g.p);
-    f.compact = feature_needs_compact(c->maxM, c->Cmax) ? 1 : 0;
+    f.compact = feature_needs_compact(c->maxM) ? 1 : 0;
     f.tau = reinterpret_cast<T*>(c->tau.p);
     f.ysq = reinterpret_cast<T*>(c->ysq.p);
     f.gamma = reinterpret_cast<T*>(c->gamma.p);
@@ -232,9 +227,14 @@ int load_features(msckf_ctx* c, int nf, const int32_t* feat_off, int single_filt
         int b = h_filt[f];
         if (M < 1 || M > 128) FAIL(-1, "feature %d has %d observations (1..128 supported)", f, M);
         if (M > c->h_ncams[b]) FAIL(-1, "feature %d has more observations than cam states", f);
-        for (int i = obs_off[f]; i < obs_off[f + 1]; ++i)
-            if (obs_cam[i] < 0 || obs_cam[i] >= c->h_ncams[b])
-                FAIL(-1, "feature %d observes cam slot %d (filter %d has %d)", f, obs_cam[i], b, c->h_ncams[b]);
+        unsigned long long seen[2] = {0, 0};   // cam slots < 128: k_info's cam -> record table needs them distinct
+        for (int i = obs_off[f]; i < obs_off[f + 1]; ++i) {
+            const int cam = obs_cam[i];
+            if (cam < 0 || cam >= c->h_ncams[b])
+                FAIL(-1, "feature %d observes cam slot %d (filter %d has %d)", f, cam, b, c->h_ncams[b]);
+            if ((seen[cam >> 6] >> (cam & 63)) & 1ull) FAIL(-1, "feature %d observes cam slot %d twice", f, cam);
+            seen[cam >> 6] |= 1ull << (cam & 63);
+        }
         ysq[f + 1] = ysq[f] + 16LL * M * M;
     }
     const size_t ts = sizeof(T);
@@ -340,17 +340,6 @@ int run_update_chain(msckf_ctx* c, int row_cap, bool triangulate) {
     Params<T> prm = make_params<T>(c);
     FeatBatch<T> fb = feat_batch<T>(c);
     UpdWs<T> ws = upd_ws<T>(c);
-    // Kalman stage A depends on P only: fork it onto the side stream now, join
-    // before stage B (it overlaps triangulation .. information assembly)
-    const bool a_early = kalman_a_early(c->Cmax);
-    if (a_early) {
-        HIPC(hipEventRecord(c->ev_fork, s));
-        HIPC(hipStreamWaitEvent(c->side, c->ev_fork, 0));
-        c->timer.begin(c->side, "kalman_a");
-        launch_kalman_a_early<T>(c->side, st, ws);
-        c->timer.end(c->side);
-        HIPC(hipEventRecord(c->ev_join, c->side));
-    }
     if (triangulate) {
         c->timer.begin(s, "triangulate");
         launch_triangulate<T>(s, st, prm, fb, c->sc);
@@ -368,8 +357,7 @@ int run_update_chain(msckf_ctx* c, int row_cap, bool triangulate) {
     c->timer.begin(s, "compress");
     launch_compress<T>(s, st, fb, ws);
     c->timer.end(s);
-    if (a_early) HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
-    launch_kalman<T>(s, st, prm, ws, &c->timer, a_early);
+    launch_kalman<T>(s, st, prm, ws, &c->timer);
     HIPC(hipGetLastError());
     return 0;
 }
@@ -405,16 +393,11 @@ int do_create(msckf_ctx* c) {
     HIPC(c->cams.ensure(B * c->Nmax * CAM_STRIDE * ts));
     HIPC(c->ncams.ensure(B));
     HIPC(c->Hthin.ensure(B * c->Cmax * (c->Cmax + 1) * sizeof(KT)));
-    {   // QR row-merge scratch only for MSCKF_UPDATE=qr (A/B runs)
-        if (update_mode(c->Cmax) == UPD_QR) HIPC(c->Hqr.ensure(B * c->Cmax * (c->Cmax + 1) * ts));
-    }
-    HIPC(c->HP.ensure(B * c->Cmax * c->Dmax * sizeof(KT)));
-    HIPC(c->S.ensure(B * c->Cmax * c->Cmax * sizeof(KT)));
     HIPC(c->dx.ensure(B * (c->Dmax + c->Cmax) * sizeof(KT)));
     HIPC(c->info.ensure(4 * B));
     HIPC(c->afail.ensure(B));
     HIPC(hipMemset(c->afail.p, 0, B * sizeof(int)));
-    if (update_mode(c->Cmax) == UPD_CHOL) {   // Cholesky-form Kalman workspace
+    {   // Cholesky-form Kalman workspace
         const size_t Cp = (c->Cmax + 15) & ~15, kb = sizeof(KT);
         HIPC(c->Lc.ensure(B * Cp * Cp * kb));
         HIPC(c->Vi.ensure(B * 24 * Cp * kb));
@@ -736,13 +719,6 @@ int msckf_create(const msckf_config_t* cfg, int hip_device, int scalar_bytes, in
         delete c;
         FAIL(-2, "hipStreamCreate: %s", hipGetErrorString(e));
     }
-    e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming);
-    if (e != hipSuccess) {
-        msckf_destroy(c);
-        FAIL(-2, "hipStreamCreate / hipEventCreate: %s", hipGetErrorString(e));
-    }
     int r = DISPATCH(c, do_create, c);
     if (r) {
         msckf_destroy(c);
@@ -756,8 +732,7 @@ int msckf_destroy(msckf_ctx_t* c) {
     if (!c) return 0;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    if (c->side) (void)hipStreamSynchronize(c->side);
-    for (auto* b : {&c->P, &c->imu, &c->cams, &c->P_snap, &c->imu_snap, &c->cams_snap, &c->Hthin, &c->Hqr, &c->HP, &c->S, &c->Lc, &c->Vi, &c->Sii, &c->G, &c->Tm, &c->W, &c->Wk,
+    for (auto* b : {&c->P, &c->imu, &c->cams, &c->P_snap, &c->imu_snap, &c->cams_snap, &c->Hthin, &c->Lc, &c->Vi, &c->Sii, &c->G, &c->Tm, &c->W, &c->Wk,
                     &c->dx, &c->obs_z, &c->chi2, &c->p_w, &c->obs_ws, &c->obs_g, &c->tau, &c->ysq, &c->gamma, &c->scratch})
         b->release();
     for (auto* b : {&c->ncams, &c->ncams_snap, &c->info, &c->afail, &c->feat_filter, &c->feat_off, &c->obs_off, &c->obs_cam,
@@ -767,9 +742,6 @@ int msckf_destroy(msckf_ctx_t* c) {
     c->valid.release();
     c->accept.release();
     c->include.release();
-    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
-    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
-    if (c->side) (void)hipStreamDestroy(c->side);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return 0;

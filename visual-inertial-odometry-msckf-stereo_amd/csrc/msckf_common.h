@@ -91,12 +91,9 @@ struct FeatBatch {
 using KT = double;
 template <typename T>
 struct UpdWs {
-    KT* Hthin;   // [B][Cmax][Cmax+1]   (H_thin | r_thin): rows of the factor F, F^T F = H^T H
-    T* Hqr;      // [B][Cmax][Cmax+1]   QR row-merge output (MSCKF_COMPRESS=qr only)
-    KT* HP;      // [B][Cmax][Dmax]     H_thin P, then L^-1 H_thin P
-    KT* S;       // [B][Cmax][Cmax]     innovation covariance -> its Cholesky factor
+    KT* Hthin;   // [B][Cmax][Cmax+1]   [A | b] = [H^T H | H^T r] (k_info)
     KT* dx;      // [B][Dmax + Cmax]
-    int* info;   // [B][4]: rows stacked, n (rows of H_thin), compress flag, status
+    int* info;   // [B][4]: rows stacked, C (0: no update), compress flag, status
     int Cmax;
     // Cholesky-form Kalman stage (msckf_kalman.hip); Cp = Cmax rounded up to 4
     KT* Lc;      // [B][Cp][Cp]          chol(P_cc), lower

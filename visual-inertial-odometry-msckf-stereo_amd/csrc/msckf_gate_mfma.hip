@@ -48,8 +48,7 @@ __host__ __device__ constexpr int bidx(int rb, int cb) { return rb * (rb + 1) / 
 
 template <int NB, bool MP>
 __global__ void __launch_bounds__(256) k_gate_mfma(DevState<float> st, Params<float> prm, FeatBatch<float> fb,
-                                                   const int* __restrict__ flist, int nlist, int Mmax, int capb,
-                                                   int phases) {
+                                                   const int* __restrict__ flist, int nlist, int Mmax, int capb) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wpb = blockDim.x >> 6;
     // wave-uniform by construction; readfirstlane tells the compiler, so every
@@ -97,9 +96,7 @@ __global__ void __launch_bounds__(256) k_gate_mfma(DevState<float> st, Params<fl
     // (H_f~ = -Ht[:, 3:6]) in rows 12..15 of block nb - 1, unit padding pivots,
     // zeros.  The stage offset of Y[q][p] separates into a row part and a
     // column part: 9 (a (a + 1) / 2 + b) + 3 c_q + c_p with a = q / 3, b = p / 3.
-    // (phases: profiling aid, bit0 Y, bit2 elimination; without the Y phase the
-    // range rows get unit pivots so that the elimination still runs.)
-    const int pad_lo = (phases & 1) ? M3 : 0;
+    const int pad_lo = M3;
     const float s2 = prm.sigma2;
     auto assemble = [&](int R0, int R1, int kbase) {
         int col_l = lane & 15, rg = lane >> 4;   // opaque copies: index math stays in the pass loop
@@ -169,7 +166,7 @@ __global__ void __launch_bounds__(256) k_gate_mfma(DevState<float> st, Params<fl
             ++R1;
             ahi = ah2;
         }
-        const int kbase = alo * (alo + 1) / 2, nbp = (phases & 1) ? npairs(alo, ahi) : 0;
+        const int kbase = alo * (alo + 1) / 2, nbp = npairs(alo, ahi);
         for (int k0 = 0; k0 < nbp; k0 += 64 * BIF) {
             float Pl[BIF][36];
             int oa[BIF], ob[BIF];
@@ -240,7 +237,7 @@ __global__ void __launch_bounds__(256) k_gate_mfma(DevState<float> st, Params<fl
     const int csel = rg;   // pivot column of this lane's operands
 #pragma unroll
     for (int KB = 0; KB < NB; ++KB) {
-        if (4 * KB >= nY || fail || !(phases & 4)) break;
+        if (4 * KB >= nY || fail) break;
         for (int sc = 0; sc < 4; ++sc) {
             const int j = 4 * KB + sc;
             if (j >= nY) break;
@@ -604,29 +601,20 @@ void launch_cfg(hipStream_t s, const DevState<float>& st, const Params<float>& p
                                   (int)lds);
         attr = lds;
     }
-    static int phases = -1;   // MSCKF_GATE_PHASES: profiling aid (bit0 Y blocks, bit2 elimination)
-    if (phases < 0) {
-        const char* e = getenv("MSCKF_GATE_PHASES");
-        phases = e ? atoi(e) : 7;
-    }
     hipLaunchKernelGGL((k_gate_mfma<NB, MP>), dim3((cnt + wpb - 1) / wpb), dim3(64 * wpb), lds, s, st, prm, fb, list,
-                       cnt, Mmax, capb, phases);
+                       cnt, Mmax, capb);
 }
 
 template <int NB>
 void launch_nb(hipStream_t s, const DevState<float>& st, const Params<float>& prm, const FeatBatch<float>& fb,
                const int* list, int cnt, int Mmax) {
     // Y staging capacity: all M (M + 1) / 2 pair blocks in one pass unless four
-    // waves would then need more than MSCKF_GATE_SPKB KB; otherwise passes (of
+    // waves would then need more than 36 KB; otherwise passes (of
     // whole block rows) sized for half of that.  Multi-pass also drops the Y
     // phase's registers (one pair in flight per lane, 82-88 VGPRs), so the
     // classes with nb >= 4 gain a wave per SIMD.  Measured at 30x200 (gate
     // ms): budget 80: 3.46, 60: 3.28, 50: 3.10, 36: 3.05, 20 / 12: 3.06-3.10.
-    static int single_kb = -1;
-    if (single_kb < 0) {
-        const char* e = getenv("MSCKF_GATE_SPKB");
-        single_kb = e ? atoi(e) : 36;
-    }
+    constexpr int single_kb = 36;
     const int nbk = Mmax * (Mmax + 1) / 2;
     const int cmin = 6 * Mmax < nbk ? 6 * Mmax : nbk;   // one block row (up to six observation rows) per pass
     auto per_wave = [&](int cb) { return (size_t)gm_wave_floats(Mmax, cb) * sizeof(float); };

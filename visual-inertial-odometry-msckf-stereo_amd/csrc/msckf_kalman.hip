@@ -10,18 +10,16 @@
 // batched over filters:
 //   A  k_kal_a   partial Cholesky of [P_cc P_ci; P_ic P_ii] over the cam
 //                pivots: Lc, Vc_i = P_ic Lc^-T, S_ii = P_ii - Vc_i Vc_i^T
-//   B  k_kal_b1  G = A Lc;   k_kal_b2  [T | c] = s2 I + Lc^T [G | b]
-//   C  k_kal_c   Cholesky of T with the extra rows [Vc_i ; Lc ; c^T]
-//                appended: their panel rows are W = [Vc_i ; Lc] L_T^-T and
-//                y = L_T^-1 c (rows split over several workgroups per
-//                filter, each refactoring T)
-//   E  k_kal_e   P+ = blockdiag(S_ii, 0) + s2 W W^T and dx = W y
-// A and C keep the matrix in registers as 4x4 tiles (one workgroup per
-// filter); B and E are 64 x 64-tiled LDS GEMMs.
+//   B  k_kal_b   [T | c] = s2 I + Lc^T [A Lc | b] (fp64 MFMA accumulators)
+//   C  k_kal_c1  Cholesky of T; k_kal_c2: W^T = L_T^-1 [Vc_i ; Lc]^T and
+//                y = L_T^-1 c (MFMA blocked forward substitution)
+//   E  k_kal_e1  P+ = blockdiag(S_ii, 0) + s2 W W^T and dx = W y
+// Up to 32 cams A and C1 keep the matrix in registers as 4x4 tiles (one
+// workgroup per filter); larger windows run A and C as blocked global-memory
+// Choleskys (k_gchol_*) and B / E as 64 x 64-tiled GEMMs (k_kal_b1/b2, k_kal_e).
 #include "msckf_common.h"
 #include "msckf_launch.h"
 #include "msckf_rchol.h"
-#include "msckf_mchol.h"
 
 namespace msckf {
 
@@ -32,264 +30,13 @@ __device__ __forceinline__ int round4(int x) { return (x + 3) & ~3; }
 
 typedef double v4d __attribute__((ext_vector_type(4)));
 
-// ===========================================================================
-// MFMA partial Cholesky with 16-wide steps -- EXPERIMENTAL (MSCKF_KALMAN_TILE=16),
-// slower than rchol_core today: measured per 16 pivots ~27K cycles in the
-// wave-0 diagonal factor + inverse (serial sqrt / div / LDS chain) and ~20K in
-// the update (column reads of the [R][16] panel hit 8-way bank conflicts; each
-// slot's four MFMAs form one dependent chain).  One step per tile column of
-// 16 pivots.
-//   1. owners of the tile column dump it to LDS (buf[row][16], double-buffered)
-//   2. wave 0 factors the 16 x 16 diagonal block (lane i < 16 holds row i,
-//      right-looking with shuffles) and inverts it (lane j: column j of
-//      L_d^-1 by forward substitution); both go to LDS
-//   3. owners of the panel tiles form W = A L_d^-T as four MFMAs (operands from
-//      LDS), store it over the raw rows and to panel(); the diagonal tile's
-//      rows become zero (finished)
-//   4. every tile right of the panel takes acc -= W_i W_l^T as four
-//      v_mfma_f64_16x16x4 (k-chunks of 4 panel columns), operands from LDS.
-// Three barriers per 16 pivots.
-// ===========================================================================
-template <int NW, int TPW, class Load, class Panel, class Trail>
-__device__ __forceinline__ bool mchol16_core(int nrow, int ncol, int nelim, double* lds, Load load, Panel panel,
-                                             Trail trail, int dbg = 0) {
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int ntiles = ncol * nrow - ncol * (ncol - 1) / 2;
-    const int R = 16 * nrow;
-    const bool prof = dbg && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0;
-    unsigned long long tph[5] = {0, 0, 0, 0, 0}, tlast = prof ? __builtin_amdgcn_s_memtime() : 0;
-#define MPROF16(k)                                                       \
-    if (prof) {                                                          \
-        const unsigned long long now = __builtin_amdgcn_s_memtime();     \
-        tph[k] += now - tlast;                                           \
-        tlast = now;                                                     \
-    }
-    int crd[TPW], tlmax[TPW];
-#pragma unroll
-    for (int s = 0; s < TPW; ++s) {
-        const int t = NW * s + wv;
-        const int c = colmajor_col(t < ntiles ? t : 0, nrow);
-        const int rem = (t < ntiles ? t : 0) - (c * nrow - c * (c - 1) / 2);
-        crd[s] = __builtin_amdgcn_readfirstlane(t < ntiles ? ((c + rem) | (c << 16)) : -1);
-        const int tm = NW * s + NW - 1 < ntiles - 1 ? NW * s + NW - 1 : ntiles - 1;
-        tlmax[s] = __builtin_amdgcn_readfirstlane(NW * s < ntiles ? colmajor_col(tm, nrow) : -1);
-    }
-#define QTI(s) (crd[s] & 0xffff)
-#define QTL(s) (crd[s] >> 16)
-#define QOK(s) (crd[s] >= 0)
-    const int lc = lane & 15, lr = lane >> 4;
-    v4d acc[TPW];
-#pragma unroll
-    for (int s = 0; s < TPW; ++s) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[s][r] = QOK(s) ? load(16 * QTI(s) + lr + 4 * r, 16 * QTL(s) + lc) : 0.0;
-        asm volatile("" ::: "memory");
-    }
-    MPROF16(0);
-    double* Ld = lds + 2 * 16 * R;   // [16][16] L_d, [16][16] L_d^-1, then a failure flag
-    double* Linv = Ld + 256;
-    double* sflag = Linv + 256;
-    bool fail = false;
-    for (int tc = 0; 16 * tc < nelim; ++tc) {
-        double* buf = lds + (tc & 1) * 16 * R;   // [R][16]
-        // opaque per step: stops the compiler from hoisting every slot's row
-        // offsets / store addresses out of the loop (that alone spilled ~200 VGPRs)
-#pragma unroll
-        for (int s = 0; s < TPW; ++s) asm volatile("" : "+s"(crd[s]));
-#pragma unroll
-        for (int s = 0; s < TPW; ++s) {
-            if (!QOK(s) || QTL(s) != tc) continue;
-            const int row0 = 16 * QTI(s) + lr;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) buf[(row0 + 4 * r) * 16 + lc] = acc[s][r];
-        }
-        LDS_BARRIER();
-        MPROF16(1);
-        const int p0 = 16 * tc;
-        if (wv == 0) {   // 16 x 16 Cholesky of the diagonal block in place in LDS, then L_d^-1
-            // lane -> entries (i = lane & 15, j = 4 (lane >> 4) .. +3) of the block
-            double* blk = buf + p0 * 16;   // [16][16], row-major
-            const int bi = lane & 15, bj0 = 4 * (lane >> 4);
-            bool bad = false;
-            for (int k = 0; k < 16; ++k) {
-                const double piv = blk[k * 16 + k];
-                bad |= !(piv > 0.0);
-                const double d = sqrt(piv > 0.0 ? piv : 1.0), inv = 1.0 / d;
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // every lane has read the pivot
-                if (bj0 == (k & ~3) && bi >= k) blk[bi * 16 + k] = bi == k ? d : blk[bi * 16 + k] * inv;
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                const double lik = blk[bi * 16 + k];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int j = bj0 + q;
-                    if (j > k && bi >= j) blk[bi * 16 + j] -= lik * blk[j * 16 + k];
-                }
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            }
-            if (lane < 16) {
-#pragma unroll
-                for (int j = 0; j < 16; ++j) {
-                    const double v = j <= lane ? blk[lane * 16 + j] : 0.0;
-                    Ld[lane * 16 + j] = v;
-                    if (j <= lane) panel(p0 + lane, p0 + j, v);   // factor rows of the diagonal block
-                }
-            }
-            if (lane == 0) sflag[0] = bad ? 1.0 : 0.0;
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            // column j = lane of X = L_d^-1 by forward substitution (L_d rows broadcast from LDS)
-            double x[16];
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                double v = (i == lane) ? 1.0 : 0.0;
-#pragma unroll
-                for (int m = 0; m < i; ++m) v -= Ld[i * 16 + m] * x[m];
-                x[i] = v / Ld[i * 16 + i];
-            }
-            if (lane < 16) {
-#pragma unroll
-                for (int i = 0; i < 16; ++i) Linv[i * 16 + lane] = x[i];   // Linv[i][j] = (L_d^-1)[i][j]
-            }
-        }
-        LDS_BARRIER();
-        MPROF16(2);
-        if (sflag[0] != 0.0) { fail = true; break; }
-        // panel tiles (ti > tc): W = A L_d^-T as four MFMAs, B[k][n] = (L_d^-T)[k][n] = Linv[n][k];
-        // a tile's rows are read and rewritten only by its owner wave (no barrier between)
-#pragma unroll
-        for (int s = 0; s < TPW; ++s) {
-            if (!QOK(s) || QTL(s) != tc) continue;
-            const int row0 = 16 * QTI(s) + lr;
-            if (QTI(s) == tc) {   // diagonal tile: finished, enters the update as zero
-#pragma unroll
-                for (int r = 0; r < 4; ++r) buf[(row0 + 4 * r) * 16 + lc] = 0.0;
-                continue;
-            }
-            const double* ra = buf + (16 * QTI(s) + lc) * 16 + lr;
-            v4d wacc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-            for (int c = 0; c < 4; ++c)
-                wacc = __builtin_amdgcn_mfma_f64_16x16x4f64(ra[4 * c], Linv[lc * 16 + 4 * c + lr], wacc, 0, 0, 0);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                buf[(row0 + 4 * r) * 16 + lc] = wacc[r];
-                panel(row0 + 4 * r, p0 + lc, wacc[r]);
-            }
-        }
-        LDS_BARRIER();
-        MPROF16(3);
-#pragma unroll
-        for (int s = 0; s < TPW; ++s) {
-            if (tlmax[s] <= tc) continue;   // slot entirely in finished tile columns
-            if (!QOK(s) || QTL(s) <= tc) continue;
-            const double* ri = buf + (16 * QTI(s) + lc) * 16 + lr;
-            const double* rl = buf + (16 * QTL(s) + lc) * 16 + lr;
-#pragma unroll
-            for (int c = 0; c < 4; ++c)
-                acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(-ri[4 * c], rl[4 * c], acc[s], 0, 0, 0);
-        }
-        MPROF16(4);
-    }
-    if (prof)
-        printf("mchol16 wg0: load %llu dump+barrier %llu diag %llu panel %llu update %llu cycles (%d steps)\n",
-               tph[0], tph[1], tph[2], tph[3], tph[4], nelim / 16);
-#undef MPROF16
-    if (!fail) {
-#pragma unroll
-        for (int s = 0; s < TPW; ++s) {
-            if (!QOK(s) || 16 * QTL(s) < nelim) continue;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) trail(16 * QTI(s) + lr + 4 * r, 16 * QTL(s) + lc, acc[s][r]);
-        }
-    }
-#undef QTI
-#undef QTL
-#undef QOK
-    return !fail;
-}
-
-__device__ __forceinline__ int round16(int x) { return (x + 15) & ~15; }
-constexpr int KW16 = 32;   // IMU block padded to a multiple of 16 (MFMA path)
-
-// ---- stage A (MFMA): index space [cams (Cq = round16 C) | IMU (32)] ----
-template <typename T, int NW, int TPW>
-__global__ void __launch_bounds__(64 * NW) k_kal_a16(DevState<T> st, UpdWs<T> ws, int dbg) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    const int b = blockIdx.x;
-    const int* info = ws.info + 4 * b;
-    if (info[0] == 0) return;
-    const int C = 6 * st.ncams[b], Cq = round16(C);
-    const int nrow = (Cq + KW16) / 16;
-    const T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
-    const int ld = st.Dmax, Cpw = ws.Cp;
-    KT* Lc = ws.Lc + (size_t)b * Cpw * Cpw;
-    KT* Vi = ws.Vi + (size_t)b * KW * Cpw;
-    KT* Sii = ws.Sii + (size_t)b * KW * KW;
-    auto map = [&](int i) { return i < C ? 21 + i : (i < Cq ? -1 : (i < Cq + 21 ? i - Cq : -1)); };
-    auto load = [&](int i, int j) -> double {
-        const int mi = map(i), mj = map(j);
-        if (mi < 0 || mj < 0) return i == j ? 1.0 : 0.0;
-        return (double)P[(size_t)mi * ld + mj];
-    };
-    auto panel = [&](int r, int c, double v) {
-        if (r >= Cq + KW) return;
-        (r < Cq ? Lc + (size_t)r * Cpw : Vi + (size_t)(r - Cq) * Cpw)[c] = v;
-    };
-    auto trail = [&](int i, int j, double v) {
-        if (i - Cq < KW && j - Cq < KW) Sii[(i - Cq) * KW + (j - Cq)] = v;
-    };
-    const bool ok = mchol16_core<NW, TPW>(nrow, nrow, Cq, reinterpret_cast<double*>(smem_raw), load, panel, trail, dbg);
-    if (!ok && threadIdx.x == 0) ws.info[4 * b + 3] = -1;
-}
-
-// ---- stage C (MFMA): T (Cq) with extra rows [Vc_i (21); Lc (C); c^T], 16-row tiles ----
-template <typename T, int NW, int TPW>
-__global__ void __launch_bounds__(64 * NW) k_kal_c16(DevState<T> st, UpdWs<T> ws, int ner, int dbg) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    const int b = blockIdx.y, g = blockIdx.x;
-    const int* info = ws.info + 4 * b;
-    if (info[0] == 0) return;
-    const int C = 6 * st.ncams[b], Cq = round16(C), nTc = Cq / 16;
-    const int E = 21 + C + 1, ER = (E + 15) / 16;
-    const int e0 = g * ner;
-    if (e0 >= ER) return;
-    const int nr = ER - e0 < ner ? ER - e0 : ner;
-    const int Cpw = ws.Cp, ldt = ws.Cmax + 1;
-    const KT* Tm = ws.Tm + (size_t)b * ws.Cmax * ldt;
-    const KT* Lc = ws.Lc + (size_t)b * Cpw * Cpw;
-    const KT* Vi = ws.Vi + (size_t)b * KW * Cpw;
-    KT* W = ws.W + (size_t)b * (st.Dmax + 1) * Cpw;
-    auto load = [&](int i, int j) -> double {
-        if (i < Cq) {
-            if (i >= C || j >= C) return i == j ? 1.0 : 0.0;
-            return i >= j ? Tm[(size_t)i * ldt + j] : Tm[(size_t)j * ldt + i];
-        }
-        const int e = i - Cq + 16 * e0;
-        if (j >= C) return 0.0;
-        if (e < 21) return Vi[(size_t)e * Cpw + j];
-        if (e < 21 + C) return j <= e - 21 ? Lc[(size_t)(e - 21) * Cpw + j] : 0.0;
-        if (e == 21 + C) return Tm[(size_t)j * ldt + C];
-        return 0.0;
-    };
-    auto panel = [&](int r, int c, double v) {
-        if (r < Cq) return;
-        const int e = r - Cq + 16 * e0;
-        if (e < E) W[(size_t)e * Cpw + c] = v;
-    };
-    auto trail = [](int, int, double) {};
-    const bool ok = mchol16_core<NW, TPW>(nTc + nr, nTc, Cq, reinterpret_cast<double*>(smem_raw), load, panel, trail, dbg);
-    if (!ok && threadIdx.x == 0) ws.info[4 * b + 3] = -1;
-}
-
 // ---- stage A: [P_cc P_ci; P_ic P_ii] in index space [cams (Cp) | IMU (24)] ----
 template <typename T, int NT, int TPL>
-__global__ void __launch_bounds__(NT) k_kal_a(DevState<T> st, UpdWs<T> ws, int early) {
+__global__ void __launch_bounds__(NT) k_kal_a(DevState<T> st, UpdWs<T> ws) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int b = blockIdx.x;
     const int* info = ws.info + 4 * b;
-    // early: launched on the side stream while the feature kernels run, before
-    // k_select has written info -- stage A depends on P only
-    if (!early && info[0] == 0) return;
+    if (info[0] == 0) return;
     const int C = 6 * st.ncams[b], Cp = round4(C);
     const int nrow = (Cp + KW) / 4;
     const T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
@@ -310,123 +57,12 @@ __global__ void __launch_bounds__(NT) k_kal_a(DevState<T> st, UpdWs<T> ws, int e
     auto trail = [&](int i, int j, double v) { Sii[(i - Cp) * KW + (j - Cp)] = v; };
     const bool ok = rchol_core<NT, TPL>(nrow, nrow, Cp / 4, reinterpret_cast<double*>(smem_raw), load, panel, trail);
     if (threadIdx.x == 0) {
-        ws.afail[b] = ok ? 0 : 1;   // read by k_kal_c1 (info[3] may not exist yet when early)
-        if (!ok && !early) ws.info[4 * b + 3] = -1;
+        ws.afail[b] = ok ? 0 : 1;   // read by k_kal_c1
+        if (!ok) ws.info[4 * b + 3] = -1;
     }
 }
 
-// ---- stages A and C1 on fp64 MFMA tiles (msckf_mchol.h), n <= 208 ----
-template <typename T>
-__global__ void __launch_bounds__(64 * MC_NW) k_kal_a_m(DevState<T> st, UpdWs<T> ws, int early) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    const int b = blockIdx.x;
-    const int* info = ws.info + 4 * b;
-    if (!early && info[0] == 0) return;
-    const int C = 6 * st.ncams[b], Cp = round4(C);
-    const T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
-    const int ld = st.Dmax, Cpw = ws.Cp;
-    KT* Lc = ws.Lc + (size_t)b * Cpw * Cpw;
-    KT* Vi = ws.Vi + (size_t)b * KW * Cpw;
-    KT* Sii = ws.Sii + (size_t)b * KW * KW;
-    auto map = [&](int i) { return i < C ? 21 + i : (i < Cp ? -1 : (i < Cp + 21 ? i - Cp : -1)); };
-    auto load = [&](int i, int j) -> double {
-        const int mi = map(i), mj = map(j);
-        if (mi < 0 || mj < 0) return i == j ? 1.0 : 0.0;
-        return (double)P[(size_t)mi * ld + mj];
-    };
-    auto put = [&](int r, int c, double v) {
-        if (r < Cp) Lc[(size_t)r * Cpw + c] = v;
-        else Vi[(size_t)(r - Cp) * Cpw + c] = v;
-    };
-    auto trail = [&](int i, int j, double v) { Sii[(i - Cp) * KW + (j - Cp)] = v; };
-    const bool ok = mchol_core(Cp + KW, Cp / 4, reinterpret_cast<double*>(smem_raw), load, put, trail);
-    if (threadIdx.x == 0) {
-        ws.afail[b] = ok ? 0 : 1;
-        if (!ok && !early) ws.info[4 * b + 3] = -1;
-    }
-}
-
-template <typename T>
-__global__ void __launch_bounds__(64 * MC_NW) k_kal_c1_m(DevState<T> st, UpdWs<T> ws) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    const int b = blockIdx.x;
-    if (ws.info[4 * b] == 0) return;
-    if (ws.afail[b]) {   // stage A failed (P_cc not PD): no update for this filter
-        if (threadIdx.x == 0) ws.info[4 * b + 3] = -1;
-        return;
-    }
-    const int C = 6 * st.ncams[b], Cp = round4(C);
-    const int ldt = ws.Cmax + 1;
-    const KT* Tm = ws.Tm + (size_t)b * ws.Cmax * ldt;
-    KT* L = ws.G + (size_t)b * ws.Cmax * ldt;
-    auto load = [&](int i, int j) -> double {
-        if (i >= C || j >= C) return i == j ? 1.0 : 0.0;
-        return i >= j ? Tm[(size_t)i * ldt + j] : Tm[(size_t)j * ldt + i];
-    };
-    auto put = [&](int r, int c, double v) {
-        if (r < C && c < C && c <= r) L[(size_t)r * ldt + c] = v;
-    };
-    auto trail = [](int, int, double) {};
-    const bool ok = mchol_core(Cp, Cp / 4, reinterpret_cast<double*>(smem_raw), load, put, trail);
-    if (!ok && threadIdx.x == 0) ws.info[4 * b + 3] = -1;
-}
-
-// MSCKF_KAL_MCHOL=1: stages A / C1 on the fp64 MFMA workgroup Cholesky.  Off by
-// default: slower than rchol_core's 4x4 VALU tiles at 30x200 (A 1.45 vs 0.82 ms,
-// C1 1.15 vs 0.73 ms) -- fp64 MFMA has no rate advantage on MI355X, and eight
-// waves with two block rows each leave the MFMA pipe waiting on the step chain.
-static bool kal_mchol() {
-    static int en = -1;
-    if (en < 0) {
-        const char* e = getenv("MSCKF_KAL_MCHOL");
-        en = e ? atoi(e) : 0;
-    }
-    return en != 0;
-}
-
-// ---- stage C: Cholesky of T (Cp) with extra rows [Vc_i (21); Lc (C); c^T] ----
-// blockIdx.x = group g of extra-row tiles handled by this workgroup
-template <typename T, int NT, int TPL>
-__global__ void __launch_bounds__(NT) k_kal_c(DevState<T> st, UpdWs<T> ws, int ner) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    const int b = blockIdx.y, g = blockIdx.x;
-    const int* info = ws.info + 4 * b;
-    if (info[0] == 0) return;
-    const int C = 6 * st.ncams[b], Cp = round4(C), nTc = Cp / 4;
-    const int E = 21 + C + 1, ER = (E + 3) / 4;   // extra rows / extra tile rows
-    const int e0 = g * ner;                       // first extra tile row of this group
-    if (e0 >= ER) return;
-    const int nr = ER - e0 < ner ? ER - e0 : ner;
-    const int Cpw = ws.Cp, ldt = ws.Cmax + 1;
-    const KT* Tm = ws.Tm + (size_t)b * ws.Cmax * ldt;
-    const KT* Lc = ws.Lc + (size_t)b * Cpw * Cpw;
-    const KT* Vi = ws.Vi + (size_t)b * KW * Cpw;
-    KT* W = ws.W + (size_t)b * (st.Dmax + 1) * Cpw;
-    auto load = [&](int i, int j) -> double {
-        if (i < Cp) {   // T (lower stored), identity padding
-            if (i >= C || j >= C) return i == j ? 1.0 : 0.0;
-            return i >= j ? Tm[(size_t)i * ldt + j] : Tm[(size_t)j * ldt + i];
-        }
-        const int e = i - Cp + 4 * e0;
-        if (j >= C) return 0.0;
-        if (e < 21) return Vi[(size_t)e * Cpw + j];
-        if (e < 21 + C) return j <= e - 21 ? Lc[(size_t)(e - 21) * Cpw + j] : 0.0;
-        if (e == 21 + C) return Tm[(size_t)j * ldt + C];
-        return 0.0;
-    };
-    auto panel = [&](int r, int c0, double w0, double w1, double w2, double w3) {
-        if (r < Cp) return;
-        const int e = r - Cp + 4 * e0;
-        if (e >= E) return;
-        KT* dst = W + (size_t)e * Cpw + c0;
-        dst[0] = w0; dst[1] = w1; dst[2] = w2; dst[3] = w3;
-    };
-    auto trail = [](int, int, double) {};
-    const bool ok = rchol_core<NT, TPL>(nTc + nr, nTc, nTc, reinterpret_cast<double*>(smem_raw), load, panel, trail);
-    if (!ok && threadIdx.x == 0) ws.info[4 * b + 3] = -1;
-}
-
-// ---- stage C, split form (production path when C <= 16 * NTM) ----
+// ---- stage C (register-tile windows, C <= 192) ----
 // C1: Cholesky of T alone (4x4 register tiles, one workgroup per filter), L_T
 //     written over the G workspace (free after stage B).
 // C2: W^T = L_T^-1 X^T with X = [Vc_i ; Lc ; c^T] (E = 22 + C rows) as a
@@ -438,7 +74,7 @@ __global__ void __launch_bounds__(NT) k_kal_c(DevState<T> st, UpdWs<T> ws, int n
 //         Y'[J] = Linv_JJ (X^T[J] - sum_{K<J} L_T[J, K] Y'[K])
 //     with -L_T[J, 0:16J] staged in LDS ([col][row], 17-double rows) and the
 //     16 x 16 inverses of the diagonal blocks formed once up front.  W^T is
-//     stored row-major over k (coalesced), the layout k_kal_e1<WT=true> reads.
+//     stored row-major over k (coalesced), the layout k_kal_e1 reads.
 template <typename T, int NT, int TPL>
 __global__ void __launch_bounds__(NT) k_kal_c1(DevState<T> st, UpdWs<T> ws) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
@@ -1088,7 +724,7 @@ __global__ void __launch_bounds__(256) k_kal_e(DevState<T> st, Params<T> prm, Up
 // MFMA accumulators.  W streams once through double-buffered LDS in chunks of
 // 16 columns ([k][row] images, so each MFMA operand is one ds_read_b64); the
 // same chunks give dx = W y (thread i < D accumulates row i).
-template <typename T, int NW, int TPW, bool WT>
+template <typename T, int NW, int TPW>
 __global__ void __launch_bounds__(64 * NW) k_kal_e1(DevState<T> st, Params<T> prm, UpdWs<T> ws) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int b = blockIdx.x;
@@ -1119,29 +755,23 @@ __global__ void __launch_bounds__(64 * NW) k_kal_e1(DevState<T> st, Params<T> pr
     // current chunk's MFMAs, put() after them
     constexpr int NT = 64 * NW, Q = (16 * 16 * (NW * TPW <= 96 ? 13 : 15) + NT - 1) / NT;
     double rw[Q], ry = 0.0;
-    // WT: W stored transposed (row-major over k, leading dimension Dmax + 1; stage C2)
+    // W^T as stage C2 stores it: row-major over k, leading dimension Dmax + 1
     const int ldw = st.Dmax + 1;
     auto load = [&](int k0) {
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
             const int e = tid + NT * q;
-            if (WT) {
-                const int k = e / Dp, row = e - k * Dp;
-                rw[q] = (e < 16 * Dp && row < D && k0 + k < C) ? W[(size_t)(k0 + k) * ldw + row] : 0.0;
-            } else {
-                const int row = e >> 4, k = e & 15;
-                rw[q] = (e < 16 * Dp && row < D && k0 + k < C) ? W[(size_t)row * Cpw + k0 + k] : 0.0;
-            }
+            const int k = e / Dp, row = e - k * Dp;
+            rw[q] = (e < 16 * Dp && row < D && k0 + k < C) ? W[(size_t)(k0 + k) * ldw + row] : 0.0;
         }
-        if (tid < 16)
-            ry = k0 + tid < C ? (WT ? W[(size_t)(k0 + tid) * ldw + D] : W[(size_t)D * Cpw + k0 + tid]) : 0.0;
+        if (tid < 16) ry = k0 + tid < C ? W[(size_t)(k0 + tid) * ldw + D] : 0.0;
     };
     auto put = [&](int buf) {
         double* im = img + buf * 16 * Dp;
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
             const int e = tid + NT * q;
-            if (e < 16 * Dp) im[WT ? e : (e & 15) * Dp + (e >> 4)] = rw[q];
+            if (e < 16 * Dp) im[e] = rw[q];
         }
         if (tid < 16) yb[buf * 16 + tid] = ry;
     };
@@ -1205,25 +835,9 @@ static bool pick_rchol(int tiles, RcholCfg& c) {
 }
 
 template <typename T, int NT, int TPL>
-static void launch_a_cfg(hipStream_t s, const DevState<T>& st, const UpdWs<T>& ws, size_t lds, int early = 0) {
-    hipLaunchKernelGGL((k_kal_a<T, NT, TPL>), dim3(st.B), dim3(NT), lds, s, st, ws, early);
+static void launch_a_cfg(hipStream_t s, const DevState<T>& st, const UpdWs<T>& ws, size_t lds) {
+    hipLaunchKernelGGL((k_kal_a<T, NT, TPL>), dim3(st.B), dim3(NT), lds, s, st, ws);
 }
-template <typename T, int NT, int TPL>
-static void launch_c_cfg(hipStream_t s, const DevState<T>& st, const UpdWs<T>& ws, int groups, int ner, size_t lds) {
-    hipLaunchKernelGGL((k_kal_c<T, NT, TPL>), dim3(groups, st.B), dim3(NT), lds, s, st, ws, ner);
-}
-
-
-// MFMA path configurations (waves, tiles per wave) that compile without
-// spills: 14 accumulator tiles (112 VGPRs) in a 256-register budget at 8
-// waves, 8 tiles (64 VGPRs) in a 128-register budget at 16 waves.
-struct MfmaCfg { int nw, tpw; };
-static bool pick_mfma(int tiles, MfmaCfg& c) {
-    if (tiles <= 8 * 14) { c = {8, 14}; return true; }
-    if (tiles <= 16 * 8) { c = {16, 8}; return true; }
-    return false;
-}
-
 
 // Host side of the blocked global-memory factorisation (large windows).
 template <int STAGE, typename T>
@@ -1249,65 +863,19 @@ static void launch_gchol(hipStream_t s, const DevState<T>& st, const UpdWs<T>& w
     else hipLaunchKernelGGL(k_gchol_c_store<T>, dim3(ld_chunks, st.B), dim3(256), 0, s, st, ws);
 }
 
-static bool mfma_kalman(int Cmax) {
-    static int mode = -1;   // MSCKF_KALMAN_TILE=16 selects the experimental MFMA tiles (A/B runs)
-    if (mode < 0) {
-        const char* e = getenv("MSCKF_KALMAN_TILE");
-        mode = (e && atoi(e) == 16) ? 1 : 0;
-    }
-    if (!mode) return false;
-    const int Cq = (Cmax + 15) & ~15;
-    const int nrowA = (Cq + 32) / 16, nTc = Cq / 16;
-    MfmaCfg c;
-    return pick_mfma(nrowA * (nrowA + 1) / 2, c) && pick_mfma(nTc * (nTc + 1) / 2 + nTc, c);
-}
-
-bool kalman_chol_supported(int Cmax) {
-    if (mfma_kalman(Cmax)) return true;
-    const int Cp = (Cmax + 3) & ~3;
-    const int nrowA = (Cp + KW) / 4;
-    RcholCfg c;
-    if (!pick_rchol(nrowA * (nrowA + 1) / 2, c)) return false;
-    const int nTc = Cp / 4;
-    return pick_rchol(nTc * (nTc + 1) / 2 + nTc, c);
-}
+// Register-tile stages A / C1 / C2 and E1 up to 32 cams (C <= 192); larger
+// windows run A and C as blocked global-memory Choleskys.
+bool kalman_chol_supported(int Cmax) { return ((Cmax + 15) & ~15) <= 16 * 12; }
 
 template <typename T, int NW, int TPW>
-static void launch_a16(hipStream_t s, const DevState<T>& st, const UpdWs<T>& ws, size_t lds) {
+static void launch_e1(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const UpdWs<T>& ws, size_t lds) {
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_kal_a16<T, NW, TPW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)hipFuncSetAttribute((const void*)k_kal_e1<T, NW, TPW>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   160 * 1024);
         attr = true;
     }
-    static const int dbg = getenv("MSCKF_DBG_KAL") ? 1 : 0;
-    hipLaunchKernelGGL((k_kal_a16<T, NW, TPW>), dim3(st.B), dim3(64 * NW), lds, s, st, ws, dbg);
-}
-template <typename T, int NW, int TPW>
-static void launch_c16(hipStream_t s, const DevState<T>& st, const UpdWs<T>& ws, int groups, int ner, size_t lds) {
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_kal_c16<T, NW, TPW>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
-        attr = true;
-    }
-    static const int dbg = getenv("MSCKF_DBG_KAL") ? 1 : 0;
-    hipLaunchKernelGGL((k_kal_c16<T, NW, TPW>), dim3(groups, st.B), dim3(64 * NW), lds, s, st, ws, ner, dbg);
-}
-
-template <typename T, int NW, int TPW>
-static void launch_e1(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const UpdWs<T>& ws, size_t lds,
-                      bool wt) {
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_kal_e1<T, NW, TPW, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
-        (void)hipFuncSetAttribute((const void*)k_kal_e1<T, NW, TPW, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
-        attr = true;
-    }
-    if (wt) hipLaunchKernelGGL((k_kal_e1<T, NW, TPW, true>), dim3(st.B), dim3(64 * NW), lds, s, st, prm, ws);
-    else hipLaunchKernelGGL((k_kal_e1<T, NW, TPW, false>), dim3(st.B), dim3(64 * NW), lds, s, st, prm, ws);
+    hipLaunchKernelGGL((k_kal_e1<T, NW, TPW>), dim3(st.B), dim3(64 * NW), lds, s, st, prm, ws);
 }
 
 template <typename T, int NT, int TPL>
@@ -1338,147 +906,57 @@ static void launch_b(hipStream_t s, const DevState<T>& st, const Params<T>& prm,
     hipLaunchKernelGGL((k_kal_b<T, NW, WR, WC, NTM>), dim3(st.B), dim3(64 * NW), lds, s, st, prm, ws);
 }
 
-// Stage A (4x4-tile path) can run before the update's feature kernels finish:
-// it reads P only.  With MSCKF_KALMAN_A_EARLY=1 the context forks it onto a
-// side stream at the start of the update chain and joins before stage B.  Off
-// by default: at 2048 x 30x200 the chip is already full -- stage A stretched
-// from 0.82 to 2.8 ms and the gating from 3.5 to 3.7 ms, no net change.
-bool kalman_a_early(int Cmax) {
-    static int en = -1;
-    if (en < 0) {
-        const char* e = getenv("MSCKF_KALMAN_A_EARLY");
-        en = e ? atoi(e) : 0;
-    }
-    return en && update_mode(Cmax) == UPD_CHOL && kalman_chol_supported(Cmax) && !mfma_kalman(Cmax);
-}
-
-template <typename T>
-void launch_kalman_a_early(hipStream_t s, const DevState<T>& st, const UpdWs<T>& ws) {
-    const int Cp = (ws.Cmax + 3) & ~3;
-    if (kal_mchol() && mchol_fits(Cp + KW)) {
-        hipLaunchKernelGGL(k_kal_a_m<T>, dim3(st.B), dim3(64 * MC_NW), mchol_lds_doubles() * sizeof(double), s, st, ws,
-                           1);
-        return;
-    }
-    const int nrow = (Cp + KW) / 4;
-    RcholCfg c;
-    pick_rchol(nrow * (nrow + 1) / 2, c);
-    const size_t lds = rchol_lds_doubles(nrow) * sizeof(double);
-    if (c.nt == 256) launch_a_cfg<T, 256, 4>(s, st, ws, lds, 1);
-    else launch_a_cfg<T, 512, 4>(s, st, ws, lds, 1);
-}
-
 template <typename T>
 void launch_kalman_chol(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const UpdWs<T>& ws,
-                        KernelTimer* kt, bool a_done) {
+                        KernelTimer* kt) {
     const int Cp = (ws.Cmax + 3) & ~3, Cmax = ws.Cmax;
-    const bool mf = mfma_kalman(Cmax);
-    const bool glob = !kalman_chol_supported(Cmax);   // large window: global-memory stages A and C
+    const bool reg = kalman_chol_supported(Cmax);   // else large window: global-memory stages A and C
     const int Cq = (Cmax + 15) & ~15;
-    if (a_done) {
-        // stage A already ran on the side stream (launch_kalman_a_early)
-    } else if (glob) {
-        kt->begin(s, "kalman_a");
-        launch_gchol<0, T>(s, st, ws);
-        kt->end(s);
-    } else if (mf) {   // stage A, MFMA tiles
-        const int nrow = (Cq + 32) / 16;
-        MfmaCfg c;
-        pick_mfma(nrow * (nrow + 1) / 2, c);
-        const size_t lds = (2 * 16 * 16 * (size_t)nrow + 512 + 8) * sizeof(double);
-        kt->begin(s, "kalman_a");
-        if (c.nw == 8) launch_a16<T, 8, 14>(s, st, ws, lds);
-        else launch_a16<T, 16, 8>(s, st, ws, lds);
-        kt->end(s);
-    } else if (kal_mchol() && mchol_fits(Cp + KW)) {   // stage A, fp64 MFMA tiles
-        kt->begin(s, "kalman_a");
-        hipLaunchKernelGGL(k_kal_a_m<T>, dim3(st.B), dim3(64 * MC_NW), mchol_lds_doubles() * sizeof(double), s, st, ws,
-                           0);
-        kt->end(s);
-    } else {   // stage A, 4x4 VALU tiles
+    kt->begin(s, "kalman_a");
+    if (reg) {   // stage A, 4x4 register tiles
         const int nrow = (Cp + KW) / 4;
         RcholCfg c;
         pick_rchol(nrow * (nrow + 1) / 2, c);
         const size_t lds = rchol_lds_doubles(nrow) * sizeof(double);
-        kt->begin(s, "kalman_a");
         if (c.nt == 256) launch_a_cfg<T, 256, 4>(s, st, ws, lds);
         else launch_a_cfg<T, 512, 4>(s, st, ws, lds);
-        kt->end(s);
+    } else {
+        launch_gchol<0, T>(s, st, ws);
     }
-    const int tiles = (Cmax + GT - 1) / GT;
+    kt->end(s);
     kt->begin(s, "kalman_b");
     if (Cq <= 16 * 8) {
         launch_b<T, 8, 4, 2, 8>(s, st, prm, ws, (4 * 16 * (size_t)Cq + 32) * sizeof(double));
     } else if (Cq <= 16 * 12) {
-        static const int bnw = getenv("MSCKF_KB_NW") ? atoi(getenv("MSCKF_KB_NW")) : 16;
-        if (bnw == 16) launch_b<T, 16, 4, 4, 12>(s, st, prm, ws, (4 * 16 * (size_t)Cq + 32) * sizeof(double));
-        else launch_b<T, 8, 4, 2, 12>(s, st, prm, ws, (4 * 16 * (size_t)Cq + 32) * sizeof(double));
+        launch_b<T, 16, 4, 4, 12>(s, st, prm, ws, (4 * 16 * (size_t)Cq + 32) * sizeof(double));
     } else {   // large windows: 64 x 64 output tiles, one workgroup each
+        const int tiles = (Cmax + GT - 1) / GT;
         hipLaunchKernelGGL(k_kal_b1<T>, dim3(tiles, tiles, st.B), dim3(256), 0, s, st, ws);
         hipLaunchKernelGGL(k_kal_b2<T>, dim3((Cmax + 1 + GT - 1) / GT, tiles, st.B), dim3(256), 0, s, st, prm, ws);
     }
     kt->end(s);
-    // split stage C (C1 + C2) whenever the register tiles of C1 and C2 fit
-    static const int csplit = getenv("MSCKF_KAL_C_SPLIT") ? atoi(getenv("MSCKF_KAL_C_SPLIT")) : 1;
-    const bool split = csplit && !glob && !mf && Cq <= 16 * 12;
-    if (glob) {
-        kt->begin(s, "kalman_c");
-        launch_gchol<1, T>(s, st, ws);
-        kt->end(s);
-    } else if (split) {
+    kt->begin(s, "kalman_c");
+    if (reg) {   // C1: Cholesky of T (register tiles); C2: MFMA forward substitution of the extra rows
         const int nTc = Cp / 4;
         RcholCfg c;
         pick_rchol(nTc * (nTc + 1) / 2, c);
         const size_t lds = rchol_lds_doubles(nTc) * sizeof(double);
-        kt->begin(s, "kalman_c");
-        if (kal_mchol() && mchol_fits(Cp))
-            hipLaunchKernelGGL(k_kal_c1_m<T>, dim3(st.B), dim3(64 * MC_NW), mchol_lds_doubles() * sizeof(double), s, st,
-                               ws);
-        else if (c.nt == 256) launch_c1<T, 256, 4>(s, st, ws, lds);
+        if (c.nt == 256) launch_c1<T, 256, 4>(s, st, ws, lds);
         else launch_c1<T, 512, 4>(s, st, ws, lds);
         if (Cq <= 16 * 8) launch_c2<T, 7, 2, 8>(s, st, ws);
         else launch_c2<T, 7, 2, 12>(s, st, ws);
-        kt->end(s);
-    } else if (mf) {   // stage C, MFMA tiles: T + as many extra-row tiles as fit, the rest in more groups
-        const int nTc = Cq / 16, Tt = nTc * (nTc + 1) / 2;
-        const int ER = (21 + Cmax + 1 + 15) / 16;
-        MfmaCfg c{16, 8};
-        if (Tt + ER * nTc <= 8 * 14) c = {8, 14};
-        if (const char* e = getenv("MSCKF_KAL_C_CFG")) c = atoi(e) == 8 ? MfmaCfg{8, 14} : MfmaCfg{16, 8};
-        const int ner_max = (c.nw * c.tpw - Tt) / nTc;
-        const int groups = (ER + ner_max - 1) / ner_max;
-        const int ner = (ER + groups - 1) / groups;
-        const size_t lds = (2 * 16 * 16 * (size_t)(nTc + ner) + 512 + 8) * sizeof(double);
-        kt->begin(s, "kalman_c");
-        if (c.nw == 8) launch_c16<T, 8, 14>(s, st, ws, groups, ner, lds);
-        else launch_c16<T, 16, 8>(s, st, ws, groups, ner, lds);
-        kt->end(s);
-    } else {   // stage C, 4x4 VALU tiles: T tiles + as many extra-row tiles as fit
-        const int nTc = Cp / 4, Tt = nTc * (nTc + 1) / 2;
-        const int ER = (21 + Cmax + 1 + 3) / 4;
-        RcholCfg c{512, 4};
-        if (Tt + ER * nTc <= 256 * 4) c = {256, 4};
-        const int ner_max = (c.nt * c.tpl - Tt) / nTc;
-        const int groups = (ER + ner_max - 1) / ner_max;
-        const int ner = (ER + groups - 1) / groups;
-        const size_t lds = rchol_lds_doubles(nTc + ner) * sizeof(double);
-        kt->begin(s, "kalman_c");
-        if (c.nt == 256) launch_c_cfg<T, 256, 4>(s, st, ws, groups, ner, lds);
-        else launch_c_cfg<T, 512, 4>(s, st, ws, groups, ner, lds);
-        kt->end(s);
+    } else {
+        launch_gchol<1, T>(s, st, ws);
     }
+    kt->end(s);
     kt->begin(s, "kalman_e");
     const int nTe = (st.Dmax + 15) / 16, tilesE = nTe * (nTe + 1) / 2;
     const size_t ldsE = (2 * 16 * 16 * (size_t)nTe + 32) * sizeof(double);
-    static const int enw = getenv("MSCKF_KE_NW") ? atoi(getenv("MSCKF_KE_NW")) : 16;
-    if (tilesE <= 16 * 6 && enw == 16) {
-        launch_e1<T, 16, 6>(s, st, prm, ws, ldsE, split);
-    } else if (tilesE <= 8 * 12) {
-        launch_e1<T, 8, 12>(s, st, prm, ws, ldsE, split);
-    } else if (tilesE <= 8 * 16) {
-        launch_e1<T, 8, 16>(s, st, prm, ws, ldsE, split);
-    } else {
-        if (split) { fprintf(stderr, "msckf: split stage C needs k_kal_e1\n"); abort(); }   // large windows: one 64 x 64 tile per workgroup
+    if (reg && tilesE <= 16 * 6) {
+        launch_e1<T, 16, 6>(s, st, prm, ws, ldsE);
+    } else if (reg) {
+        launch_e1<T, 8, 16>(s, st, prm, ws, ldsE);
+    } else {   // large windows: one 64 x 64 tile per workgroup
         const int dt = (st.Dmax + GT - 1) / GT, dt1 = (st.Dmax + 1 + GT - 1) / GT;
         hipLaunchKernelGGL(k_kal_e<T>, dim3(dt1, dt, st.B), dim3(256), 0, s, st, prm, ws);
     }
@@ -1486,10 +964,8 @@ void launch_kalman_chol(hipStream_t s, const DevState<T>& st, const Params<T>& p
 }
 
 template void launch_kalman_chol<float>(hipStream_t, const DevState<float>&, const Params<float>&,
-                                        const UpdWs<float>&, KernelTimer*, bool);
+                                        const UpdWs<float>&, KernelTimer*);
 template void launch_kalman_chol<double>(hipStream_t, const DevState<double>&, const Params<double>&,
-                                         const UpdWs<double>&, KernelTimer*, bool);
-template void launch_kalman_a_early<float>(hipStream_t, const DevState<float>&, const UpdWs<float>&);
-template void launch_kalman_a_early<double>(hipStream_t, const DevState<double>&, const UpdWs<double>&);
+                                         const UpdWs<double>&, KernelTimer*);
 
 }  // namespace msckf

@@ -11,11 +11,12 @@
 //                                            jit_utils.py:137-167   -> k_augment
 //   Feature.initialize_position feature.py:167-295                  -> k_triangulate
 //   measurement_jacobian + feature_jacobian msckf.py:429-541        -> k_feature
-//   gating_test msckf.py:606-614                                    -> k_gate
+//   gating_test msckf.py:606-614                                    -> k_gate_wave /
+//                       k_gate_big / k_gate_lds / k_gate (fp32: msckf_gate_mfma.hip)
 //   stacking + row cap msckf.py:661-682, 776-798                    -> k_select
-//   measurement_update QR msckf.py:549-556 (_fastQR)                -> k_compress_reg
-//   measurement_update S, K, dx, P msckf.py:559-604 (_fastSolve)    -> k_hp, k_s,
-//                                  k_chol, k_trsm, k_dx, k_pupdate, k_correct
+//   measurement_update QR msckf.py:549-556 (_fastQR)                -> k_info
+//   measurement_update S, K, dx, P msckf.py:559-604 (_fastSolve)    -> msckf_kalman.hip,
+//                                                                      k_correct
 //   P compaction msckf.py:803-818                                   -> k_prune_*
 #include <type_traits>
 
@@ -1238,8 +1239,7 @@ __host__ __device__ constexpr int gate_wave_lds_T(int Mmax, int capb) {
 
 template <typename T, int TPL, bool MP>
 __global__ void __launch_bounds__(256) k_gate_wave(DevState<T> st, Params<T> prm, FeatBatch<T> fb,
-                                                   const int* __restrict__ flist, int nlist, int Mmax, int capb,
-                                                   int phases) {
+                                                   const int* __restrict__ flist, int nlist, int Mmax, int capb) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wpb = blockDim.x >> 6;
     const int li = xcd_remap(blockIdx.x, gridDim.x) * wpb + wv;
@@ -1326,7 +1326,7 @@ __global__ void __launch_bounds__(256) k_gate_wave(DevState<T> st, Params<T> prm
         }
     };
     if (MP) { init_tiles(); tiles_init = true; }
-    for (int c0 = 0; c0 < ((phases & 1) ? M : 0);) {
+    for (int c0 = 0; c0 < M;) {
         int c1 = c0, nbp = 0;
         while (c1 < M) {
             const int ce = c1 + 4 < M ? c1 + 4 : M;
@@ -1461,7 +1461,7 @@ __global__ void __launch_bounds__(256) k_gate_wave(DevState<T> st, Params<T> prm
 
     // ---- blocked LDL^T over the nY Y tile columns, 4 pivots per step ----
     bool fail = false;
-    for (int tj = 0; tj < ((phases & 4) ? nY : 0); ++tj) {
+    for (int tj = 0; tj < nY; ++tj) {
         // 1. owners of the tile column dump it (raw rows 4 tj .. 4 nT - 1)
 #pragma unroll
         for (int s = 0; s < TPL; ++s) {
@@ -1753,47 +1753,36 @@ __global__ void __launch_bounds__(256) k_select(DevState<T> st, FeatBatch<T> fb,
 }
 
 // ===========================================================================
-// Information assembly + factorisation (replaces the QR compression of
+// Information assembly (replaces the QR compression of
 // msckf.py:549-556).  The update msckf.py:559-604 depends on the stacked
 // (H, r) only through A = H^T H and b = H^T r:
 //   K r = P H^T (H P H^T + s2 I)^-1 r = P (A P + s2 I)^-1 b,
 //   K H P = P (A P + s2 I)^-1 A P,
-// so any F, r_F with F^T F = A and F^T r_F = b gives the reference's update --
-// the QR's [R | Q^T r] is one such pair, the pivoted Cholesky factor of the
-// augmented Gram matrix [A b] is another.  Per feature the projected block's
-// Gram matrix is assembled from the fp64 terms of k_feature:
+// so the Cholesky-form Kalman stage (msckf_kalman.hip) takes [A | b] in place
+// of the QR's [R | Q^T r].  Per feature the projected block's Gram matrix is
+// assembled from the fp64 terms of k_feature:
 //   H0^T H0 = blockdiag_i(Hx_i^T Hx_i) - G^T G,   H0^T r0 = sum_i UB_i,
 // which needs O(M^2) work per feature and never materialises the stacked
 // rows (the QR merge streamed its C x C factor through memory once per
 // 16-row chunk: ~160 GB per 2048-filter launch, profiles/r01/README.md).
 //
-// One workgroup per filter.  Thread t owns 6x6 cam-pair blocks (I >= J) of A
-// in registers (block index t + NT m, m < BPT); features are staged FB at a
-// time in LDS, indexed by cam, with a cam bitmask per feature, and each
-// thread accumulates the blocks whose two cams the feature observes.  Then an
-// outer-product Cholesky with diagonal pivoting runs on the register blocks:
-// per step the diagonal owners publish their diagonal, wave 0 picks the
-// pivot, the owners of the pivot's row publish it scaled (the row of F), and
-// every block takes the rank-1 downdate.  It stops at the numerical rank
-// (pivot <= tol_rel * max diag(A)): the 4 gauge directions that the
-// observability-constrained Jacobians leave unobservable (eigenvalues
-// ~1e-17 |A| against >= 1e-6 |A| for the observable ones on the bench
-// problems) carry no information and produce no row.
-// Output: rows 0..n-1 of [F | r_F] in H_thin (KT), n = rank in info[1].
+// One workgroup per filter (several for Nmax > 40).  Each wave owns an 8 x 8
+// tile of cam pairs (lane: I = 8 ti + lane / 8, J = 8 tj + lane % 8), the
+// thread its 6x6 block of A in registers; features are staged FB at a time in
+// LDS, indexed by cam, with a cam bitmask per feature, and each thread
+// accumulates the blocks whose two cams the feature observes.
+// Output: [A | b] in H_thin (Cmax x (Cmax + 1), KT), info[1] = C.
 // ===========================================================================
-// features staged per round (one staging wave each): 5, 4, 2 or 1, as many as
-// the double-buffered slots fit in LDS
-// (five, or as many as fit: 2 x 5 slots at <= 40 cams, 4 at 50, 2 at 80 -- measured at 30x200
-// four / five / six: 2.17 / 2.06 / 2.11 ms; at 50x400 two / three / four: 3.0 / 2.5 / 2.18 ms)
-__host__ __device__ constexpr int info_fb(int Nmax) { return Nmax > 0 ? 5 : 1; }
-
+// features staged per round (one staging wave each): five, capped by what the
+// double-buffered slots leave of the LDS (measured at 30x200 four / five / six:
+// 2.17 / 2.06 / 2.11 ms; at 50x400 two / three / four: 3.0 / 2.5 / 2.18 ms)
+constexpr int INFO_FB_MAX = 5;
 // Doubles per staging slot: a feature's M <= Nmax records copied contiguously,
 // rounded up to whole 1 KiB global_load_lds wave-instructions.
 __host__ __device__ constexpr int info_slot_doubles(int Nmax) { return (Nmax * OBG_STRIDE + 127) / 128 * 128; }
 
 template <typename T, int BPT, int NT>
-__global__ void __launch_bounds__(NT) k_info(DevState<T> st, FeatBatch<T> fb, UpdWs<T> ws, double tol_rel,
-                                             int phases, int assemble_only, int tiled, int fbn) {
+__global__ void __launch_bounds__(NT) k_info(DevState<T> st, FeatBatch<T> fb, UpdWs<T> ws, int fbn) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int b = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwave = NT >> 6;
@@ -1805,43 +1794,27 @@ __global__ void __launch_bounds__(NT) k_info(DevState<T> st, FeatBatch<T> fb, Up
     }
     const int SLOT = info_slot_doubles(Nmax), INFO_FB = fbn;
     double* rec = reinterpret_cast<double*>(smem_raw);                      // [2][FB][SLOT]
-    double* fvec = rec + (size_t)2 * INFO_FB * SLOT;                         // [Cmax + 1]
-    double* dval = fvec + Cmax + 1;                                          // [Cmax]
-    unsigned long long* mask = reinterpret_cast<unsigned long long*>(dval + Cmax);   // [2][FB][2] cams 0..127
-    int* chosen = reinterpret_cast<int*>(mask + 4 * INFO_FB);                // [Cmax]
-    int* pos = chosen + Cmax;                                                // [2][FB][Nmax] cam -> record
-    __shared__ int s_p, s_stop;
-    __shared__ double s_inv, s_d0;
+    unsigned long long* mask = reinterpret_cast<unsigned long long*>(rec + (size_t)2 * INFO_FB * SLOT);   // [2][FB][2]
+    int* pos = reinterpret_cast<int*>(mask + 4 * INFO_FB);                   // [2][FB][Nmax] cam -> record
 
     double a[BPT][6][6], bv[BPT][6];
     int I[BPT], J[BPT];
     bool act[BPT];
 #pragma unroll
     for (int m = 0; m < BPT; ++m) {
-        if (tiled) {
-            // wave = one 8 x 8 tile of cam pairs (lane: I = 8 ti + lane / 8, J = 8 tj + lane % 8):
-            // a feature's contiguous cam range [s, e] activates the pairs s <= J <= I <= e,
-            // a triangle that whole tiles cover far better than the row-major block order
-            // (whose 64-block strips are mostly inactive for every feature)
-            const int tt = blockIdx.y * (NT >> 6) * BPT + (tid >> 6) + (NT >> 6) * m;
-            const int TS = (Nmax + 7) >> 3, ntl = TS * (TS + 1) / 2;
-            int ti = (int)((sqrtf(8.0f * (float)tt + 1.0f) - 1.0f) * 0.5f);
-            while (ti * (ti + 1) / 2 > tt) --ti;
-            while ((ti + 1) * (ti + 2) / 2 <= tt) ++ti;
-            const int tj = tt - ti * (ti + 1) / 2;
-            I[m] = 8 * ti + (lane >> 3);
-            J[m] = 8 * tj + (lane & 7);
-            act[m] = tt < ntl && I[m] < nc && J[m] <= I[m];
-        } else {
-            // blocks of this workgroup: part blockIdx.y of the filter's lower-triangle blocks
-            const int blk = blockIdx.y * (NT * BPT) + tid + NT * m;
-            int i = (int)((sqrtf(8.0f * (float)blk + 1.0f) - 1.0f) * 0.5f);
-            while (i * (i + 1) / 2 > blk) --i;
-            while ((i + 1) * (i + 2) / 2 <= blk) ++i;
-            I[m] = i;
-            J[m] = blk - i * (i + 1) / 2;
-            act[m] = i < nc;
-        }
+        // wave = one 8 x 8 tile of cam pairs (lane: I = 8 ti + lane / 8, J = 8 tj + lane % 8):
+        // a feature's contiguous cam range [s, e] activates the pairs s <= J <= I <= e,
+        // a triangle that whole tiles cover far better than the row-major block order
+        // (whose 64-block strips are mostly inactive for every feature)
+        const int tt = blockIdx.y * (NT >> 6) * BPT + (tid >> 6) + (NT >> 6) * m;
+        const int TS = (Nmax + 7) >> 3, ntl = TS * (TS + 1) / 2;
+        int ti = (int)((sqrtf(8.0f * (float)tt + 1.0f) - 1.0f) * 0.5f);
+        while (ti * (ti + 1) / 2 > tt) --ti;
+        while ((ti + 1) * (ti + 2) / 2 <= tt) ++ti;
+        const int tj = tt - ti * (ti + 1) / 2;
+        I[m] = 8 * ti + (lane >> 3);
+        J[m] = 8 * tj + (lane & 7);
+        act[m] = tt < ntl && I[m] < nc && J[m] <= I[m];
 #pragma unroll
         for (int x = 0; x < 6; ++x) {
             bv[m][x] = 0;
@@ -1849,14 +1822,12 @@ __global__ void __launch_bounds__(NT) k_info(DevState<T> st, FeatBatch<T> fb, Up
             for (int y = 0; y < 6; ++y) a[m][x][y] = 0;
         }
     }
-    for (int i = tid; i < Cmax; i += NT) chosen[i] = 0;
-
     // ---- assembly ----
     // Batches of FB features; wave s < FB stages feature f0 + s of the next
     // batch while all waves accumulate the current one: a contiguous copy of
     // its M records (global_load_lds, 16 B per lane), a cam -> record table
     // and a cam bitmask.
-    const int fbeg = fb.feat_off[b], fend = (phases & 1) ? fb.feat_off[b + 1] : fbeg;
+    const int fbeg = fb.feat_off[b], fend = fb.feat_off[b + 1];
     auto stage = [&](int f0, int buf) {
         for (int s = wave; s < INFO_FB; s += nwave) {
             const int f = f0 + s;
@@ -1938,310 +1909,21 @@ __global__ void __launch_bounds__(NT) k_info(DevState<T> st, FeatBatch<T> fb, Up
 
     KT* F = ws.Hthin + (size_t)b * Cmax * (Cmax + 1);
     const int ldf = Cmax + 1;
-    if (assemble_only) {   // [A | b] for the Cholesky-form Kalman stage (msckf_kalman.hip)
 #pragma unroll
-        for (int m = 0; m < BPT; ++m) {
-            if (!act[m]) continue;
+    for (int m = 0; m < BPT; ++m) {
+        if (!act[m]) continue;
 #pragma unroll
-            for (int x = 0; x < 6; ++x)
+        for (int x = 0; x < 6; ++x)
 #pragma unroll
-                for (int y = 0; y < 6; ++y) {
-                    F[(size_t)(6 * I[m] + x) * ldf + 6 * J[m] + y] = a[m][x][y];
-                    F[(size_t)(6 * J[m] + y) * ldf + 6 * I[m] + x] = a[m][x][y];
-                }
-            if (I[m] == J[m])
-#pragma unroll
-                for (int x = 0; x < 6; ++x) F[(size_t)(6 * I[m] + x) * ldf + Cmax] = bv[m][x];
-        }
-        if (tid == 0 && blockIdx.y == 0) info[1] = C;
-        return;
-    }
-    // ---- augmented outer-product Cholesky with diagonal pivoting ----
-    int k = 0;
-    for (; k < ((phases & 2) ? C : 0); ++k) {
-#pragma unroll
-        for (int m = 0; m < BPT; ++m)
-            if (act[m] && I[m] == J[m])
-#pragma unroll
-                for (int x = 0; x < 6; ++x) dval[6 * I[m] + x] = chosen[6 * I[m] + x] ? -1.0 : a[m][x][x];
-        LDS_BARRIER();
-        if (wave == 0) {
-            double best = -2.0;
-            int bi = 0;
-            for (int i = lane; i < C; i += 64) {
-                const double d = dval[i];
-                if (d > best) { best = d; bi = i; }
+            for (int y = 0; y < 6; ++y) {
+                F[(size_t)(6 * I[m] + x) * ldf + 6 * J[m] + y] = a[m][x][y];
+                F[(size_t)(6 * J[m] + y) * ldf + 6 * I[m] + x] = a[m][x][y];
             }
+        if (I[m] == J[m])
 #pragma unroll
-            for (int w = 32; w >= 1; w >>= 1) {
-                const double ob = __shfl_xor(best, w, 64);
-                const int oi = __shfl_xor(bi, w, 64);
-                if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
-            }
-            if (lane == 0) {
-                if (k == 0) s_d0 = best;
-                const bool stop = !(best > 0.0) || best <= tol_rel * s_d0;
-                s_stop = stop;
-                if (!stop) {
-                    s_p = bi;
-                    s_inv = 1.0 / sqrt(best);
-                    chosen[bi] = 1;
-                }
-            }
-        }
-        LDS_BARRIER();
-        if (s_stop) break;
-        const int p = s_p, P = p / 6, q = p - 6 * P;
-        const double inv = s_inv;
-#pragma unroll
-        for (int m = 0; m < BPT; ++m) {
-            if (!act[m]) continue;
-            if (I[m] == P) {   // row q of block (P, J): A[p][6J + y]
-#pragma unroll
-                for (int y = 0; y < 6; ++y) {
-                    double v = 0;
-#pragma unroll
-                    for (int x = 0; x < 6; ++x) v = x == q ? a[m][x][y] : v;
-                    const int c = 6 * J[m] + y;
-                    fvec[c] = (chosen[c] && c != p) ? 0.0 : v * inv;
-                }
-                if (J[m] == P) {
-                    double v = 0;
-#pragma unroll
-                    for (int x = 0; x < 6; ++x) v = x == q ? bv[m][x] : v;
-                    fvec[Cmax] = v * inv;
-                }
-            } else if (J[m] == P) {   // column q of block (I, P): A[6I + y][p]
-#pragma unroll
-                for (int y = 0; y < 6; ++y) {
-                    double v = 0;
-#pragma unroll
-                    for (int x = 0; x < 6; ++x) v = x == q ? a[m][y][x] : v;
-                    const int c = 6 * I[m] + y;
-                    fvec[c] = chosen[c] ? 0.0 : v * inv;
-                }
-            }
-        }
-        LDS_BARRIER();
-        for (int c = tid; c < C; c += NT) F[(size_t)k * ldf + c] = fvec[c];
-        if (tid == 0) F[(size_t)k * ldf + Cmax] = fvec[Cmax];
-#pragma unroll
-        for (int m = 0; m < BPT; ++m) {
-            if (!act[m]) continue;
-            double u[6], v[6];
-#pragma unroll
-            for (int x = 0; x < 6; ++x) { u[x] = fvec[6 * I[m] + x]; v[x] = fvec[6 * J[m] + x]; }
-#pragma unroll
-            for (int x = 0; x < 6; ++x)
-#pragma unroll
-                for (int y = 0; y < 6; ++y) a[m][x][y] -= u[x] * v[y];
-            if (I[m] == J[m]) {
-                const double rk = fvec[Cmax];
-#pragma unroll
-                for (int x = 0; x < 6; ++x) bv[m][x] -= u[x] * rk;
-            }
-        }
+            for (int x = 0; x < 6; ++x) F[(size_t)(6 * I[m] + x) * ldf + Cmax] = bv[m][x];
     }
-    if (tid == 0) info[1] = k;
-}
-
-// ===========================================================================
-// Kalman update (msckf.py:559-604) on H_thin (n x C, IMU columns zero):
-//   HP = H_thin P[21:D, :]              k_hp      (n x D)
-//   S  = HP[:, 21:] H_thin^T + s2 I     k_s       (n x n)
-//   S = L L^T ; y_r = L^-1 r_thin        k_chol
-//   Y = L^-1 HP                          k_trsm
-//   dx = Y^T y_r                         k_dx      (= K r_thin)
-//   P <- P - Y^T Y                       k_pupdate (= (I - K H) P, symmetric)
-//   state correction                     k_correct
-// The GEMMs are 32x32 LDS-tiled, one tile per workgroup, batched over filters.
-// ===========================================================================
-constexpr int TB = 32;
-
-// C[i][j] (+)= sum_k A(i,k) B(k,j) with accessor lambdas; tile (ti, tj) of a
-// m x nn output, K = kk, 256 threads, 2x2 outputs per thread.
-template <typename T, typename FA, typename FB, typename FC>
-__device__ __forceinline__ void tile_gemm(int m, int nn, int kk, int ti, int tj, FA A, FB Bf, FC Cf) {   // T = accumulation type
-    __shared__ T sa[TB][TB + 1], sb[TB][TB + 1];
-    const int tid = threadIdx.x;
-    const int tx = tid % 16, ty = tid / 16;
-    T acc[2][2] = {{0, 0}, {0, 0}};
-    for (int k0 = 0; k0 < kk; k0 += TB) {
-        for (int e = tid; e < TB * TB; e += blockDim.x) {
-            int r = e / TB, c = e % TB;
-            int gi = ti * TB + r, gk = k0 + c;
-            sa[r][c] = (gi < m && gk < kk) ? A(gi, gk) : T(0);
-            int gk2 = k0 + r, gj = tj * TB + c;
-            sb[r][c] = (gk2 < kk && gj < nn) ? Bf(gk2, gj) : T(0);
-        }
-        __syncthreads();
-#pragma unroll 8
-        for (int q = 0; q < TB; ++q) {
-            T a0 = sa[ty][q], a1 = sa[ty + 16][q];
-            T b0 = sb[q][tx], b1 = sb[q][tx + 16];
-            acc[0][0] += a0 * b0; acc[0][1] += a0 * b1;
-            acc[1][0] += a1 * b0; acc[1][1] += a1 * b1;
-        }
-        __syncthreads();
-    }
-    for (int u = 0; u < 2; ++u)
-        for (int v = 0; v < 2; ++v) {
-            int gi = ti * TB + ty + 16 * u, gj = tj * TB + tx + 16 * v;
-            if (gi < m && gj < nn) Cf(gi, gj, acc[u][v]);
-        }
-}
-
-template <typename T>
-__global__ void __launch_bounds__(256) k_hp(DevState<T> st, UpdWs<T> ws) {
-    const int b = blockIdx.z;
-    const int n = ws.info[4 * b + 1];
-    const int C = 6 * st.ncams[b], D = 21 + C;
-    const int ti = blockIdx.y, tj = blockIdx.x;
-    if (ti * TB >= n || tj * TB >= D) return;
-    const KT* H = ws.Hthin + (size_t)b * ws.Cmax * (ws.Cmax + 1);
-    const T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
-    KT* HP = ws.HP + (size_t)b * ws.Cmax * st.Dmax;
-    const int ldh = ws.Cmax + 1, ld = st.Dmax;
-    tile_gemm<KT>(n, D, C, ti, tj,
-                  [&](int i, int k) { return (KT)H[(size_t)i * ldh + k]; },
-                  [&](int k, int j) { return (KT)P[(size_t)(21 + k) * ld + j]; },
-                  [&](int i, int j, KT v) { HP[(size_t)i * ld + j] = v; });
-}
-
-template <typename T>
-__global__ void __launch_bounds__(256) k_s(DevState<T> st, Params<T> prm, UpdWs<T> ws) {
-    const int b = blockIdx.z;
-    const int n = ws.info[4 * b + 1];
-    const int C = 6 * st.ncams[b];
-    const int ti = blockIdx.y, tj = blockIdx.x;
-    if (ti * TB >= n || tj * TB >= n || tj > ti) return;   // lower triangle of tiles
-    const KT* H = ws.Hthin + (size_t)b * ws.Cmax * (ws.Cmax + 1);
-    const KT* HP = ws.HP + (size_t)b * ws.Cmax * st.Dmax;
-    KT* S = ws.S + (size_t)b * ws.Cmax * ws.Cmax;
-    const int ldh = ws.Cmax + 1, ld = st.Dmax, lds = ws.Cmax;
-    const KT s2 = (KT)prm.sigma2;
-    tile_gemm<KT>(n, n, C, ti, tj,
-                  [&](int i, int k) { return HP[(size_t)i * ld + 21 + k]; },
-                  [&](int k, int j) { return (KT)H[(size_t)j * ldh + k]; },
-                  [&](int i, int j, KT v) { S[(size_t)i * lds + j] = v + (i == j ? s2 : KT(0)); });
-}
-
-// Cholesky of S (lower, in place) + y_r = L^-1 r_thin; one workgroup per filter.
-template <typename T>
-__global__ void __launch_bounds__(256) k_chol(DevState<T> st, UpdWs<T> ws) {
-    const int b = blockIdx.x;
-    const int tid = threadIdx.x;
-    const int n = ws.info[4 * b + 1];
-    if (n == 0) return;
-    KT* S = ws.S + (size_t)b * ws.Cmax * ws.Cmax;
-    const int lds = ws.Cmax;
-    const KT* H = ws.Hthin + (size_t)b * ws.Cmax * (ws.Cmax + 1);
-    const int ldh = ws.Cmax + 1;
-    __shared__ KT s_y[512];
-    __shared__ int s_fail;
-    for (int i = tid; i < n; i += blockDim.x) s_y[i] = H[(size_t)i * ldh + ws.Cmax];
-    if (tid == 0) s_fail = 0;
-    __syncthreads();
-    for (int j = 0; j < n; ++j) {
-        if (tid == 0) {
-            KT d = S[(size_t)j * lds + j];
-            if (!(d > 0)) { s_fail = 1; d = KT(1); }
-            KT l = sqrt(d);
-            S[(size_t)j * lds + j] = l;
-            s_y[j] = s_y[j] / l;
-        }
-        __syncthreads();
-        const KT ljj = S[(size_t)j * lds + j];
-        const KT yj = s_y[j];
-        for (int i = j + 1 + tid; i < n; i += blockDim.x) {
-            KT lij = S[(size_t)i * lds + j] / ljj;
-            S[(size_t)i * lds + j] = lij;
-            s_y[i] -= lij * yj;
-        }
-        __syncthreads();
-        const int m = n - j - 1;
-        for (int e = tid; e < m * m; e += blockDim.x) {
-            int i = j + 1 + e / m, l = j + 1 + e % m;
-            if (l <= i) S[(size_t)i * lds + l] -= S[(size_t)i * lds + j] * S[(size_t)l * lds + j];
-        }
-        __syncthreads();
-    }
-    // y_r = L^-1 r_thin goes to the tail of the dx row (dx itself is D long)
-    KT* yr = ws.dx + (size_t)b * (st.Dmax + ws.Cmax) + st.Dmax;
-    for (int i = tid; i < n; i += blockDim.x) yr[i] = s_y[i];
-    if (tid == 0 && s_fail) ws.info[4 * b + 3] = -1;
-}
-
-// Y = L^-1 HP, one thread per column of HP.  Rows are solved in blocks of 8
-// kept in registers; each block's stores are drained before later blocks
-// re-read them (same-address RAW through global memory).
-template <typename T>
-__global__ void __launch_bounds__(256) k_trsm(DevState<T> st, UpdWs<T> ws) {
-    const int b = blockIdx.y;
-    const int n = ws.info[4 * b + 1];
-    const int D = 21 + 6 * st.ncams[b];
-    const int col = blockIdx.x * blockDim.x + threadIdx.x;
-    if (n == 0 || col >= D) return;
-    const KT* L = ws.S + (size_t)b * ws.Cmax * ws.Cmax;
-    KT* HP = ws.HP + (size_t)b * ws.Cmax * st.Dmax;
-    const int lds = ws.Cmax, ld = st.Dmax;
-    constexpr int RB = 8;
-    for (int i0 = 0; i0 < n; i0 += RB) {
-        KT y[RB];
-#pragma unroll
-        for (int t = 0; t < RB; ++t) y[t] = (i0 + t < n) ? HP[(size_t)(i0 + t) * ld + col] : KT(0);
-        for (int j = 0; j < i0; ++j) {   // earlier blocks (already final in memory)
-            const KT yj = HP[(size_t)j * ld + col];
-#pragma unroll
-            for (int t = 0; t < RB; ++t)
-                if (i0 + t < n) y[t] -= L[(size_t)(i0 + t) * lds + j] * yj;
-        }
-#pragma unroll
-        for (int t = 0; t < RB; ++t) {   // inside the block
-            if (i0 + t < n) {
-#pragma unroll
-                for (int q = 0; q < t; ++q) y[t] -= L[(size_t)(i0 + t) * lds + i0 + q] * y[q];
-                y[t] /= L[(size_t)(i0 + t) * lds + i0 + t];
-                HP[(size_t)(i0 + t) * ld + col] = y[t];
-            }
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-}
-
-// dx = Y^T y_r
-template <typename T>
-__global__ void __launch_bounds__(256) k_dx(DevState<T> st, UpdWs<T> ws) {
-    const int b = blockIdx.x;
-    const int n = ws.info[4 * b + 1];
-    const int D = 21 + 6 * st.ncams[b];
-    if (n == 0) return;
-    const KT* Y = ws.HP + (size_t)b * ws.Cmax * st.Dmax;
-    KT* dx = ws.dx + (size_t)b * (st.Dmax + ws.Cmax);
-    const KT* yr = dx + st.Dmax;
-    for (int col = threadIdx.x; col < D; col += blockDim.x) {
-        KT s = 0;
-        for (int i = 0; i < n; ++i) s += Y[(size_t)i * st.Dmax + col] * yr[i];
-        dx[col] = s;
-    }
-}
-
-// P <- P - Y^T Y (symmetric by construction: entry (i,j) and (j,i) use the
-// same products in the same order)
-template <typename T>
-__global__ void __launch_bounds__(256) k_pupdate(DevState<T> st, UpdWs<T> ws) {
-    const int b = blockIdx.z;
-    const int n = ws.info[4 * b + 1];
-    const int D = 21 + 6 * st.ncams[b];
-    const int ti = blockIdx.y, tj = blockIdx.x;
-    if (n == 0 || ti * TB >= D || tj * TB >= D) return;
-    const KT* Y = ws.HP + (size_t)b * ws.Cmax * st.Dmax;
-    T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
-    const int ld = st.Dmax;
-    tile_gemm<KT>(D, D, n, ti, tj,
-                  [&](int i, int k) { return Y[(size_t)k * ld + i]; },
-                  [&](int k, int j) { return Y[(size_t)k * ld + j]; },
-                  [&](int i, int j, KT v) { P[(size_t)i * ld + j] = (T)((KT)P[(size_t)i * ld + j] - v); });
+    if (tid == 0 && blockIdx.y == 0) info[1] = C;
 }
 
 // State correction (msckf.py:566-595).
@@ -2371,7 +2053,7 @@ size_t gate_lds_bytes(int maxM) {
 
 template <typename T, int TPL, bool MP>
 static void launch_gate_wave_cfg(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const FeatBatch<T>& fb,
-                                 const int* list, int cnt, int Mmax, int capb, int wpb, size_t lds, int phases) {
+                                 const int* list, int cnt, int Mmax, int capb, int wpb, size_t lds) {
     static size_t attr = 64 * 1024;
     if (lds > attr) {
         (void)hipFuncSetAttribute((const void*)k_gate_wave<T, TPL, MP>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2379,7 +2061,7 @@ static void launch_gate_wave_cfg(hipStream_t s, const DevState<T>& st, const Par
         attr = lds;
     }
     hipLaunchKernelGGL((k_gate_wave<T, TPL, MP>), dim3((cnt + wpb - 1) / wpb), dim3(64 * wpb), lds, s, st, prm, fb,
-                       list, cnt, Mmax, capb, phases);
+                       list, cnt, Mmax, capb);
 }
 
 template <typename T, int TPL>
@@ -2403,33 +2085,18 @@ static void launch_gate_wave(hipStream_t s, const DevState<T>& st, const Params<
     const size_t per_wave = per_wave_of(capb);
     const int wpb = 4 * per_wave <= 160 * 1024 ? 4 : (2 * per_wave <= 160 * 1024 ? 2 : 1);
     const size_t lds = wpb * per_wave;
-    static int phases = -1;   // MSCKF_GATE_PHASES: profiling aid (bit0 Y tiles, bit2 elimination)
-    if (phases < 0) {
-        const char* e = getenv("MSCKF_GATE_PHASES");
-        phases = e ? atoi(e) : 7;
-    }
-    if (capb < nbk) launch_gate_wave_cfg<T, TPL, true>(s, st, prm, fb, list, cnt, Mmax, capb, wpb, lds, phases);
-    else launch_gate_wave_cfg<T, TPL, false>(s, st, prm, fb, list, cnt, Mmax, capb, wpb, lds, phases);
+    if (capb < nbk) launch_gate_wave_cfg<T, TPL, true>(s, st, prm, fb, list, cnt, Mmax, capb, wpb, lds);
+    else launch_gate_wave_cfg<T, TPL, false>(s, st, prm, fb, list, cnt, Mmax, capb, wpb, lds);
 }
 
 // Features are launched in size classes (by M, listed on the host at load
 // time): the register-tile wave kernel sized for the class, or for the
 // largest features the workgroup LDS kernel (global-memory kernel if even
 // that does not fit).
-static int gate_mode() {   // MSCKF_GATE=lds forces the workgroup kernel for every class, =wave the
-    static int mode = -1;     // 4x4 register-tile wave kernel for fp32 too (A/B runs)
-    if (mode < 0) {
-        const char* e = getenv("MSCKF_GATE");
-        mode = (e && e[0] == 'l') ? 1 : ((e && e[0] == 'w') ? 2 : 0);
-    }
-    return mode;
-}
 
-// The workgroup gating kernels and the QR merge read the compact factors
-// (V, W, Q^T r, tau) that k_feature otherwise skips.
-bool feature_needs_compact(int maxM, int Cmax) {
-    return gate_mode() == 1 || maxM > GateClasses::LIM[GateClasses::NC - 2] || update_mode(Cmax) == UPD_QR;   // (also Hx, r)
-}
+// The workgroup gating kernels (M > 82) read the compact factors (V, W,
+// Q^T r, tau, Hx, r) that k_feature otherwise skips.
+bool feature_needs_compact(int maxM) { return maxM > GateClasses::LIM[GateClasses::NC - 2]; }
 
 template <typename T>
 void launch_gate(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const FeatBatch<T>& fb,
@@ -2440,23 +2107,22 @@ void launch_gate(hipStream_t s, const DevState<T>& st, const Params<T>& prm, con
         (void)hipFuncSetAttribute((const void*)k_gate_lds<T>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_set = true;
     }
-    const int mode = gate_mode();
     for (int c = 0; c < GateClasses::NC; ++c) {
         const int cnt = gc.off[c + 1] - gc.off[c];
         if (cnt == 0) continue;
         const int maxM = gc.maxM[c];
         const int* list = gc.list + gc.off[c];
         if constexpr (sizeof(T) == 4) {   // fp32: MFMA tiles (msckf_gate_mfma.hip)
-            if (mode == 0 && c < GateClasses::NC - 2 && gate_mfma_fits(maxM)) {
+            if (c < GateClasses::NC - 2 && gate_mfma_fits(maxM)) {
                 launch_gate_mfma(s, st, prm, fb, list, cnt, maxM);
                 continue;
             }
-            if (mode == 0 && c == GateClasses::NC - 2 && gate_mfma_wg_fits(maxM)) {
+            if (c == GateClasses::NC - 2 && gate_mfma_wg_fits(maxM)) {
                 launch_gate_mfma_wg(s, st, prm, fb, list, cnt, maxM);
                 continue;
             }
         }
-        if (mode != 1 && c == GateClasses::NC - 2) {   // 40 < M <= 82: register tiles, one workgroup per feature
+        if (c == GateClasses::NC - 2) {   // 40 < M <= 82: register tiles, one workgroup per feature
             const int nrow = gate_nt(maxM), tiles = nrow * (nrow + 1) / 2;
             const size_t lds = gate_big_lds_bytes(maxM);
             if (tiles <= 256 * 4) {
@@ -2470,7 +2136,7 @@ void launch_gate(hipStream_t s, const DevState<T>& st, const Params<T>& prm, con
             }
             continue;
         }
-        if (mode != 1 && c < GateClasses::NC - 2) {
+        if (c < GateClasses::NC - 2) {
             switch (GateClasses::TPL[c]) {
                 case 1: launch_gate_wave<T, 1>(s, st, prm, fb, list, cnt, maxM); break;
                 case 2: launch_gate_wave<T, 2>(s, st, prm, fb, list, cnt, maxM); break;
@@ -2498,130 +2164,38 @@ void launch_select(hipStream_t s, const DevState<T>& st, const FeatBatch<T>& fb,
     hipLaunchKernelGGL(k_select<T>, dim3((st.B + 3) / 4), dim3(256), 0, s, st, fb, ws, row_cap);
 }
 
-// Numerical-rank threshold of the pivoted Cholesky, relative to max diag(A).
-constexpr double INFO_TOL_REL = 1e-11;
-
-// MSCKF_INFO_TILED=0: the row-major cam-pair order in k_info (A/B runs).  The
-// pivoted-Cholesky variant needs every block in one workgroup: row-major there.
-static bool info_tiled(int Cmax) {
-    static int en = -1;
-    if (en < 0) {
-        const char* e = getenv("MSCKF_INFO_TILED");
-        en = e ? atoi(e) : 1;
-    }
-    return en != 0 && update_mode(Cmax) == UPD_CHOL;
-}
-
-template <typename T, int BPT, int NT>
+template <typename T, int NT>
 static void launch_info_cfg(hipStream_t s, const DevState<T>& st, const FeatBatch<T>& fb, const UpdWs<T>& ws) {
-    int fbn = info_fb(st.Nmax);
-    {   // MSCKF_INFO_FB: features staged per batch (as many as the double-buffered slots fit in LDS)
-        static int want = -1;
-        if (want < 0) {
-            const char* e = getenv("MSCKF_INFO_FB");
-            want = e ? atoi(e) : 0;
-        }
-        const size_t per = ((size_t)2 * info_slot_doubles(st.Nmax)) * sizeof(double) + 4 * sizeof(unsigned long long) +
-                           2 * st.Nmax * sizeof(int);
-        const size_t fixed = (2 * (size_t)ws.Cmax + 1) * sizeof(double) + (size_t)ws.Cmax * sizeof(int);
-        if (want > 0) fbn = want;
-        while (fbn > 1 && fixed + fbn * per > 160 * 1024) --fbn;
-    }
-    const size_t lds = ((size_t)2 * fbn * info_slot_doubles(st.Nmax) + 2 * (size_t)ws.Cmax + 1) * sizeof(double) +
-                       4 * fbn * sizeof(unsigned long long) + ((size_t)ws.Cmax + 2 * fbn * st.Nmax) * sizeof(int);
+    // features staged per batch: INFO_FB_MAX, or as many as the double-buffered slots fit in LDS
+    const size_t per = ((size_t)2 * info_slot_doubles(st.Nmax)) * sizeof(double) + 4 * sizeof(unsigned long long) +
+                       2 * st.Nmax * sizeof(int);
+    int fbn = INFO_FB_MAX;
+    while (fbn > 1 && fbn * per > 160 * 1024) --fbn;
+    const size_t lds = fbn * per;
     const int TS = (st.Nmax + 7) / 8, ntl = TS * (TS + 1) / 2;
-    const int tiled = info_tiled(ws.Cmax) ? 1 : 0;
-    const int nblk = st.Nmax * (st.Nmax + 1) / 2;
-    const int parts = tiled ? (ntl + (NT / 64) * BPT - 1) / ((NT / 64) * BPT) : (nblk + NT * BPT - 1) / (NT * BPT);
+    const int parts = (ntl + (NT / 64) - 1) / (NT / 64);
     static size_t attr = 64 * 1024;   // dynamic LDS granted so far (default 64 KB)
     if (lds > attr) {
-        (void)hipFuncSetAttribute((const void*)k_info<T, BPT, NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)lds);
+        (void)hipFuncSetAttribute((const void*)k_info<T, 1, NT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         attr = lds;
     }
-    static int phases = -1;   // MSCKF_INFO_PHASES: profiling aid (bit0 assembly, bit1 factorisation)
-    if (phases < 0) {
-        const char* e = getenv("MSCKF_INFO_PHASES");
-        phases = e ? atoi(e) : 3;
-    }
-    // the pivoted Cholesky needs every block in one workgroup: update_mode() only
-    // selects it when parts == 1
-    hipLaunchKernelGGL((k_info<T, BPT, NT>), dim3(st.B, parts), dim3(NT), lds, s, st, fb, ws, INFO_TOL_REL, phases,
-                       update_mode(ws.Cmax) == UPD_CHOL ? 1 : 0, tiled, fbn);
-}
-
-// Update path (MSCKF_UPDATE env, for A/B runs):
-//   chol  (default) k_info assembles [A | b]; Cholesky-form Kalman stage
-//         (msckf_kalman.hip) -- when the cam capacity fits its register tiles
-//   pchol k_info assembles A and factors it by pivoted Cholesky into H_thin;
-//         Kalman stage on H_thin (k_hp ... k_pupdate)
-//   qr    round-1 QR row-merge into H_thin (msckf_qr_merge.hip); same Kalman
-int update_mode(int Cmax) {
-    static int mode = -1;
-    if (mode < 0) {
-        const char* e = getenv("MSCKF_UPDATE");
-        mode = UPD_CHOL;
-        if (e && e[0] == 'q') mode = UPD_QR;
-        if (e && e[0] == 'p') mode = UPD_PCHOL;
-    }
-    const int N = Cmax / 6;
-    if (mode == UPD_PCHOL && N * (N + 1) / 2 > 1024) return UPD_CHOL;   // k_info's pivoted Cholesky: one workgroup
-    return mode;
+    hipLaunchKernelGGL((k_info<T, 1, NT>), dim3(st.B, parts), dim3(NT), lds, s, st, fb, ws, fbn);
 }
 
 template <typename T>
 void launch_compress(hipStream_t s, const DevState<T>& st, const FeatBatch<T>& fb, const UpdWs<T>& ws) {
-    if (update_mode(ws.Cmax) == UPD_QR) {
-        launch_compress_qr<T>(s, st, fb, ws);
-        return;
-    }
-    if (update_mode(ws.Cmax) == UPD_CHOL && info_mfma_enabled(st.Nmax)) {
-        launch_info_mfma<T>(s, st, fb, ws);
-        return;
-    }
-    if (info_tiled(ws.Cmax)) {   // one wave per 8 x 8 tile of cam pairs
-        const int TS = (st.Nmax + 7) / 8, ntl = TS * (TS + 1) / 2;
-        if (ntl <= 4) launch_info_cfg<T, 1, 256>(s, st, fb, ws);
-        else if (ntl <= 8) launch_info_cfg<T, 1, 512>(s, st, fb, ws);
-        else if (ntl <= 10) launch_info_cfg<T, 1, 640>(s, st, fb, ws);
-        else launch_info_cfg<T, 1, 1024>(s, st, fb, ws);   // > 10 tiles: several workgroups per filter
-        return;
-    }
-    const int nblk = st.Nmax * (st.Nmax + 1) / 2;   // 6x6 cam-pair blocks of A (lower triangle)
-    if (nblk <= 256) launch_info_cfg<T, 1, 256>(s, st, fb, ws);
-    else if (nblk <= 512) launch_info_cfg<T, 1, 512>(s, st, fb, ws);
-    else launch_info_cfg<T, 1, 1024>(s, st, fb, ws);   // Nmax > 44: several workgroups per filter (assembly only)
+    // one wave per 8 x 8 tile of cam pairs
+    const int TS = (st.Nmax + 7) / 8, ntl = TS * (TS + 1) / 2;
+    if (ntl <= 4) launch_info_cfg<T, 256>(s, st, fb, ws);
+    else if (ntl <= 8) launch_info_cfg<T, 512>(s, st, fb, ws);
+    else if (ntl <= 10) launch_info_cfg<T, 640>(s, st, fb, ws);
+    else launch_info_cfg<T, 1024>(s, st, fb, ws);   // > 10 tiles: several workgroups per filter
 }
 
 template <typename T>
 void launch_kalman(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const UpdWs<T>& ws,
-                   KernelTimer* kt, bool a_done) {
-    if (update_mode(ws.Cmax) == UPD_CHOL) {
-        launch_kalman_chol<T>(s, st, prm, ws, kt, a_done);
-        kt->begin(s, "kalman_correct");
-        hipLaunchKernelGGL(k_correct<T>, dim3(st.B), dim3(64), 0, s, st, ws);
-        kt->end(s);
-        return;
-    }
-    const int tc = (ws.Cmax + TB - 1) / TB, td = (st.Dmax + TB - 1) / TB;
-    kt->begin(s, "kalman_hp");
-    hipLaunchKernelGGL(k_hp<T>, dim3(td, tc, st.B), dim3(256), 0, s, st, ws);
-    kt->end(s);
-    kt->begin(s, "kalman_s");
-    hipLaunchKernelGGL(k_s<T>, dim3(tc, tc, st.B), dim3(256), 0, s, st, prm, ws);
-    kt->end(s);
-    kt->begin(s, "kalman_chol");
-    hipLaunchKernelGGL(k_chol<T>, dim3(st.B), dim3(256), 0, s, st, ws);
-    kt->end(s);
-    kt->begin(s, "kalman_trsm");
-    hipLaunchKernelGGL(k_trsm<T>, dim3((st.Dmax + 255) / 256, st.B), dim3(256), 0, s, st, ws);
-    kt->end(s);
-    kt->begin(s, "kalman_dx");
-    hipLaunchKernelGGL(k_dx<T>, dim3(st.B), dim3(256), 0, s, st, ws);
-    kt->end(s);
-    kt->begin(s, "kalman_pupdate");
-    hipLaunchKernelGGL(k_pupdate<T>, dim3(td, td, st.B), dim3(256), 0, s, st, ws);
-    kt->end(s);
+                   KernelTimer* kt) {
+    launch_kalman_chol<T>(s, st, prm, ws, kt);
     kt->begin(s, "kalman_correct");
     hipLaunchKernelGGL(k_correct<T>, dim3(st.B), dim3(64), 0, s, st, ws);
     kt->end(s);
@@ -2640,7 +2214,7 @@ void launch_kalman(hipStream_t s, const DevState<T>& st, const Params<T>& prm, c
     template void launch_gate<T>(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&, const GateClasses&); \
     template void launch_select<T>(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const UpdWs<T>&, int); \
     template void launch_compress<T>(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const UpdWs<T>&); \
-    template void launch_kalman<T>(hipStream_t, const DevState<T>&, const Params<T>&, const UpdWs<T>&, KernelTimer*, bool);
+    template void launch_kalman<T>(hipStream_t, const DevState<T>&, const Params<T>&, const UpdWs<T>&, KernelTimer*);
 INSTANTIATE(float)
 INSTANTIATE(double)
 

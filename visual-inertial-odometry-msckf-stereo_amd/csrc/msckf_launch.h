@@ -115,26 +115,13 @@ template <typename T>
 void launch_select(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const UpdWs<T>&, int row_cap);
 template <typename T>
 void launch_compress(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const UpdWs<T>&);
-// [A | b] assembly on fp64 MFMA tiles (msckf_info_mfma.hip), Cholesky-form update path
-bool info_mfma_enabled(int Nmax);
-template <typename T>
-void launch_info_mfma(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const UpdWs<T>&);
-template <typename T>
-void launch_compress_qr(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const UpdWs<T>&);
-enum UpdateMode { UPD_CHOL = 0, UPD_PCHOL = 1, UPD_QR = 2 };
-int update_mode(int Cmax);
-bool feature_needs_compact(int maxM, int Cmax);
+// The workgroup gating kernels (M > 82) need k_feature's compact QR factors
+bool feature_needs_compact(int maxM);
 bool kalman_chol_supported(int Cmax);
 size_t kalman_global_ws_doubles(int Cmax);
 template <typename T>
-void launch_kalman_chol(hipStream_t, const DevState<T>&, const Params<T>&, const UpdWs<T>&, KernelTimer*,
-                        bool a_done = false);
+void launch_kalman_chol(hipStream_t, const DevState<T>&, const Params<T>&, const UpdWs<T>&, KernelTimer*);
 template <typename T>
-void launch_kalman(hipStream_t, const DevState<T>&, const Params<T>&, const UpdWs<T>&, KernelTimer*,
-                   bool a_done = false);
-// Kalman stage A ahead of the feature kernels on a side stream (msckf_kalman.hip)
-bool kalman_a_early(int Cmax);
-template <typename T>
-void launch_kalman_a_early(hipStream_t, const DevState<T>&, const UpdWs<T>&);
+void launch_kalman(hipStream_t, const DevState<T>&, const Params<T>&, const UpdWs<T>&, KernelTimer*);
 
 }  // namespace msckf

@@ -51,6 +51,22 @@ class Feature:
         self.is_initialized = False
 
 
+def check_motion(observations, cams, threshold):
+    """Feature.check_motion (feature.py:124-165): is the translation between the
+    first and the last observing cam, orthogonal to the first observation's
+    ray, above ``threshold``?  ``cams``: cam id -> dict(q, p).  A negative
+    threshold (the EuRoC config, config.py:10) accepts every feature."""
+    if threshold < 0:
+        return True
+    ids = list(observations.keys())
+    c0, c1 = cams[ids[0]], cams[ids[-1]]
+    d = np.array([*observations[ids[0]][:2], 1.0])
+    d = to_rotation(np.asarray(c0["q"], float)).T @ (d / np.linalg.norm(d))
+    tr = np.asarray(c1["p"], float) - np.asarray(c0["p"], float)
+    orth = tr - (tr @ d) * d
+    return bool(np.linalg.norm(orth) > threshold)
+
+
 class MSCKF:
     ROW_CAP = 1500   # msckf.py:678
 
@@ -77,6 +93,7 @@ class MSCKF:
         self.is_first_img = True
         self.gate_log = []                 # (frame, dof, rows, accepted) like tools/gen_golden.py
         self.shape_log = []
+        self.reset_log = []                # frames after which online_reset fired
         self._n_published = 0
         T_cam0_imu = np.linalg.inv(config.T_imu_cam0)
         self._T_imu_body = Isometry3d(config.T_imu_body[:3, :3], config.T_imu_body[:3, 3])
@@ -301,12 +318,16 @@ class MSCKF:
                 invalid.append(feat.id)
                 continue
             candidates.append(feat)
-        # check_motion is always True with the EuRoC config (translation
-        # threshold -1, config.py:10); triangulations are independent of each
-        # other, so they are batched into one launch.
-        if self.config.optimization.translation_threshold >= 0:
-            raise NotImplementedError("check_motion with a positive translation threshold")
-        yield from self._triangulate([f for f in candidates if not f.is_initialized])
+        # check_motion (always True with the EuRoC config's threshold -1,
+        # config.py:10) needs the cam poses; the triangulations are independent
+        # of each other, so they are batched into one launch.
+        thr = self.config.optimization.translation_threshold
+        to_init = [f for f in candidates if not f.is_initialized]
+        if thr >= 0 and to_init:
+            _, cams_arr = yield ("states",)
+            cams = self._cam_dict(cams_arr)
+            to_init = [f for f in to_init if check_motion(f.observations, cams, thr)]
+        yield from self._triangulate(to_init)
         processed = []
         for feat in candidates:
             if not feat.is_initialized:
@@ -352,6 +373,8 @@ class MSCKF:
             return
         _, cams_arr = yield ("states",)
         rm = self._find_redundant_cam_states(cams_arr)
+        thr = self.config.optimization.translation_threshold
+        cams = self._cam_dict(cams_arr)
         to_init = []
         for feat in self.map_server.values():
             inv = [c for c in rm if c in feat.observations]
@@ -362,7 +385,9 @@ class MSCKF:
                 continue
             if not feat.is_initialized:
                 to_init.append(feat)
-        yield from self._triangulate(to_init)
+        # features that fail check_motion stay uninitialized: their involved
+        # observations are dropped below like those of a failed triangulation
+        yield from self._triangulate([f for f in to_init if check_motion(f.observations, cams, thr)])
         for feat in to_init:
             if not feat.is_initialized:
                 for c in rm:
@@ -411,6 +436,7 @@ class MSCKF:
             return
         self.cam_ids.clear()
         self.map_server.clear()
+        self.reset_log.append(self._n_published - 1)   # the frame just published
         imu, _ = yield ("states",)
         yield ("set_state", imu, None, self._initial_cov())
 
