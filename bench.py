@@ -1,22 +1,33 @@
-"""Throughput bench: EKF measurement updates/s at 30 cam-states x 200 features.
+"""Throughput bench: EKF measurement updates/s at N cam-states x F features
+(default 30 x 200, BASELINE.json's metric).
 
 One "step" = one batched EKF measurement update of B independent filters
 (SURVEY.md 8(d) unit of work): triangulation of every feature, per-feature
 Jacobian + nullspace projection + chi2 gating, stacking (no row cap), the
 compression of the stacked rows (information assembly) and the
-Kalman / covariance update -- on inputs already resident in HBM.  Each step first restores the filters' pristine state on the device (a
-D2D copy that is counted inside the timed region) so every step does
-identical work.
+Kalman / covariance update -- on inputs already resident in HBM.  Each step
+first restores the filters' pristine state on the device (a D2D copy that is
+counted inside the timed region) so every step does identical work.
 
   python bench.py [--gpus N --steps K --warmup W --batch B --N 30 --F 200 --dtype fp32]
 
-For N > 1 it runs under torch.distributed.run, one rank per GPU; ranks are
-independent replicas (the filter does not shard); RCCL is only
-used for the start/stop barriers and the max-over-ranks of the timing.
+The JSON line carries the headline (fp32 context, BASELINE config 2) and,
+unless --no-fp64, the same workload in the fp64 context (the precision the
+north-star's 1e-6 tolerance is stated at) as ``fp64``; ``accuracy`` compares
+the GPU's updated filters with the CPU oracle's (computed in the
+cpu_baseline leg, as the checker).
+
+--gpus N > 1: N ranks, one process per GPU -- spawned by this script (its
+parent process never touches the GPU) or by an external launcher
+(torch.distributed.run sets WORLD_SIZE).  Ranks are independent replicas
+(the filter does not shard): disjoint problem seeds, no data
+exchange; a host TCP hub (msckf_amd.replicas) carries only the start/stop
+barriers and the max-over-ranks of the elapsed time.
 """
 import argparse
 import json
 import os
+import platform
 import sys
 import time
 
@@ -26,12 +37,12 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 import msckf_pkg  # noqa: E402,F401
 from msckf_amd import synth, replicas, FilterConfig, CHI2_05  # noqa: E402
-from msckf_amd._lib import Context, pack_imu, pack_cams  # noqa: E402
 
-METRIC = "EKF measurement updates/sec at 30 cam-states x 200 features; ATE RMSE vs ref"
+BASE_METRIC = "EKF measurement updates/sec at 30 cam-states x 200 features; ATE RMSE vs ref"
 HBM_PEAK_GBS = 8000.0
 FP32_PEAK_TFLOPS = 157.3      # MI355X dense FP32 (vector = MFMA f32 rate), MI355X_MICROARCH.md
 FP64_PEAK_TFLOPS = 78.6
+N_CHECK = 4                   # distinct problems the accuracy block compares with the oracle
 
 
 def parse():
@@ -46,17 +57,29 @@ def parse():
     ap.add_argument("--unique", type=int, default=32, help="distinct synthetic problems tiled over the batch")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-fp64", action="store_true", help="skip the fp64-context leg")
     ap.add_argument("--no-ate", action="store_true", help="skip the ATE replay leg")
     ap.add_argument("--no-prop", action="store_true", help="skip the IMU-propagation leg")
+    ap.add_argument("--stub", action="store_true",
+                    help="TESTS ONLY: a CPU stand-in for the device context (exercises the multi-rank launch, "
+                         "barriers and max-over-ranks without a GPU; the line it prints is not a measurement)")
     return ap.parse_args()
 
 
-def build_batch(args, rank, local_rank):
-    probs = [synth.make_update_problem(args.N, args.F, seed=sd)
-             for sd in replicas.problem_seeds(rank, min(args.unique, args.batch))]
+def metric_name(args):
+    if (args.N, args.F) == (30, 200):
+        return BASE_METRIC
+    return "EKF measurement updates/sec at %d cam-states x %d features" % (args.N, args.F)
+
+
+def make_problems(args, rank, unique):
+    return [synth.make_update_problem(args.N, args.F, seed=sd) for sd in replicas.problem_seeds(rank, unique)]
+
+
+def build_batch(args, probs, dtype, device):
+    from msckf_amd._lib import Context, pack_imu, pack_cams
     B = args.batch
-    dtype = np.float32 if args.dtype == "fp32" else np.float64
-    ctx = Context(FilterConfig(), n_filters=B, n_cam_capacity=args.N, dtype=dtype, device=local_rank)
+    ctx = Context(FilterConfig(), n_filters=B, n_cam_capacity=args.N, dtype=dtype, device=device)
     feat_off, obs_off, cams, zs, chi = [0], [0], [], [], []
     for b in range(B):
         p = probs[b % len(probs)]
@@ -73,7 +96,7 @@ def build_batch(args, rank, local_rank):
     ctx.batch_load(np.array(feat_off), np.array(obs_off), np.concatenate(cams), np.concatenate(zs),
                    None, np.array(chi))
     ctx.snapshot()
-    return ctx, probs
+    return ctx, np.array(feat_off)
 
 
 def flops_model(probs, B, accepted, valid, feat_off):
@@ -118,7 +141,8 @@ def flops_model(probs, B, accepted, valid, feat_off):
 def pmc_traffic(stage, dtype, workload):
     """HBM bytes per step of a stage's kernels from the committed rocprofv3 PMC
     summary (tools/pmc_summary.py; FETCH_SIZE and WRITE_SIZE from separate
-    passes), or None if no summary covers them."""
+    passes, FETCH_SIZE doubled as MI355X_MICROARCH.md prescribes for gfx950),
+    or None if no summary covers them."""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     if not os.path.exists(path):
         return None
@@ -126,13 +150,15 @@ def pmc_traffic(stage, dtype, workload):
         summ = json.load(fh)
     if summ.get("dtype") != dtype or summ.get("workload", "N30xF200xB2048") != workload:
         return None
-    return summ.get("stages", {}).get(stage, {}).get("bytes_per_step")
+    return summ.get("stages", {}).get(stage, {}).get("fetch_x2_bytes_per_step")
 
 
+# ------------------------------------------------------------ cpu_baseline --
 def _oracle_worker(payload):
-    """One CPU worker of the all-cores baseline: oracle updates on 1 BLAS
-    thread for about ``seconds``; returns (updates, elapsed)."""
-    probs, seconds, tests_dir = payload
+    """One CPU worker of the baseline: oracle updates on 1 BLAS thread for
+    about ``seconds``; returns (updates, elapsed, outputs of the first
+    ``keep`` distinct problems)."""
+    probs, seconds, tests_dir, keep = payload
     sys.path.insert(0, tests_dir)
     from helpers import problem_to_dict, oracle_update
     try:
@@ -141,23 +167,37 @@ def _oracle_worker(payload):
     except Exception:
         pass
     oracle_update(problem_to_dict(probs[0]))          # warm-up
-    done, t0 = 0, time.perf_counter()
+    done, outs, t0 = 0, [], time.perf_counter()
     while True:
-        oracle_update(problem_to_dict(probs[done % len(probs)]))
+        st, acc, _, _, _ = oracle_update(problem_to_dict(probs[done % len(probs)]))
+        if done < keep:
+            outs.append((st, acc))
         done += 1
         el = time.perf_counter() - t0
-        if el > seconds:
-            return done, el
+        if el > seconds and done >= keep:
+            return done, el, outs
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
 
 
 def cpu_baseline(args, probs):
     """Oracle (numpy restatement of the reference) on a bounded sample of the
     same workload: 1 BLAS thread in this process, and -- SURVEY.md 8(d) asks
     for both -- one single-threaded worker per host core of this job's CPU
-    share (forked before this process touches the GPU)."""
+    share (forked before this process touches the GPU).  The first N_CHECK
+    distinct problems' oracle outputs are kept for the accuracy block."""
     tests_dir = os.path.join(ROOT, "tests")
-    done, el = _oracle_worker((probs, args.cpu_seconds, tests_dir))
-    out = {"value": done / el, "unit": "updates/s", "cores": 1, "kind": "port",
+    done, el, outs = _oracle_worker((probs, args.cpu_seconds, tests_dir, min(N_CHECK, len(probs))))
+    out = {"value": done / el, "unit": "updates/s", "cores": 1, "kind": "port", "cpu": cpu_model(),
            "sample": "%d synthetic %dx%d updates (triangulation + jacobian + gating + QR + Kalman as in the reference), "
                      "numpy/OpenBLAS 1 thread, oracle/msckf_oracle.py" % (done, args.N, args.F)}
     try:
@@ -169,10 +209,118 @@ def cpu_baseline(args, probs):
         import multiprocessing as mp
         with mp.get_context("fork").Pool(workers) as pool:
             res = pool.map(_oracle_worker, [(probs[w % len(probs):] + probs[:w % len(probs)],
-                                             args.cpu_seconds / 2, tests_dir) for w in range(workers)])
-        out["all_cores"] = {"value": sum(d for d, _ in res) / max(e for _, e in res), "unit": "updates/s",
+                                             args.cpu_seconds / 2, tests_dir, 0) for w in range(workers)])
+        out["all_cores"] = {"value": sum(r[0] for r in res) / max(r[1] for r in res), "unit": "updates/s",
                             "cores": workers, "sample": "%d updates over %d single-threaded worker processes"
-                                                        % (sum(d for d, _ in res), workers)}
+                                                        % (sum(r[0] for r in res), workers)}
+    return out, outs
+
+
+def _state_vector(imu, cams):
+    return np.concatenate([imu["q"], imu["p"], imu["v"], imu["bg"], imu["ba"],
+                           np.asarray(cams)[:, 0:7].ravel()])
+
+
+def accuracy(ctx, refs, acc, feat_off):
+    """Checker: the GPU's updated filters 0..len(refs)-1 against the oracle's
+    outputs for the same problems (from the cpu_baseline leg): chi2 decision
+    agreement, relative deviation of the state vector (IMU q, p, v, bg, ba and
+    every cam's q, p) and of the covariance (Frobenius), the north-star
+    quantities (<= 1e-6 relative)."""
+    from msckf_amd._lib import unpack_imu
+    agree, sdev, pdev = [], [], []
+    for b, (st, acc_o) in enumerate(refs):
+        sl = slice(feat_off[b], feat_off[b + 1])
+        agree.append(float(np.mean(acc[sl].astype(bool) == acc_o)))
+        imu, cams, P = ctx.get_state(b)
+        x = _state_vector(unpack_imu(imu), cams)
+        xo = np.concatenate([st.imu.q, st.imu.p, st.imu.v, st.imu.bg, st.imu.ba] +
+                            [np.concatenate([c.q, c.p]) for c in st.cams.values()])
+        sdev.append(float(np.linalg.norm(x - xo) / np.linalg.norm(xo)))
+        pdev.append(float(np.linalg.norm(P - st.P) / np.linalg.norm(st.P)))
+    return {"filters_checked": len(refs), "decision_agreement": min(agree),
+            "state_rel_dev_max": max(sdev), "cov_frobenius_rel_dev_max": max(pdev),
+            "within_1e-6": bool(max(sdev) <= 1e-6 and max(pdev) <= 1e-6),
+            "reference": "oracle/msckf_oracle.py (fp64 numpy restatement of the reference, pinned to its fixtures) "
+                         "on the same problems, its own triangulation and decisions"}
+
+
+# ------------------------------------------------------------------- legs --
+def timed_update(ctx, args, grp):
+    """Warm-up, then exactly args.steps steps between barriers, the device
+    synchronised on both sides; returns (max-over-ranks seconds, kernel times)."""
+    for _ in range(args.warmup):
+        ctx.restore()
+        ctx.batch_update(row_cap=0, triangulate=True)
+    ctx.sync()
+    ctx.set_profiling(True)
+    grp.barrier()
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ctx.restore()
+        ctx.batch_update(row_cap=0, triangulate=True)
+    ctx.sync()
+    grp.barrier()
+    el = time.perf_counter() - t0
+    times = ctx.kernel_times()
+    ctx.set_profiling(False)
+    return grp.max_over_ranks(el), times
+
+
+def roofline_of(times, fl, args, dtype):
+    """Dominant stage by device time (HIP events on the launch stream, timed
+    region only) against the peak of its arithmetic type."""
+    kern = {k: v for k, v in times.items() if k != "restore"}
+    dom = max(kern, key=lambda k: kern[k][0])
+    dom_ms = kern[dom][0] / args.steps
+    dom_flops = fl.get(dom)
+    # gating computes in the context's scalar type; projection, assembly and Kalman stages in fp64
+    peak = (FP32_PEAK_TFLOPS if dtype == "fp32" else FP64_PEAK_TFLOPS) if dom == "gate" else FP64_PEAK_TFLOPS
+    if not dom_flops:
+        return None
+    ach = dom_flops / (dom_ms * 1e-3) / 1e12
+    traffic = pmc_traffic(dom, dtype, "N%dxF%dxB%d" % (args.N, args.F, args.batch))
+    return {"bound": "mfma", "kernel": dom, "achieved": round(ach, 3), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(ach / peak, 5), "traffic": traffic, "ms_per_step": round(dom_ms, 4),
+            "flops_per_step": dom_flops,
+            "note": "peak of the stage's arithmetic type (fp32 vector = fp32 MFMA, fp64 vector = fp64 MFMA on "
+                    "MI355X); achieved = algorithmic flops (DESIGN.md section 5) / HIP-event device time; traffic = "
+                    "PMC 2 x FETCH_SIZE + WRITE_SIZE bytes per step (profiles/pmc_summary.json)"}
+
+
+def no_triangulation_leg(ctx, args, grp):
+    """updates/s without the triangulation (positions from
+    the previous triangulating step stay resident), the quantity the survey's
+    CPU probe numbers are quoted on."""
+    ctx.restore()
+    ctx.batch_update(row_cap=0, triangulate=False)
+    ctx.sync()
+    grp.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ctx.restore()
+        ctx.batch_update(row_cap=0, triangulate=False)
+    ctx.sync()
+    grp.barrier()
+    el = grp.max_over_ranks(time.perf_counter() - t0)
+    return {"value": round(replicas.whole_job_rate(args.batch, grp.world, args.steps, el), 2),
+            "unit": "updates/s", "ms_per_step": round(el / args.steps * 1e3, 3)}
+
+
+def fp64_leg(args, grp, probs, refs):
+    ctx, feat_off = build_batch(args, probs, np.float64, grp.local_rank)
+    el, times = timed_update(ctx, args, grp)
+    acc, gam, pw, valid, rows = ctx.batch_results()
+    fl = flops_model(probs, args.batch, acc, valid, feat_off)
+    out = {"value": round(replicas.whole_job_rate(args.batch, grp.world, args.steps, el), 2),
+           "unit": "updates/s", "dtype": "f64", "ms_per_step": round(el / args.steps * 1e3, 3),
+           "roofline": roofline_of(times, fl, args, "fp64"),
+           "kernel_ms_per_step": {k: round(v[0] / args.steps, 3)
+                                  for k, v in sorted(times.items(), key=lambda kv: -kv[1][0])}}
+    if refs:
+        out["accuracy"] = accuracy(ctx, refs, acc, feat_off)
+    ctx.close()
     return out
 
 
@@ -203,6 +351,7 @@ def propagation_leg(ctx, args, n_samples=10, steps=5):
     ctx.sync()
     el = time.perf_counter() - t0
     kms = ctx.kernel_times()["propagate"][0] / steps
+    ctx.set_profiling(False)
     ts = 4 if args.dtype == "fp32" else 8
     D, C = 21 + 6 * N, 6 * N
     nbytes = B * (21 * D + 441 + 2 * 21 * C) * ts
@@ -238,55 +387,49 @@ def ate_leg():
                         "tests/golden/sequence_s1.npz; fp64, host loop + one filter per call" % len(traj)}
 
 
-def main():
-    args = parse()
-    grp = replicas.init("nccl")      # replicas only: RCCL carries the barriers and the max of the timing
-    world, rank = grp.world, grp.rank
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:   # before this process initialises the GPU
-        cpu = cpu_baseline(args, [synth.make_update_problem(args.N, args.F, seed=sd)
-                                  for sd in replicas.problem_seeds(rank, min(args.unique, 4))])
-    ctx, probs = build_batch(args, rank, grp.local_rank)
-    barrier = grp.barrier
-
-    for _ in range(args.warmup):
-        ctx.restore()
-        ctx.batch_update(row_cap=0, triangulate=True)
-    ctx.sync()
-    acc, gam, pw, valid, rows = ctx.batch_results()
-    ctx.set_profiling(True)
-    barrier()
-    ctx.sync()
+def stub_main(args, grp):
+    """--stub (tests only): the launch / barrier / max-over-ranks path with a
+    CPU stand-in for a step (rank r sleeps 2 (r + 1) ms per step)."""
+    grp.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        ctx.restore()
-        ctx.batch_update(row_cap=0, triangulate=True)
-    ctx.sync()
-    barrier()
-    el = time.perf_counter() - t0
-    times = ctx.kernel_times()
-    el = grp.max_over_ranks(el)
-    value = replicas.whole_job_rate(args.batch, world, args.steps, el)
-    feat_off = np.concatenate([[0], np.cumsum([probs[b % len(probs)].F for b in range(args.batch)])])
+        time.sleep(0.002 * (grp.rank + 1))
+    grp.barrier()
+    el = grp.max_over_ranks(time.perf_counter() - t0)
+    if grp.rank == 0:
+        print(json.dumps({"metric": metric_name(args), "value": replicas.whole_job_rate(args.batch, grp.world,
+                                                                                      args.steps, el),
+                          "unit": "updates/s", "n_gpus": grp.world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(el / args.steps * 1e3, 3), "data": "stub (no GPU, not a measurement)",
+                          "ranks_seconds_max": el}), flush=True)
+
+
+def main():
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU; this parent never initialises the GPU
+        sys.exit(replicas.spawn([os.path.abspath(__file__)] + sys.argv[1:], args.gpus))
+    grp = replicas.init()
+    if grp.world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but the launcher started %d rank(s)" % (args.gpus, grp.world))
+    if args.stub:
+        stub_main(args, grp)
+        grp.close()
+        return
+    rank = grp.rank
+    dtype = np.float32 if args.dtype == "fp32" else np.float64
+    probs = make_problems(args, rank, min(args.unique, args.batch))
+    cpu, refs = None, []
+    if rank == 0 and grp.world == 1 and not args.no_cpu:   # before this process initialises the GPU
+        cpu, refs = cpu_baseline(args, probs[:N_CHECK])
+
+    ctx, feat_off = build_batch(args, probs, dtype, grp.local_rank)
+    el, times = timed_update(ctx, args, grp)
+    value = replicas.whole_job_rate(args.batch, grp.world, args.steps, el)
+    acc, gam, pw, valid, rows = ctx.batch_results()
     fl = flops_model(probs, args.batch, acc, valid, feat_off)
-    # dominant stage by device time (HIP events on the launch stream, timed region only)
-    kern = {k: v for k, v in times.items() if k != "restore"}
-    dom = max(kern, key=lambda k: kern[k][0])
-    dom_ms = kern[dom][0] / args.steps                  # device ms of the stage per step (all its launches)
-    dom_flops = fl.get(dom)
-    # gating computes in the context's scalar type; projection, assembly and Kalman stages in fp64
-    peak = (FP32_PEAK_TFLOPS if args.dtype == "fp32" else FP64_PEAK_TFLOPS) if dom == "gate" else FP64_PEAK_TFLOPS
-    roof = None
-    if dom_flops:
-        ach = dom_flops / (dom_ms * 1e-3) / 1e12
-        traffic = pmc_traffic(dom, args.dtype, "N%dxF%dxB%d" % (args.N, args.F, args.batch))
-        roof = {"bound": "mfma", "kernel": dom, "achieved": round(ach, 3), "peak": peak, "unit": "TFLOP/s",
-                "frac": round(ach / peak, 5), "traffic": traffic, "ms_per_step": round(dom_ms, 4),
-                "flops_per_step": dom_flops,
-                "note": "vector-ALU peak of the stage's arithmetic type (fp64 vector = fp64 matrix peak on MI355X); "
-                        "traffic = PMC FETCH_SIZE+WRITE_SIZE bytes per step from profiles/pmc_summary.json"}
     out = {
-        "metric": METRIC, "value": round(value, 2), "unit": "updates/s", "n_gpus": world,
+        "metric": metric_name(args), "value": round(value, 2), "unit": "updates/s", "n_gpus": grp.world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "f32/f64" if args.dtype == "fp32" else "f64",
@@ -296,20 +439,25 @@ def main():
                                "triangulation + jacobian + gating + information assembly + Kalman, no row cap"
                                % (args.N, args.F, args.batch),
                    "cam_states": args.N, "features": args.F, "filters_per_gpu": args.batch,
-                   "stacked_rows_mean": float(np.mean(rows)), "parallelism": "replicas%d" % world},
-        "roofline": roof,
+                   "stacked_rows_mean": float(np.mean(rows)), "parallelism": "replicas%d" % grp.world},
+        "roofline": roofline_of(times, fl, args, args.dtype),
         "kernel_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in sorted(times.items(), key=lambda kv: -kv[1][0])},
         "canonical_gflop_per_update": round(fl["canonical"] / args.batch / 1e9, 4),
     }
+    if refs:
+        out["accuracy"] = accuracy(ctx, refs, acc, feat_off)
     if cpu is not None:
         out["cpu_baseline"] = cpu
+    out["without_triangulation"] = no_triangulation_leg(ctx, args, grp)
     if not args.no_prop:
         out["propagation"] = propagation_leg(ctx, args)
+    ctx.close()
+    if args.dtype == "fp32" and not args.no_fp64:
+        out["fp64"] = fp64_leg(args, grp, probs, refs)
     if rank == 0 and not args.no_ate:
         out["ate"] = ate_leg()
     if rank == 0:
         print(json.dumps(out), flush=True)
-    ctx.close()
     grp.close()
 
 

@@ -1,11 +1,16 @@
-"""N > 1 path of bench.py: independent replicas over torch.distributed.
+"""N > 1 path of bench.py: independent replicas, one process per GPU, with a
+host TCP hub for the control messages (msckf_amd/replicas.py, no PyTorch).
 
-Runs the replica helpers (msckf_amd/replicas.py) at world size 2 over gloo on
-CPU: the barrier, the MAX all-reduce of the timing, disjoint problem seeds and
-the whole-job rate -- the same code bench.py runs over RCCL on the GPUs."""
+CPU only: the hub's barrier / MAX / SUM at world size 2, bench.py spawning two
+ranks itself (``--gpus 2``) and the same bench.py under the driver's external
+launcher (torch.distributed.run, rendezvous through the hub file), both with
+``--stub`` in place of the device context."""
+import json
 import os
 import socket
+import subprocess
 import sys
+import textwrap
 
 import pytest
 
@@ -14,6 +19,8 @@ sys.path.insert(0, ROOT)
 import msckf_pkg  # noqa: E402,F401
 from msckf_amd import replicas  # noqa: E402
 
+PKG_DIR = os.path.join(ROOT, "visual-inertial-odometry-msckf-stereo_amd")
+
 
 def _free_port():
     with socket.socket() as s:
@@ -21,33 +28,17 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
-                      LOCAL_RANK=str(rank), WORLD_SIZE=str(world))
-    try:
-        from msckf_amd import synth
-        grp = replicas.init("gloo")
-        seeds = replicas.problem_seeds(grp.rank, 3)
-        # a replica's work is its own batch of synthetic problems
-        prob = synth.make_update_problem(6, 12, seed=seeds[0])
-        grp.barrier()
-        el = 0.5 + grp.rank            # rank 1 is the slow one
-        mx = grp.max_over_ranks(el)
-        rate = replicas.whole_job_rate(64, grp.world, 10, mx)
-        mine = replicas.shard(list(range(11)), grp.rank, grp.world)   # 11 sequences over the ranks
-        total = grp.sum_over_ranks(len(mine))
-        grp.barrier()
-        q.put((grp.rank, grp.world, seeds, float(prob.P.sum()), mx, rate, mine, total))
-        grp.close()
-    except Exception as e:   # surface the failure in the parent
-        q.put((rank, "error", repr(e)))
+def _json_line(stdout):
+    lines = [l for l in stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, stdout
+    return json.loads(lines[0])
 
 
-def test_single_process_needs_no_group(monkeypatch):
-    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+def test_single_process_needs_no_hub(monkeypatch):
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", replicas.HUB_ENV):
         monkeypatch.delenv(k, raising=False)
-    grp = replicas.init("nccl")      # world 1: no process group, no GPU touched
-    assert grp.world == 1 and grp.dist is None
+    grp = replicas.init()      # world 1: no hub, no socket
+    assert grp.world == 1 and grp._sock is None
     assert grp.max_over_ranks(1.25) == 1.25
     grp.barrier()
     grp.close()
@@ -68,27 +59,83 @@ def test_whole_job_rate():
     assert replicas.whole_job_rate(2048, 8, 10, 0.2) == pytest.approx(2048 * 8 * 10 / 0.2)
 
 
+_WORKER = textwrap.dedent("""
+    import json, sys
+    sys.path.insert(0, %r)
+    import msckf_pkg
+    from msckf_amd import replicas
+    grp = replicas.init()
+    grp.barrier()
+    mx = grp.max_over_ranks(0.5 + grp.rank)          # rank 1 is the slow one
+    mine = replicas.shard(list(range(11)), grp.rank, grp.world)
+    total = grp.sum_over_ranks(len(mine))
+    grp.barrier()
+    print(json.dumps({"rank": grp.rank, "world": grp.world, "max": mx, "total": total, "mine": mine}))
+    grp.close()
+""") % ROOT
+
+
 @pytest.mark.timeout(120)
-def test_gloo_world2_replicas():
-    import torch.multiprocessing as mp
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
+def test_hub_world2_collectives():
+    """replicas.spawn: two ranks, the parent hosting the hub."""
+    script = os.path.join(ROOT, "tests", "_replica_worker.py")
+    with open(script, "w") as fh:
+        fh.write(_WORKER)
+    try:
+        out = subprocess.run([sys.executable, "-c",
+                              "import sys; sys.path.insert(0, %r); import msckf_pkg; from msckf_amd import replicas; "
+                              "sys.exit(replicas.spawn([%r], 2))" % (ROOT, script)],
+                             capture_output=True, text=True, timeout=100)
+    finally:
+        os.unlink(script)
+    assert out.returncode == 0, out.stderr
+    res = sorted((json.loads(l) for l in out.stdout.splitlines() if l.startswith("{")), key=lambda r: r["rank"])
+    assert [r["rank"] for r in res] == [0, 1] and all(r["world"] == 2 for r in res)
+    assert all(r["max"] == pytest.approx(1.5) for r in res)       # both see the slowest rank's value
+    assert all(r["total"] == 11 for r in res)
+    assert sorted(res[0]["mine"] + res[1]["mine"]) == list(range(11))
+
+
+@pytest.mark.timeout(120)
+def test_bench_spawns_ranks():
+    """bench.py --gpus 2 starts its own two ranks (the parent never touches a
+    GPU) and reports n_gpus = 2 with the slowest rank's time."""
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--no-cpu", "--stub",
+                          "--steps", "5"], capture_output=True, text=True, timeout=100,
+                         env={k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")})
+    assert out.returncode == 0, out.stderr
+    line = _json_line(out.stdout)
+    assert line["n_gpus"] == 2
+    assert line["ms_per_step"] >= 4.0              # rank 1 sleeps 4 ms per step
+    assert line["value"] == pytest.approx(2048 * 2 * 5 / line["ranks_seconds_max"])
+
+
+@pytest.mark.timeout(180)
+def test_bench_under_external_launcher():
+    """The driver's launch: torch.distributed.run starts the ranks with
+    WORLD_SIZE set; rank 0 hosts the hub and the others find it through the
+    rendezvous file."""
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    res = [q.get(timeout=100) for _ in procs]
-    for p in procs:
-        p.join(timeout=30)
-        assert p.exitcode == 0
-    for r in res:
-        assert r[1] != "error", r
-    res.sort()
-    (r0, w0, s0, p0, m0, v0, sh0, t0), (r1, w1, s1, p1, m1, v1, sh1, t1) = res
-    assert sorted(sh0 + sh1) == list(range(11)) and not (set(sh0) & set(sh1))   # each sequence on one rank
-    assert t0 == t1 == 11
-    assert (r0, r1) == (0, 1) and w0 == w1 == 2
-    assert not (set(s0) & set(s1))          # different problems per replica
-    assert p0 != p1
-    assert m0 == m1 == pytest.approx(1.5)   # both ranks see the slowest rank's time
-    assert v0 == v1 == pytest.approx(64 * 2 * 10 / 1.5)
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                          "--master-addr", "127.0.0.1", "--master-port", str(port),
+                          os.path.join(ROOT, "bench.py"), "--gpus", "2", "--no-cpu", "--stub", "--steps", "5"],
+                         capture_output=True, text=True, timeout=170)
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = _json_line(out.stdout)
+    assert line["n_gpus"] == 2 and line["ms_per_step"] >= 4.0
+
+
+def test_bench_rejects_gpus_mismatch():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--stub"],
+                         capture_output=True, text=True, timeout=60, env=env)
+    assert out.returncode != 0 and "--gpus 2" in out.stderr
+
+
+def test_package_has_no_torch():
+    """north_star: no PyTorch in the product -- not even in the replica layer."""
+    for dirpath, _, files in os.walk(PKG_DIR):
+        for f in files:
+            if f.endswith(".py"):
+                src = open(os.path.join(dirpath, f)).read()
+                assert "import torch" not in src and "from torch" not in src, f

@@ -39,7 +39,7 @@ def main():
     ap.add_argument("--no-single", action="store_true")
     a = ap.parse_args()
     dtype = np.float32 if a.fp32 else np.float64
-    grp = replicas.init("nccl")
+    grp = replicas.init()
     mine = replicas.shard(list(range(a.seqs)), grp.rank, grp.world)
     streams = [FeatureStream.from_synthetic(synth.make_sequence(a.frames, 100 + i)) for i in mine]
     n_frames = sum(s.n_frames for s in streams)

@@ -3,17 +3,100 @@
 The EKF update does not shard: one filter's covariance is a
 few hundred KB and every stage of its update is a chain of small dependent
 factorisations, so there is no data-parallel exchange to make.  N GPUs run N
-independent batches of filters, one process per GPU (torch.distributed.run);
-the process group is used only for the start/stop barriers of the timed
-region and for the max-over-ranks of the elapsed time.  No collective touches
-the data path.
+independent batches of filters, one process per GPU.  The ranks exchange only
+control: the start / stop barriers of the timed region and the max (or sum)
+of a float.  No collective touches the data path, so none is on a GPU: the
+control messages travel over a host TCP hub (stdlib sockets, no PyTorch).
 
-The helpers take the backend as a parameter so the same code runs over RCCL
-("nccl") on the GPU box and over gloo on CPU in the tests.
+Launch modes (both one process per GPU, RANK / LOCAL_RANK / WORLD_SIZE in the
+environment):
+* ``spawn(argv, n)`` -- the parent process (which never touches the GPU)
+  starts n children, hosts the hub and passes its address in MSCKF_HUB;
+* an external launcher (``python -m torch.distributed.run --nproc-per-node N``
+  on one node, as the driver runs bench.py) -- rank 0 hosts the hub and
+  publishes its port in a rendezvous file keyed by MASTER_PORT and the
+  launcher's pid (every rank's parent), under the temp directory.
 """
+import json
 import os
+import socket
+import subprocess
+import sys
+import tempfile
+import threading
+import time
 from dataclasses import dataclass
 from typing import List, Optional
+
+HUB_ENV = "MSCKF_HUB"
+TIMEOUT_S = 900.0
+
+
+def _send(sock, obj):
+    sock.sendall((json.dumps(obj) + "\n").encode())
+
+
+class _Lines:
+    """Newline-delimited JSON reader over a socket."""
+
+    def __init__(self, sock):
+        self.sock, self.buf = sock, b""
+
+    def read(self):
+        while b"\n" not in self.buf:
+            chunk = self.sock.recv(65536)
+            if not chunk:
+                raise ConnectionError("replica hub: peer closed the connection")
+            self.buf += chunk
+        line, self.buf = self.buf.split(b"\n", 1)
+        return json.loads(line)
+
+
+class Hub:
+    """Serves ``world`` ranks: each round every rank sends {op, v}; once all
+    have arrived the hub replies to each with the reduction (max / sum /
+    barrier).  All ranks issue the same collectives in the same order."""
+
+    def __init__(self, world: int, host: str = "127.0.0.1", port: int = 0):
+        self.world = world
+        self.srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+        self.srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+        self.srv.bind((host, port))
+        self.srv.listen(world)
+        self.srv.settimeout(TIMEOUT_S)
+        self.address = "%s:%d" % self.srv.getsockname()[:2]
+        self.error: Optional[BaseException] = None
+        self.thread = threading.Thread(target=self._run, daemon=True)
+        self.thread.start()
+
+    def _run(self):
+        conns = {}
+        try:
+            while len(conns) < self.world:
+                c, _ = self.srv.accept()
+                c.settimeout(TIMEOUT_S)
+                r = _Lines(c)
+                hello = r.read()
+                conns[int(hello["rank"])] = (c, r)
+            order = [conns[k] for k in sorted(conns)]
+            while True:
+                msgs = [r.read() for _, r in order]
+                ops = {m["op"] for m in msgs}
+                if len(ops) != 1:
+                    raise RuntimeError("replica hub: ranks disagree on the collective: %s" % sorted(ops))
+                op = ops.pop()
+                vals = [float(m.get("v", 0.0)) for m in msgs]
+                res = {"max": max(vals), "sum": sum(vals)}.get(op, 0.0)
+                for c, _ in order:
+                    _send(c, {"v": res})
+                if op == "close":
+                    break
+        except BaseException as e:   # surfaced to the ranks as a closed connection
+            self.error = e
+        finally:
+            for c, _ in conns.values():
+                c.close()
+            self.srv.close()
 
 
 @dataclass
@@ -21,53 +104,108 @@ class ReplicaGroup:
     rank: int
     world: int
     local_rank: int
-    dist: Optional[object]   # torch.distributed when world > 1
-    device: str              # tensor device used for the reductions
+    _sock: Optional[socket.socket] = None
+    _lines: Optional[_Lines] = None
+    _hub: Optional[Hub] = None
+    _rdzv: Optional[str] = None
+
+    def _call(self, op, v=0.0):
+        if self._sock is None:
+            return float(v)
+        _send(self._sock, {"op": op, "v": float(v)})
+        return float(self._lines.read()["v"])
 
     def barrier(self):
-        if self.dist is not None:
-            self.dist.barrier()
+        self._call("barrier")
 
     def max_over_ranks(self, x: float) -> float:
-        """MAX all-reduce of one float (the timed region's elapsed seconds)."""
-        if self.dist is None:
-            return float(x)
-        import torch
-        t = torch.tensor([float(x)], dtype=torch.float64, device=self.device)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
-        return float(t.item())
+        """MAX over ranks of one float (the timed region's elapsed seconds)."""
+        return self._call("max", x)
 
     def sum_over_ranks(self, x: float) -> float:
-        """SUM all-reduce of one float (e.g. frames processed by every rank)."""
-        if self.dist is None:
-            return float(x)
-        import torch
-        t = torch.tensor([float(x)], dtype=torch.float64, device=self.device)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
-        return float(t.item())
+        """SUM over ranks of one float (e.g. frames processed by every rank)."""
+        return self._call("sum", x)
 
     def close(self):
-        if self.dist is not None:
-            self.dist.destroy_process_group()
+        if self._sock is not None:
+            self._call("close")
+            self._sock.close()
+            self._sock = None
+        if self._hub is not None:
+            self._hub.thread.join(timeout=30)
+        if self._rdzv and os.path.exists(self._rdzv):
+            os.unlink(self._rdzv)
 
 
-def init(backend: str = "nccl") -> ReplicaGroup:
-    """One process per GPU; RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* from the
-    environment (torch.distributed.run sets them).  World size 1 needs no
-    process group."""
+def _rdzv_path():
+    key = "%s_%d" % (os.environ.get("MASTER_PORT", "0"), os.getppid())
+    return os.path.join(tempfile.gettempdir(), "msckf_replicas_%s.hub" % key)
+
+
+def _connect(address: str, rank: int):
+    host, port = address.rsplit(":", 1)
+    deadline = time.time() + 120
+    while True:
+        try:
+            s = socket.create_connection((host, int(port)), timeout=TIMEOUT_S)
+            break
+        except OSError:
+            if time.time() > deadline:
+                raise
+            time.sleep(0.1)
+    _send(s, {"rank": rank})
+    return s
+
+
+def init() -> ReplicaGroup:
+    """One process per GPU; RANK / LOCAL_RANK / WORLD_SIZE from the
+    environment.  World size 1 needs no hub."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    grp = ReplicaGroup(rank, world, local)
     if world <= 1:
-        return ReplicaGroup(rank, 1, local, None, "cpu")
-    import torch
-    import torch.distributed as dist
-    device = "cpu"
-    if backend == "nccl":
-        torch.cuda.set_device(local)
-        device = "cuda"
-    dist.init_process_group(backend)
-    return ReplicaGroup(rank, world, local, dist, device)
+        return grp
+    address = os.environ.get(HUB_ENV)
+    if not address:   # external launcher: rank 0 hosts the hub, the others find it on disk
+        path = _rdzv_path()
+        if rank == 0:
+            grp._hub = Hub(world, os.environ.get("MASTER_ADDR", "127.0.0.1"))
+            address = grp._hub.address
+            tmp = path + ".%d.tmp" % os.getpid()
+            with open(tmp, "w") as fh:
+                fh.write(address)
+            os.replace(tmp, path)
+            grp._rdzv = path
+        else:   # wait for a file written by THIS job's rank 0 (not a stale one of a dead job)
+            t0 = time.time()
+            while not (os.path.exists(path) and os.path.getmtime(path) > t0 - 60):
+                if time.time() > t0 + 120:
+                    raise TimeoutError("replica hub rendezvous file %s never appeared" % path)
+                time.sleep(0.05)
+            with open(path) as fh:
+                address = fh.read().strip()
+    grp._sock = _connect(address, rank)
+    grp._lines = _Lines(grp._sock)
+    return grp
+
+
+def spawn(argv: List[str], n: int, env_extra: Optional[dict] = None) -> int:
+    """Runs ``python argv...`` as n ranks (one per GPU) from a parent that
+    never initialises the GPU; the parent hosts the hub.  Returns the first
+    non-zero exit code of the ranks (0 if all succeed)."""
+    hub = Hub(n)
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update(env_extra or {})
+        env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1")
+        env[HUB_ENV] = hub.address
+        procs.append(subprocess.Popen([sys.executable] + list(argv), env=env))
+    codes = [p.wait() for p in procs]
+    hub.thread.join(timeout=30)
+    return next((c for c in codes if c != 0), 0)
 
 
 def problem_seeds(rank: int, unique: int) -> List[int]:
