@@ -356,6 +356,36 @@ def test_gate_fp32_gamma_vs_oracle(N, F, B):
     assert np.quantile(e, 0.99) < 1e-2, np.quantile(e, 0.99)
 
 
+def test_gate_fp32_scrambled_observation_order():
+    """gamma is invariant under a permutation of a feature's observations (an
+    orthogonal row map of the stacked system, quirk Q4), so scrambling them
+    must reproduce the oracle's gamma.  With slots out of order, the
+    filter-resident fp32 gating (k_gate_res) reads P_cc blocks (b, a) of its
+    lower-triangle LDS image transposed: this exercises that path (the sorted
+    case is every other fp32 test).  Tolerance as the fp32 gamma test."""
+    rng = np.random.default_rng(11)
+    problems = [synth.make_update_problem(30, 200, seed=500 + b) for b in range(2)]
+    ref = [oracle_update(problem_to_dict(p)) for p in problems]
+    for p in problems:   # scramble in place: obs_cam / obs_z rows within each feature
+        for f in range(p.F):
+            o0, o1 = p.obs_off[f], p.obs_off[f + 1]
+            perm = o0 + rng.permutation(o1 - o0)
+            p.obs_cam[o0:o1] = p.obs_cam[perm]
+            p.obs_z[o0:o1] = p.obs_z[perm]
+    ctx, ds, feat_off, acc, gam, pw, valid, rows = _batched(problems, np.float32)
+    errs = []
+    for b, (st, acc_o, tri_p, tri_ok, gam_o) in enumerate(ref):
+        sl = slice(feat_off[b], feat_off[b + 1])
+        ok = valid[sl] & tri_ok
+        g, go = gam[sl][ok], gam_o[ok]
+        assert np.isfinite(g).all()
+        errs.append(np.abs(g - go) / np.maximum(np.abs(go), 1e-6))
+    e = np.concatenate(errs)
+    assert e.size > 300
+    assert np.median(e) < 1e-4, np.median(e)
+    assert np.quantile(e, 0.99) < 1e-2, np.quantile(e, 0.99)
+
+
 def test_restore_repeats_identically():
     problems = [synth.make_update_problem(20, 60, seed=7 + b) for b in range(2)]
     ds = [problem_to_dict(p) for p in problems]

@@ -1,0 +1,10 @@
+# GPU parity suite, the fp32 bench, and one SQ counter pass of the gating kernels.
+set -o pipefail
+OUT=gpurun_out/${1:-r02f}
+mkdir -p $OUT
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/t.log 2>&1 &&
+timeout -k 10 300 python -u bench.py --no-cpu --no-ate --no-fp64 --no-prop > $OUT/b32.json 2> $OUT/b32.err || exit 1
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+CTR="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_LDS_BANK_CONFLICT"
+timeout -s KILL 90 rocprofv3 --pmc $CTR --kernel-include-regex "k_gate" -d $OUT/pmc -o run --output-format csv -- \
+    python3 bench.py --steps 1 --warmup 0 --no-cpu --no-ate --no-prop --no-fp64 > $OUT/pmc.log 2>&1

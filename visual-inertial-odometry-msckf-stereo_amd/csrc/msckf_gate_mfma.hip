@@ -35,19 +35,169 @@ using F2 = float __attribute__((ext_vector_type(2)));
 
 __host__ __device__ constexpr int gm_nb(int M) { return (3 * M + 4 + 15) / 16; }
 __host__ __device__ constexpr int gm_head(int Mmax) { return (22 * Mmax + 3) & ~3; }   // Ht rows + [r~ | r_n]
-__host__ __device__ constexpr int gm_area(int Mmax, int capb) {                         // Y staging / panel
-    return 9 * capb > 64 * gm_nb(Mmax) ? ((9 * capb + 3) & ~3) : 64 * gm_nb(Mmax);
+__host__ __device__ constexpr int gm_area(int Mmax, int capb) {   // Y staging / panel + junk panel
+    return 9 * capb > 128 * gm_nb(Mmax) + 16 ? ((9 * capb + 3) & ~3) : 128 * gm_nb(Mmax) + 16;
 }
-__host__ __device__ constexpr int gm_wave_floats(int Mmax, int capb) {
-    return gm_head(Mmax) + gm_area(Mmax, capb) + ((Mmax + 3) & ~3);
+__host__ __device__ constexpr int gm_wave_floats(int Mmax, int capb) {   // + two int offset tables
+    return gm_head(Mmax) + gm_area(Mmax, capb) + 2 * ((Mmax + 3) & ~3);
 }
 #ifndef GATE_BIF_BIG
 #define GATE_BIF_BIG 3
 #endif
 __host__ __device__ constexpr int bidx(int rb, int cb) { return rb * (rb + 1) / 2 + cb; }
+// The one-wave size classes (GateClasses::LIM) are exactly the 16-row block
+// counts: every feature of class c fills nb = c + 1 blocks, so the kernel of a
+// class runs with a compile-time block count.
+constexpr bool gm_class_exact() {
+    for (int c = 0; c < GateClasses::NC - 2; ++c) {
+        const int lo = c == 0 ? 1 : GateClasses::LIM[c - 1] + 1;
+        if (gm_nb(lo) != c + 1 || gm_nb(GateClasses::LIM[c]) != c + 1) return false;
+    }
+    return true;
+}
+static_assert(gm_class_exact(), "gating size classes must match the MFMA block counts");
+
+// Blocked LDL^T of the assembled lower block triangle, 4 pivots per step (see
+// the file header).  acc holds blocks (RB, CB), CB <= RB < NB, in the C layout
+// of v_mfma_f32_16x16x4_f32; pan is the wave's [16 NB][4] panel, followed by
+// a junk copy for the lanes that own no pivot column.  The feature
+// fills exactly NB blocks (its size class), so the elimination runs all
+// 4 NB - 1 steps up to the B rows: the unit padding pivots beyond 3M have zero
+// couplings and leave everything unchanged.  No branches (a non-positive pivot
+// only sets the returned flag; its garbage is discarded by gm_finish) and no
+// explicit LDS waits (one wave's LDS operations complete in issue order): the
+// whole elimination is one basic block, so the scheduler can overlap the next
+// step's panel dump / reads / 4x4 factor with this step's MFMA tail.
+template <int NB>
+__device__ __forceinline__ bool gm_eliminate(F4 (&acc)[NB * (NB + 1) / 2], float* pan, int lane) {
+    const int col_l = lane & 15, rg = lane >> 4;
+    const int csel = rg;   // pivot column of this lane's operands
+    // this lane's B-operand element of block row RB: panel row 16 RB + col_l, column csel
+    const float* bsrc = pan + 4 * col_l + csel;
+    const bool owner[4] = {(col_l >> 2) == 0, (col_l >> 2) == 1, (col_l >> 2) == 2, (col_l >> 2) == 3};
+    bool ok = true;
+#pragma unroll
+    for (int KB = 0; KB < NB; ++KB) {
+#pragma unroll
+        for (int sc = 0; sc < 4; ++sc) {
+            if (KB == NB - 1 && sc == 3) break;   // the last four rows are the B rows
+            const int p0 = 16 * KB + 4 * sc;
+            // 1. owners of columns p0 .. p0 + 3 dump them (rows of blocks KB..NB-1);
+            //    the other lanes write to a junk area past the panel (pan + 64 NB,
+            //    one dword column per lane: no bank conflicts) -- no divergent
+            //    branch in the step
+            {
+                float* d = owner[sc] ? pan + 4 * (16 * KB + 4 * rg) + (col_l & 3) : pan + 64 * NB + lane;
+#pragma unroll
+                for (int RB = KB; RB < NB; ++RB) {
+                    const F4 v = acc[bidx(RB, KB)];
+                    float* dd = d + 64 * (RB - KB);
+                    dd[0] = v[0]; dd[4] = v[1]; dd[8] = v[2]; dd[12] = v[3];
+                }
+            }
+            // 2. every lane factors the diagonal 4x4 A_d = L D L^T (lower entries only)
+            const F4 r0 = *reinterpret_cast<const F4*>(pan + 4 * p0);
+            const F4 r1 = *reinterpret_cast<const F4*>(pan + 4 * p0 + 4);
+            const F4 r2 = *reinterpret_cast<const F4*>(pan + 4 * p0 + 8);
+            const F4 r3 = *reinterpret_cast<const F4*>(pan + 4 * p0 + 12);
+            F4 xr[NB];   // this lane's panel row of every block row
+            float bv[NB];
+#pragma unroll
+            for (int RB = KB; RB < NB; ++RB) {
+                xr[RB] = *reinterpret_cast<const F4*>(pan + 4 * (16 * RB + col_l));
+                bv[RB] = bsrc[64 * RB];
+            }
+            const float d0 = r0.x, e0 = pivot_rcp(d0);
+            const float l10 = r1.x * e0, l20 = r2.x * e0, l30 = r3.x * e0;
+            const float d1 = r1.y - l10 * r1.x, e1 = pivot_rcp(d1);
+            const float m21 = r2.y - l20 * r1.x, m31 = r3.y - l30 * r1.x;
+            const float l21 = m21 * e1, l31 = m31 * e1;
+            const float d2 = r2.z - l20 * r2.x - l21 * m21, e2 = pivot_rcp(d2);
+            const float m32 = r3.z - l30 * r2.x - l31 * m21;
+            const float l32 = m32 * e2;
+            const float d3 = r3.w - l30 * r3.x - l31 * m31 - l32 * m32;
+            ok = ok && (d0 > 0.f) && (d1 > 0.f) && (d2 > 0.f) && (d3 > 0.f);
+            const float e3 = pivot_rcp(d3);
+            // 3. the rank-4 update is C -= X A_d^-1 X^T, X = the panel columns: the
+            //    B operand is X itself (lane: row 16 RB + col_l, pivot csel), the A
+            //    operand X m with m = -(column csel of A_d^-1 = L^-T D^-1 L^-1).  Rows
+            //    of finished pivots are not masked: exact elimination leaves them
+            //    zero, and they only ever feed finished rows / columns.
+            const float i10 = -l10, i21 = -l21, i32 = -l32;
+            const float i20 = -l20 - l21 * i10, i31 = -l31 - l32 * i21;
+            const float i30 = -l30 - l31 * i10 - l32 * i20;
+            // h_j = (L^-1)[j][csel]; u_j = h_j / d_j
+            const float u0 = csel == 0 ? e0 : 0.f;
+            const float u1 = (csel == 1 ? 1.f : (csel == 0 ? i10 : 0.f)) * e1;
+            const float u2 = (csel == 2 ? 1.f : (csel == 1 ? i21 : (csel == 0 ? i20 : 0.f))) * e2;
+            const float u3 = (csel == 3 ? 1.f : (csel == 2 ? i32 : (csel == 1 ? i31 : i30))) * e3;
+            const float mm3 = -u3;
+            const float mm2 = -fmaf(i32, u3, u2);
+            const float mm1 = -fmaf(i31, u3, fmaf(i21, u2, u1));
+            const float mm0 = -fmaf(i30, u3, fmaf(i20, u2, fmaf(i10, u1, u0)));
+            float av[NB];
+#pragma unroll
+            for (int RB = KB; RB < NB; ++RB) {
+                const F4 x = xr[RB];
+                av[RB] = fmaf(x.w, mm3, fmaf(x.z, mm2, fmaf(x.y, mm1, x.x * mm0)));
+            }
+            // 4. trailing rank-4 update of the lower block triangle right of the panel
+            //    (after a block's last step its own column is finished: skipped)
+            if (sc < 3) {
+#pragma unroll
+                for (int RB = KB; RB < NB; ++RB)
+                    acc[bidx(RB, KB)] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[RB], bv[KB], acc[bidx(RB, KB)], 0, 0, 0);
+            }
+#pragma unroll
+            for (int CB = KB + 1; CB < NB; ++CB)
+#pragma unroll
+                for (int RB = CB; RB < NB; ++RB)
+                    acc[bidx(RB, CB)] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[RB], bv[CB], acc[bidx(RB, CB)], 0, 0, 0);
+        }
+    }
+    return !ok;
+}
+
+// gamma from the B rows' 4x4 Schur block (negated [[H_f~^T Y~^-1 H_f~, .],
+// [., r~^T Y~^-1 r~]]): rows / cols 12..15 of block (nb-1, nb-1), lanes 60..63.
+template <int NB>
+__device__ __forceinline__ void gm_finish(const F4 (&acc)[NB * (NB + 1) / 2], float* pan, int nb, int lane, bool fail,
+                                          float rn2, float s2, const FeatBatch<float>& fb, int f) {
+    const int col_l = lane & 15, rg = lane >> 4;
+#pragma unroll
+    for (int RB = 0; RB < NB; ++RB)
+        if (RB == nb - 1 && rg == 3 && col_l >= 12) {
+            const F4 v = acc[bidx(RB, RB)];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) pan[4 * i + (col_l - 12)] = v[i];
+        }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) {
+        const float* a = pan;
+        const float d0 = a[0];
+        const float l10 = a[4] / d0, l20 = a[8] / d0, l30 = a[12] / d0;
+        const float d1 = a[5] - l10 * l10 * d0;
+        const float l21 = (a[9] - l20 * l10 * d0) / d1;
+        const float l31 = (a[13] - l30 * l10 * d0) / d1;
+        const float d2 = a[10] - l20 * l20 * d0 - l21 * l21 * d1;
+        const float l32 = (a[14] - l30 * l20 * d0 - l31 * l21 * d1) / d2;
+        const float d3 = a[15] - l30 * l30 * d0 - l31 * l31 * d1 - l32 * l32 * d2;
+        float gam = -d3 + rn2 / s2;
+        if (fail || !(d0 < 0.f) || !(d1 < 0.f) || !(d2 < 0.f) || !(gam == gam)) gam = INFINITY;
+        fb.gamma[f] = gam;
+        fb.accept[f] = (gam < fb.chi2[f]) ? 1 : 0;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // pan reads done before it is reused
+}
+
+// waves per SIMD the accumulators (4 NB (NB + 1) / 2 registers) leave room for
+// (single-pass Y staging keeps two or three pair blocks in flight: one wave less)
+__host__ __device__ constexpr int gm_waves(int NB, bool MP) {
+    return (NB <= 2 && MP) ? 5 : (NB <= 4 ? 4 : (NB <= 6 ? 3 : 2));
+}
 
 template <int NB, bool MP>
-__global__ void __launch_bounds__(256) k_gate_mfma(DevState<float> st, Params<float> prm, FeatBatch<float> fb,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_waves(NB, MP)))) k_gate_mfma(DevState<float> st, Params<float> prm, FeatBatch<float> fb,
                                                    const int* __restrict__ flist, int nlist, int Mmax, int capb) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wpb = blockDim.x >> 6;
@@ -63,8 +213,7 @@ __global__ void __launch_bounds__(256) k_gate_mfma(DevState<float> st, Params<fl
     const int b = __builtin_amdgcn_readfirstlane(fb.feat_filter[f]);
     const int o0 = __builtin_amdgcn_readfirstlane(fb.obs_off[f]);
     const int M = __builtin_amdgcn_readfirstlane(fb.obs_off[f + 1]) - o0, M3 = 3 * M;
-    const int nY = (M3 + 3) >> 2;          // elimination steps, 4 pivots each
-    const int nb = gm_nb(M);               // 16-row blocks in use (<= NB)
+    constexpr int nb = NB;                 // the size class: gm_nb(M) == NB (gm_class_exact)
     const int nB = 16 * nb - 4;            // first B row
     float* ht = reinterpret_cast<float*>(smem_raw) + (size_t)wv * gm_wave_floats(Mmax, capb);
     float* rt = ht + 18 * Mmax;            // [Mmax][4]: r~ (3), r_n
@@ -84,10 +233,15 @@ __global__ void __launch_bounds__(256) k_gate_mfma(DevState<float> st, Params<fl
         if ((e & 3) == 3) rn2 += v * v;
     }
     rn2 = wave_sum(rn2);
-    for (int i = lane; i < M; i += 64) slot[i] = fb.obs_cam[o0 + i];
+    // P offsets of the observations' cam blocks: row part (21 + 6 s) ldp + 21, column part 6 s
+    int* coff = slot + ((Mmax + 3) & ~3);
+    for (int i = lane; i < M; i += 64) {
+        const int sl = fb.obs_cam[o0 + i];
+        slot[i] = (21 + 6 * sl) * st.Dmax + 21;
+        coff[i] = 6 * sl;
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 
-    const int col_l = lane & 15, rg = lane >> 4;
     constexpr int NBLK = NB * (NB + 1) / 2;
     F4 acc[NBLK];
     // Matrix assembly into the C-layout blocks of block rows [R0, R1): every
@@ -138,7 +292,6 @@ __global__ void __launch_bounds__(256) k_gate_mfma(DevState<float> st, Params<fl
                     a[i] = v;
                 }
                 acc[bidx(RB, CB)] = a;
-                asm volatile("" : "+a"(acc[bidx(RB, CB)]));   // finished block -> AGPRs now (VGPR budget)
             }
         }
     };
@@ -174,16 +327,18 @@ __global__ void __launch_bounds__(256) k_gate_mfma(DevState<float> st, Params<fl
             for (int j = 0; j < BIF; ++j) {
                 const int kk = k0 + 64 * j + lane;
                 const int k = kbase + (kk < nbp ? kk : 0);
-                int a = (int)((sqrtf(8.0f * (float)k + 1.0f) - 1.0f) * 0.5f);
+                // row of pair k: the hardware square root (1 ulp) is enough, the
+                // two integer fix-ups make the decode exact
+                int a = (int)((__builtin_amdgcn_sqrtf(8.0f * (float)k + 1.0f) - 1.0f) * 0.5f);
                 if (a * (a + 1) / 2 > k) --a;
                 if ((a + 1) * (a + 2) / 2 <= k) ++a;
                 oa[j] = a;
                 ob[j] = k - a * (a + 1) / 2;
-                const float* Pb = P + (size_t)(21 + 6 * slot[oa[j]]) * ldp + 21 + 6 * slot[ob[j]];
+                const float* Pb = P + (slot[oa[j]] + coff[ob[j]]);
 #pragma unroll
                 for (int u = 0; u < 6; ++u) {
                     if (kk < nbp) {
-                        __builtin_memcpy(Pl[j] + 6 * u, Pb + (size_t)u * ldp, 6 * sizeof(float));
+                        __builtin_memcpy(Pl[j] + 6 * u, Pb + u * ldp, 6 * sizeof(float));
                     } else {
 #pragma unroll
                         for (int c2 = 0; c2 < 6; ++c2) Pl[j][6 * u + c2] = 0.f;
@@ -233,109 +388,9 @@ __global__ void __launch_bounds__(256) k_gate_mfma(DevState<float> st, Params<fl
     }
 
     // ---- blocked LDL^T, 4 pivots per step, MFMA trailing updates ----
-    bool fail = false;
-    const int csel = rg;   // pivot column of this lane's operands
-#pragma unroll
-    for (int KB = 0; KB < NB; ++KB) {
-        if (4 * KB >= nY || fail) break;
-        for (int sc = 0; sc < 4; ++sc) {
-            const int j = 4 * KB + sc;
-            if (j >= nY) break;
-            const int p0 = 4 * j;
-            // 1. owners of columns p0 .. p0 + 3 dump them (rows of blocks KB..NB-1;
-            //    blocks past nb carry stale rows that step 3 masks)
-            if ((col_l >> 2) == sc) {
-                float* d = pan + 4 * (16 * KB + 4 * rg) + (col_l & 3);
-#pragma unroll
-                for (int RB = KB; RB < NB; ++RB) {
-                    const F4 v = acc[bidx(RB, KB)];
-                    float* dd = d + 64 * (RB - KB);
-                    dd[0] = v[0]; dd[4] = v[1]; dd[8] = v[2]; dd[12] = v[3];
-                }
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            // 2. every lane factors the diagonal 4x4 (lower entries only)
-            const F4 r0 = *reinterpret_cast<const F4*>(pan + 4 * p0);
-            const F4 r1 = *reinterpret_cast<const F4*>(pan + 4 * p0 + 4);
-            const F4 r2 = *reinterpret_cast<const F4*>(pan + 4 * p0 + 8);
-            const F4 r3 = *reinterpret_cast<const F4*>(pan + 4 * p0 + 12);
-            F4 xr[NB];   // this lane's panel row of every block row
-#pragma unroll
-            for (int RB = KB; RB < NB; ++RB) xr[RB] = *reinterpret_cast<const F4*>(pan + 4 * (16 * RB + col_l));
-            const float d0 = r0.x, e0 = pivot_rcp(d0);
-            const float l10 = r1.x * e0, l20 = r2.x * e0, l30 = r3.x * e0;
-            const float d1 = r1.y - l10 * r1.x, e1 = pivot_rcp(d1);
-            const float m21 = r2.y - l20 * r1.x, m31 = r3.y - l30 * r1.x;
-            const float l21 = m21 * e1, l31 = m31 * e1;
-            const float d2 = r2.z - l20 * r2.x - l21 * m21, e2 = pivot_rcp(d2);
-            const float m32 = r3.z - l30 * r2.x - l31 * m21;
-            const float l32 = m32 * e2;
-            const float d3 = r3.w - l30 * r3.x - l31 * m31 - l32 * m32;
-            if (!(d0 > 0.f) || !(d1 > 0.f) || !(d2 > 0.f) || !(d3 > 0.f)) { fail = true; break; }
-            const float e3 = pivot_rcp(d3);
-            // 3. operands: lane l holds row 16 RB + (l & 15), pivot column c = l >> 4:
-            //    W[r][c] = (x L_d^-T)[c] = sum_k x_k (L_d^-1)[c][k] -- this lane's row
-            //    of L_d^-1 is chosen once per step; rows of finished pivots and of
-            //    blocks past nb are zero
-            const float i10 = -l10, i21 = -l21, i32 = -l32;
-            const float i20 = -l20 - l21 * i10, i31 = -l31 - l32 * i21;
-            const float i30 = -l30 - l31 * i10 - l32 * i20;
-            const float g0 = csel == 0 ? 1.f : (csel == 1 ? i10 : (csel == 2 ? i20 : i30));
-            const float g1 = csel == 0 ? 0.f : (csel == 1 ? 1.f : (csel == 2 ? i21 : i31));
-            const float g2 = csel <= 1 ? 0.f : (csel == 2 ? 1.f : i32);
-            const float g3 = csel == 3 ? 1.f : 0.f;
-            const float esel = -(csel == 0 ? e0 : (csel == 1 ? e1 : (csel == 2 ? e2 : e3)));
-            float av[NB], bv[NB];
-#pragma unroll
-            for (int RB = KB; RB < NB; ++RB) {
-                const int r = 16 * RB + col_l;
-                const F4 x = xr[RB];
-                float w = fmaf(x.w, g3, fmaf(x.z, g2, fmaf(x.y, g1, x.x * g0)));
-                w = (r <= p0 + 3 || RB >= nb) ? 0.f : w;
-                bv[RB] = w;
-                av[RB] = w * esel;
-            }
-            // 4. trailing rank-4 update of the lower block triangle right of the panel
-            //    (after a block's last step its own column is finished: skipped)
-            if (sc < 3) {
-#pragma unroll
-                for (int RB = KB; RB < NB; ++RB)
-                    acc[bidx(RB, KB)] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[RB], bv[KB], acc[bidx(RB, KB)], 0, 0, 0);
-            }
-#pragma unroll
-            for (int CB = KB + 1; CB < NB; ++CB)
-#pragma unroll
-                for (int RB = CB; RB < NB; ++RB)
-                    acc[bidx(RB, CB)] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[RB], bv[CB], acc[bidx(RB, CB)], 0, 0, 0);
-        }
-    }
-    // the B rows' 4x4 Schur block (negated [[H_f~^T Y~^-1 H_f~, .], [., r~^T Y~^-1 r~]]):
-    // rows / cols 12..15 of block (nb-1, nb-1) sit in lanes 60..63
-#pragma unroll
-    for (int RB = 0; RB < NB; ++RB)
-        if (RB == nb - 1 && rg == 3 && col_l >= 12) {
-            const F4 v = acc[bidx(RB, RB)];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) pan[4 * i + (col_l - 12)] = v[i];
-        }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (lane == 0) {
-        const float* a = pan;
-        const float d0 = a[0];
-        const float l10 = a[4] / d0, l20 = a[8] / d0, l30 = a[12] / d0;
-        const float d1 = a[5] - l10 * l10 * d0;
-        const float l21 = (a[9] - l20 * l10 * d0) / d1;
-        const float l31 = (a[13] - l30 * l10 * d0) / d1;
-        const float d2 = a[10] - l20 * l20 * d0 - l21 * l21 * d1;
-        const float l32 = (a[14] - l30 * l20 * d0 - l31 * l21 * d1) / d2;
-        const float d3 = a[15] - l30 * l30 * d0 - l31 * l31 * d1 - l32 * l32 * d2;
-        float gam = -d3 + rn2 / s2;
-        if (fail || !(d0 < 0.f) || !(d1 < 0.f) || !(d2 < 0.f) || !(gam == gam)) gam = INFINITY;
-        fb.gamma[f] = gam;
-        fb.accept[f] = (gam < fb.chi2[f]) ? 1 : 0;
-    }
+    const bool fail = gm_eliminate<NB>(acc, pan, lane);
+    gm_finish<NB>(acc, pan, NB, lane, fail, rn2, s2, fb, f);
 }
-
 
 // ---------------------------------------------------------------------------
 // Large tracks (40 < M <= 82, nb <= 16 blocks): the same MFMA elimination on a
@@ -627,6 +682,7 @@ void launch_nb(hipStream_t s, const DevState<float>& st, const Params<float>& pr
     if (capb < nbk) launch_cfg<NB, true>(s, st, prm, fb, list, cnt, Mmax, capb, wpb, wpb * pw);
     else launch_cfg<NB, false>(s, st, prm, fb, list, cnt, Mmax, capb, wpb, wpb * pw);
 }
+
 
 }  // namespace
 
