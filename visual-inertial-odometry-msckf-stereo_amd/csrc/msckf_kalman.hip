@@ -32,7 +32,7 @@ typedef double v4d __attribute__((ext_vector_type(4)));
 
 // ---- stage A: [P_cc P_ci; P_ic P_ii] in index space [cams (Cp) | IMU (24)] ----
 template <typename T, int NT, int TPL>
-__global__ void __launch_bounds__(NT) k_kal_a(DevState<T> st, UpdWs<T> ws) {
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 ? 2 : 1))) k_kal_a(DevState<T> st, UpdWs<T> ws) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int b = blockIdx.x;
     const int* info = ws.info + 4 * b;
@@ -76,7 +76,7 @@ __global__ void __launch_bounds__(NT) k_kal_a(DevState<T> st, UpdWs<T> ws) {
 //     16 x 16 inverses of the diagonal blocks formed once up front.  W^T is
 //     stored row-major over k (coalesced), the layout k_kal_e1 reads.
 template <typename T, int NT, int TPL>
-__global__ void __launch_bounds__(NT) k_kal_c1(DevState<T> st, UpdWs<T> ws) {
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 ? 2 : 1))) k_kal_c1(DevState<T> st, UpdWs<T> ws) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int b = blockIdx.x;
     if (ws.info[4 * b] == 0) return;
@@ -830,6 +830,7 @@ struct RcholCfg { int nt, tpl; };
 
 static bool pick_rchol(int tiles, RcholCfg& c) {
     if (tiles <= 256 * 4) { c = {256, 4}; return true; }
+    if (tiles <= 256 * 6) { c = {256, 6}; return true; }
     if (tiles <= 512 * 4) { c = {512, 4}; return true; }
     return false;
 }
@@ -918,7 +919,8 @@ void launch_kalman_chol(hipStream_t s, const DevState<T>& st, const Params<T>& p
         RcholCfg c;
         pick_rchol(nrow * (nrow + 1) / 2, c);
         const size_t lds = rchol_lds_doubles(nrow) * sizeof(double);
-        if (c.nt == 256) launch_a_cfg<T, 256, 4>(s, st, ws, lds);
+        if (c.nt == 256 && c.tpl == 4) launch_a_cfg<T, 256, 4>(s, st, ws, lds);
+        else if (c.nt == 256) launch_a_cfg<T, 256, 6>(s, st, ws, lds);
         else launch_a_cfg<T, 512, 4>(s, st, ws, lds);
     } else {
         launch_gchol<0, T>(s, st, ws);
@@ -941,7 +943,8 @@ void launch_kalman_chol(hipStream_t s, const DevState<T>& st, const Params<T>& p
         RcholCfg c;
         pick_rchol(nTc * (nTc + 1) / 2, c);
         const size_t lds = rchol_lds_doubles(nTc) * sizeof(double);
-        if (c.nt == 256) launch_c1<T, 256, 4>(s, st, ws, lds);
+        if (c.nt == 256 && c.tpl == 4) launch_c1<T, 256, 4>(s, st, ws, lds);
+        else if (c.nt == 256) launch_c1<T, 256, 6>(s, st, ws, lds);
         else launch_c1<T, 512, 4>(s, st, ws, lds);
         if (Cq <= 16 * 8) launch_c2<T, 7, 2, 8>(s, st, ws);
         else launch_c2<T, 7, 2, 12>(s, st, ws);

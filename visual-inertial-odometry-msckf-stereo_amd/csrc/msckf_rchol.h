@@ -10,8 +10,11 @@ namespace msckf {
 // tl <= ti < nrow, enumerated column-major; tile t lives in thread t % NT,
 // slot t / NT.  Eliminates tile columns 0..nelim-1 (4 pivots per step):
 //   1. owners of the step's tile column dump it to LDS (double-buffered)
-//   2. every thread factors the 4x4 diagonal tile (uniform) and transforms
-//      panel rows (one row per thread): W = A_panel L_d^-T -> LDS + panel()
+//      -- the diagonal tile's owner factors it (L_d and the reciprocal
+//      diagonal to LDS: one fp64 sqrt / division chain per step, not one per
+//      thread)
+//   2. every thread reads L_d and transforms panel rows (one row per thread):
+//      W = A_panel L_d^-T -> LDS + panel()
 //   3. every tile right of the panel takes A -= W_i W_l^T from registers
 // Two barriers per step.  Tiles in columns >= nelim end as the Schur
 // complement and are handed to trail().  In the LDS column buffer each 4-row
@@ -61,8 +64,10 @@ __device__ __forceinline__ bool rchol_core(int nrow, int ncol, int nelim, double
         }
     }
     bool fail = false;
+    double* fac = lds + 2 * RB * nrow;   // [2][16]: the step's diagonal factor (double-buffered)
     for (int tj = 0; tj < nelim; ++tj) {
         double* buf = lds + (tj & 1) * RB * nrow;   // [nrow][RB]: rows 4 t + x at RB t + 4 x
+        double* fj = fac + 16 * (tj & 1);
 #pragma unroll
         for (int s = 0; s < TPL; ++s) {
             if (!ROK(s) || RTL(s) != tj) continue;
@@ -71,20 +76,29 @@ __device__ __forceinline__ bool rchol_core(int nrow, int ncol, int nelim, double
             for (int x = 0; x < 4; ++x)
 #pragma unroll
                 for (int y = 0; y < 4; ++y) dst[4 * x + y] = a[s][x][y];
+            if (RTI(s) == tj) {   // the diagonal tile's owner factors it once for everyone
+                const double l00 = sqrt(a[s][0][0]);
+                const double i00 = 1.0 / l00;
+                const double l10 = a[s][1][0] * i00, l20 = a[s][2][0] * i00, l30 = a[s][3][0] * i00;
+                const double l11 = sqrt(a[s][1][1] - l10 * l10);
+                const double i11 = 1.0 / l11;
+                const double l21 = (a[s][2][1] - l20 * l10) * i11, l31 = (a[s][3][1] - l30 * l10) * i11;
+                const double l22 = sqrt(a[s][2][2] - l20 * l20 - l21 * l21);
+                const double i22 = 1.0 / l22;
+                const double l32 = (a[s][3][2] - l30 * l20 - l31 * l21) * i22;
+                const double l33 = sqrt(a[s][3][3] - l30 * l30 - l31 * l31 - l32 * l32);
+                const double i33 = 1.0 / l33;
+                fj[0] = l00; fj[1] = l10; fj[2] = l20; fj[3] = l30;
+                fj[4] = l11; fj[5] = l21; fj[6] = l31; fj[7] = l22;
+                fj[8] = l32; fj[9] = l33; fj[10] = i00; fj[11] = i11;
+                fj[12] = i22; fj[13] = i33;
+            }
         }
         LDS_BARRIER();
-        const double* dt = buf + RB * tj;
-        const double l00 = sqrt(dt[0]);
-        const double i00 = 1.0 / l00;
-        const double l10 = dt[4] * i00, l20 = dt[8] * i00, l30 = dt[12] * i00;
-        const double l11 = sqrt(dt[5] - l10 * l10);
-        const double i11 = 1.0 / l11;
-        const double l21 = (dt[9] - l20 * l10) * i11, l31 = (dt[13] - l30 * l10) * i11;
-        const double l22 = sqrt(dt[10] - l20 * l20 - l21 * l21);
-        const double i22 = 1.0 / l22;
-        const double l32 = (dt[14] - l30 * l20 - l31 * l21) * i22;
-        const double l33 = sqrt(dt[15] - l30 * l30 - l31 * l31 - l32 * l32);
-        const double i33 = 1.0 / l33;
+        const double l00 = fj[0], l10 = fj[1], l20 = fj[2], l30 = fj[3];
+        const double l11 = fj[4], l21 = fj[5], l31 = fj[6], l22 = fj[7];
+        const double l32 = fj[8], l33 = fj[9], i00 = fj[10], i11 = fj[11];
+        const double i22 = fj[12], i33 = fj[13];
         if (!(l00 > 0.0) || !(l11 > 0.0) || !(l22 > 0.0) || !(l33 > 0.0)) { fail = true; break; }
         for (int r = 4 * tj + 4 + tid; r < 4 * nrow; r += NT) {
             double* row = buf + RB * (r >> 2) + 4 * (r & 3);
@@ -109,16 +123,21 @@ __device__ __forceinline__ bool rchol_core(int nrow, int ncol, int nelim, double
             if (!ROK(s) || RTL(s) <= tj) continue;
             const double* ri = buf + RB * RTI(s);
             const double* rl = buf + RB * RTL(s);
-            double u[4][4], w[4][4];
+            double w[4][4];
 #pragma unroll
             for (int x = 0; x < 4; ++x)
 #pragma unroll
-                for (int c = 0; c < 4; ++c) { u[x][c] = ri[4 * x + c]; w[x][c] = rl[4 * x + c]; }
+                for (int c = 0; c < 4; ++c) w[x][c] = rl[4 * x + c];
 #pragma unroll
-            for (int x = 0; x < 4; ++x)
+            for (int x = 0; x < 4; ++x) {   // one row of u at a time (register budget)
+                double u[4];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) u[c] = ri[4 * x + c];
 #pragma unroll
                 for (int y = 0; y < 4; ++y)
-                    a[s][x][y] -= u[x][0] * w[y][0] + u[x][1] * w[y][1] + u[x][2] * w[y][2] + u[x][3] * w[y][3];
+                    a[s][x][y] -= u[0] * w[y][0] + u[1] * w[y][1] + u[2] * w[y][2] + u[3] * w[y][3];
+                if (TPL > 4) asm volatile("" ::: "memory");
+            }
             asm volatile("" ::: "memory");
         }
     }
@@ -139,6 +158,6 @@ __device__ __forceinline__ bool rchol_core(int nrow, int ncol, int nelim, double
     return !fail;
 }
 
-__host__ __device__ constexpr int rchol_lds_doubles(int nrow) { return 2 * RB * nrow; }
+__host__ __device__ constexpr int rchol_lds_doubles(int nrow) { return 2 * RB * nrow + 32; }
 
 }  // namespace msckf
