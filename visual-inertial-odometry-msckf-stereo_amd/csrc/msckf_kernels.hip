@@ -28,34 +28,40 @@ namespace msckf {
 
 // ===========================================================================
 // IMU propagation (process_model, msckf.py:291-368; jit_utils.py:6-135): one
-// wavefront per listed filter, four filters per 256-thread workgroup, no
-// workgroup barriers.  Filter filters[w] takes samples [smp_off[w],
-// smp_off[w+1]) in order.  The 21x21 recursion lives in the wave's LDS
-// (products: 7 outputs per lane); lane 0 runs the serial state prediction
-// (RK4, quirk Q1) and the Phi edits.  The IMU x cam cross block is updated
-// once with the product Phi_n ... Phi_1 (the per-sample full-P symmetrisation
-// of msckf.py:362-363 is a no-op on the cam x cam block and only re-rounds
-// the cross block).
+// 256-thread workgroup per listed filter; filter filters[w] takes samples
+// [smp_off[w], smp_off[w+1]) in order.  Per sample, between workgroup barriers:
+//   S0  wave 3 lane 0: the sample, bias-corrected rates, R (current q)
+//   S1  waves 0-2: F dt and G; then rows of F^2, F^3 and Phi (three rows per
+//       pass, 21 lanes per row: a row's products stay inside one wave) while
+//       wave 3 lane 0 runs the serial state prediction (RK4, quirk Q1) and the
+//       Phi edit terms (msckf.py:329-344)
+//   S2  the Phi edits
+//   S3  all waves, rows of A = Phi P11, Phi G Qc, (Phi G Qc) G^T, A Phi^T, the
+//       Q term and the cumulative Phi (jit_utils.py:130-135)
+//   S4  P11 = (A + A^T) / 2
+// The IMU x cam cross block is updated once with the product Phi_n ... Phi_1
+// (the per-sample full-P symmetrisation of msckf.py:362-363 is a no-op on the
+// cam x cam block and only re-rounds the cross block).  Every dot product runs
+// in the reference order (sum over k ascending).
 // ===========================================================================
-template <typename T>
-__device__ __forceinline__ void mm21w(const T* A, const T* B, T* C, int lane) {   // C = A B (21x21), one wave
-    for (int e = lane; e < 441; e += 64) {
-        const int i = e / 21, j = e - 21 * (e / 21);
-        T s = 0;
-#pragma unroll 7
-        for (int k = 0; k < 21; ++k) s += A[i * 21 + k] * B[k * 21 + j];
-        C[e] = s;
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-}
-
 template <typename T>
 __device__ __forceinline__ T skew_el(const T* w, int r, int c) {   // [w]x[r][c]
     return r == c ? T(0)
                   : (r == 0 ? (c == 1 ? -w[2] : w[1]) : (r == 1 ? (c == 0 ? w[2] : -w[0]) : (c == 0 ? -w[1] : w[0])));
 }
 
-constexpr int PROP_LDS = 7 * 441 + 2 * 252 + 9 + 3 + 3 + 1 + IMU_STRIDE;   // T per wave
+constexpr int PRS = 24;                 // LDS row stride of the 21-wide matrices (16-byte aligned rows)
+constexpr int PROP_MAT = 21 * PRS;
+// F, Phi, F^2, P11, P11', A, cum^T (x2), f rows; G, Phi G Qc (21 x 12); scalars; IMU record
+constexpr int PROP_LDS = 9 * PROP_MAT + 2 * 252 + 64 + IMU_STRIDE;   // T per workgroup
+enum PropScalar { PS_R = 0, PS_GYRO = 9, PS_ACC = 12, PS_DT = 15, PS_PHI00 = 16, PS_U = 25, PS_S = 28, PS_W1 = 31,
+                  PS_W2 = 34 };
+
+template <typename T>
+__device__ __forceinline__ void prop_row(const T* src, T (&v)[21]) {
+#pragma unroll
+    for (int k = 0; k < 21; ++k) v[k] = src[k];
+}
 
 template <typename T>
 __global__ void __launch_bounds__(256) k_propagate(DevState<T> st, Params<T> prm, int nfilt,
@@ -63,80 +69,101 @@ __global__ void __launch_bounds__(256) k_propagate(DevState<T> st, Params<T> prm
                                                    const int* __restrict__ smp_off,
                                                    const T* __restrict__ samples_all) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int w = blockIdx.x * 4 + wv;
-    if (w >= nfilt) return;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int w = blockIdx.x;
     const int b = filters[w];
     const int n = smp_off[w + 1] - smp_off[w];
     const T* samples = samples_all + 7 * (size_t)smp_off[w];
     if (n <= 0) return;
-    T* F = reinterpret_cast<T*>(smem_raw) + (size_t)wv * PROP_LDS;   // Fdt
-    T* Phi = F + 441;
-    T* Fdt2 = Phi + 441;
-    T* Fdt3 = Fdt2 + 441;
-    T* A = Fdt3 + 441;
-    T* P11 = A + 441;
-    T* PhiT = P11 + 441;                 // cumulative Phi
-    T* G = PhiT + 441;                   // 21 x 12
-    T* PG = G + 252;
-    T* s_R = PG + 252;
-    T* s_gyro = s_R + 9;
-    T* s_acc = s_gyro + 3;
-    T* s_dt = s_acc + 3;
-    T* s_imu = s_dt + 1;
+    T* F = reinterpret_cast<T*>(smem_raw);   // F dt
+    T* Phi = F + PROP_MAT;
+    T* F2 = Phi + PROP_MAT;
+    T* P11 = F2 + PROP_MAT;
+    T* P11n = P11 + PROP_MAT;
+    T* A = P11n + PROP_MAT;
+    T* cumT = A + PROP_MAT;                  // [2]: (Phi_k ... Phi_1)^T, ping-pong
+    T* fr = cumT + 2 * PROP_MAT;             // rows of (Phi G Qc) G^T
+    T* G = fr + PROP_MAT;                    // 21 x 12
+    T* PG = G + 252;                         // Phi G Qc
+    T* sc = PG + 252;                        // PropScalar
+    T* s_imu = sc + 64;
     T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
     const int ld = st.Dmax;
     T* imu = st.imu + (size_t)b * IMU_STRIDE;
     const int D = 21 + 6 * st.ncams[b];
-    for (int e = lane; e < IMU_STRIDE; e += 64) s_imu[e] = imu[e];
-    for (int e = lane; e < 441; e += 64) {
-        P11[e] = P[(e / 21) * ld + e % 21];
-        PhiT[e] = (e / 21 == e % 21) ? T(1) : T(0);
+    for (int e = tid; e < IMU_STRIDE; e += 256) s_imu[e] = imu[e];
+    for (int e = tid; e < 441; e += 256) {
+        const int i = e / 21, j = e - 21 * i;
+        P11[i * PRS + j] = P[i * ld + j];
+        cumT[i * PRS + j] = i == j ? T(1) : T(0);
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int rr = lane / 21, jc = lane - 21 * rr;   // row of the 3-row group, column (lane 63 idle)
+    int cur = 0;
     for (int k = 0; k < n; ++k) {
-        const T* smp = samples + 7 * k;
-        if (lane == 0) {
-            s_dt[0] = smp[0];
+        // ---- S0 ----
+        if (tid == 192) {
+            const T* smp = samples + 7 * k;
+            sc[PS_DT] = smp[0];
             for (int i = 0; i < 3; ++i) {
-                s_gyro[i] = smp[1 + i] - s_imu[I_BG + i];
-                s_acc[i] = smp[4 + i] - s_imu[I_BA + i];
+                sc[PS_GYRO + i] = smp[1 + i] - s_imu[I_BG + i];
+                sc[PS_ACC + i] = smp[4 + i] - s_imu[I_BA + i];
             }
-            quat_to_rot(s_imu + I_Q, s_R);
+            quat_to_rot(s_imu + I_Q, sc + PS_R);
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        const T dt = s_dt[0];
-        // F dt, G  (jit_utils.py:25-34); R = R_w_i
-        for (int e = lane; e < 441; e += 64) {
-            const int i = e / 21, j = e - 21 * (e / 21);
-            const int bi = i / 3, bj = j / 3, r = i - 3 * bi, c = j - 3 * bj;
-            T f = 0;
-            if (bi == 0 && bj == 0) f = -skew_el(s_gyro, r, c);
-            else if (bi == 0 && bj == 1) f = r == c ? T(-1) : T(0);
-            else if (bi == 2 && bj == 0)   // -R^T [a]x
-                f = -s_R[r] * skew_el(s_acc, 0, c) + -s_R[3 + r] * skew_el(s_acc, 1, c) + -s_R[6 + r] * skew_el(s_acc, 2, c);
-            else if (bi == 2 && bj == 3) f = -s_R[3 * c + r];
-            else if (bi == 4 && bj == 2) f = r == c ? T(1) : T(0);
-            F[e] = f * dt;
+        __syncthreads();
+        const T dt = sc[PS_DT];
+        // ---- S1: F dt, G (jit_utils.py:25-34); R = R_w_i ----
+        if (wv < 3) {
+            const T* s_R = sc + PS_R;
+            const T* s_gyro = sc + PS_GYRO;
+            const T* s_acc = sc + PS_ACC;
+            for (int e = tid; e < 441; e += 192) {
+                const int i = e / 21, j = e - 21 * (e / 21);
+                const int bi = i / 3, bj = j / 3, r = i - 3 * bi, c = j - 3 * bj;
+                T f = 0;
+                if (bi == 0 && bj == 0) f = -skew_el(s_gyro, r, c);
+                else if (bi == 0 && bj == 1) f = r == c ? T(-1) : T(0);
+                else if (bi == 2 && bj == 0)   // -R^T [a]x
+                    f = -s_R[r] * skew_el(s_acc, 0, c) + -s_R[3 + r] * skew_el(s_acc, 1, c) + -s_R[6 + r] * skew_el(s_acc, 2, c);
+                else if (bi == 2 && bj == 3) f = -s_R[3 * c + r];
+                else if (bi == 4 && bj == 2) f = r == c ? T(1) : T(0);
+                F[i * PRS + j] = f * dt;
+            }
+            for (int e = tid; e < 252; e += 192) {
+                const int i = e / 12, j = e - 12 * (e / 12);
+                const int bi = i / 3, bj = j / 3, r = i - 3 * bi, c = j - 3 * bj;
+                T g = 0;
+                if (bi == bj && (bi == 0)) g = r == c ? T(-1) : T(0);
+                else if (bi == bj && (bi == 1 || bi == 3)) g = r == c ? T(1) : T(0);
+                else if (bi == 2 && bj == 2) g = -s_R[3 * c + r];
+                G[e] = g;
+            }
         }
-        for (int e = lane; e < 252; e += 64) {
-            const int i = e / 12, j = e - 12 * (e / 12);
-            const int bi = i / 3, bj = j / 3, r = i - 3 * bi, c = j - 3 * bj;
-            T g = 0;
-            if (bi == bj && (bi == 0)) g = r == c ? T(-1) : T(0);
-            else if (bi == bj && (bi == 1 || bi == 3)) g = r == c ? T(1) : T(0);
-            else if (bi == 2 && bj == 2) g = -s_R[3 * c + r];
-            G[e] = g;
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        mm21w(F, F, Fdt2, lane);
-        mm21w(Fdt2, F, Fdt3, lane);
-        for (int e = lane; e < 441; e += 64) {
-            const T id = (e / 21 == e % 21) ? T(1) : T(0);
-            Phi[e] = id + F[e] + Fdt2[e] / T(2) + Fdt3[e] / T(6);
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (lane == 0) {
+        __syncthreads();
+        if (wv < 3) {   // rows 7 wv .. 7 wv + 6 of F^2, F^3, Phi
+            for (int p = 0; p < 3; ++p) {
+                if (rr >= 3 || 3 * p + rr >= 7) continue;
+                const int i = 7 * wv + 3 * p + rr;
+                T fi[21];
+                prop_row(F + i * PRS, fi);
+                T s2 = 0;
+#pragma unroll
+                for (int q = 0; q < 21; ++q) s2 += fi[q] * F[q * PRS + jc];
+                F2[i * PRS + jc] = s2;
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the row is this wave's: visible to its lanes
+                T f2i[21];
+                prop_row(F2 + i * PRS, f2i);
+                T s3 = 0;
+#pragma unroll
+                for (int q = 0; q < 21; ++q) s3 += f2i[q] * F[q * PRS + jc];
+                const T id = i == jc ? T(1) : T(0);
+                Phi[i * PRS + jc] = id + F[i * PRS + jc] + s2 / T(2) + s3 / T(6);
+            }
+        } else if (lane == 0) {
+            const T* s_gyro = sc + PS_GYRO;
+            const T* s_acc = sc + PS_ACC;
             // ---- _predict_new_state (jit_utils.py:46-128), quirk Q1 ----
             T* q = s_imu + I_Q;
             T* v = s_imu + I_V;
@@ -226,19 +253,16 @@ __global__ void __launch_bounds__(256) k_propagate(DevState<T> st, Params<T> prm
             }
             for (int i = 0; i < 4; ++i) q[i] = dq[i] / nn;
             for (int i = 0; i < 3; ++i) { v[i] = vn[i]; p[i] = pn[i]; }
-            // ---- Phi edits (msckf.py:329-344) ----
-            T Rkk1[9], Rq[9], Phi00[9];
+            // ---- Phi edit terms (msckf.py:329-344), applied in S2 ----
+            T Rkk1[9], Rq[9];
             quat_to_rot(s_imu + I_QN, Rkk1);
             quat_to_rot(q, Rq);
             for (int i = 0; i < 3; ++i)
                 for (int j = 0; j < 3; ++j)
-                    Phi00[3 * i + j] = Rq[3 * i] * Rkk1[3 * j] + Rq[3 * i + 1] * Rkk1[3 * j + 1] + Rq[3 * i + 2] * Rkk1[3 * j + 2];
-            for (int i = 0; i < 3; ++i)
-                for (int j = 0; j < 3; ++j) Phi[21 * i + j] = Phi00[3 * i + j];
+                    sc[PS_PHI00 + 3 * i + j] = Rq[3 * i] * Rkk1[3 * j] + Rq[3 * i + 1] * Rkk1[3 * j + 1] + Rq[3 * i + 2] * Rkk1[3 * j + 2];
             T u[3];
             mat3_vec(Rkk1, g, u);
             T uu = u[0] * u[0] + u[1] * u[1] + u[2] * u[2];
-            T s[3] = {u[0] / uu, u[1] / uu, u[2] / uu};
             T dv[3] = {v_null[0] - v[0], v_null[1] - v[1], v_null[2] - v[2]};
             T Sk[9], w1[3], w2[3];
             skew3(dv, Sk);
@@ -247,69 +271,94 @@ __global__ void __launch_bounds__(256) k_propagate(DevState<T> st, Params<T> prm
             for (int i = 0; i < 3; ++i) dp[i] = dt * v_null[i] + p_null[i] - p[i];
             skew3(dp, Sk);
             mat3_vec(Sk, g, w2);
-            for (int blk = 0; blk < 2; ++blk) {
-                int r0 = blk == 0 ? 6 : 12;
-                const T* wv = blk == 0 ? w1 : w2;
-                T A1[9];
-                for (int i = 0; i < 3; ++i)
-                    for (int j = 0; j < 3; ++j) A1[3 * i + j] = Phi[21 * (r0 + i) + j];
-                for (int i = 0; i < 3; ++i) {
-                    T au = A1[3 * i] * u[0] + A1[3 * i + 1] * u[1] + A1[3 * i + 2] * u[2];
-                    T c = au - wv[i];
-                    for (int j = 0; j < 3; ++j) Phi[21 * (r0 + i) + j] = A1[3 * i + j] - c * s[j];
-                }
+            for (int i = 0; i < 3; ++i) {
+                sc[PS_U + i] = u[i];
+                sc[PS_S + i] = u[i] / uu;
+                sc[PS_W1 + i] = w1[i];
+                sc[PS_W2 + i] = w2[i];
             }
             for (int i = 0; i < 4; ++i) s_imu[I_QN + i] = q[i];
             for (int i = 0; i < 3; ++i) { s_imu[I_VN + i] = v[i]; s_imu[I_PN + i] = p[i]; }
             s_imu[I_ALIAS] = T(1);
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        // ---- Q = Phi G Qc G^T Phi^T dt ; P11 = Phi P11 Phi^T + Q (jit_utils.py:130-135)
-        for (int e = lane; e < 252; e += 64) {
-            const int i = e / 12, j = e - 12 * (e / 12);
-            T sacc = 0;
-            for (int k2 = 0; k2 < 21; ++k2) sacc += Phi[i * 21 + k2] * G[k2 * 12 + j];
-            const T qc = j < 3 ? prm.qc_gyro : (j < 6 ? prm.qc_gbias : (j < 9 ? prm.qc_acc : prm.qc_abias));
-            PG[e] = sacc * qc;
+        __syncthreads();
+        // ---- S2: Phi edits ----
+        if (tid < 9) {
+            Phi[(tid / 3) * PRS + tid % 3] = sc[PS_PHI00 + tid];
+        } else if (tid < 15) {   // rows 6..8 and 12..14, columns 0..2
+            const int q = tid - 9, blk = q / 3, i = q - 3 * blk, r = (blk == 0 ? 6 : 12) + i;
+            const T* wvv = sc + (blk == 0 ? PS_W1 : PS_W2);
+            T a1[3] = {Phi[r * PRS], Phi[r * PRS + 1], Phi[r * PRS + 2]};
+            const T au = a1[0] * sc[PS_U] + a1[1] * sc[PS_U + 1] + a1[2] * sc[PS_U + 2];
+            const T c = au - wvv[i];
+            for (int j = 0; j < 3; ++j) Phi[r * PRS + j] = a1[j] - c * sc[PS_S + j];
         }
-        mm21w(Phi, P11, A, lane);   // A = Phi P11 (the mm's waitcnt also covers PG)
-        for (int e = lane; e < 441; e += 64) {   // Fdt2 = (Phi G Qc) G^T ; Fdt3 = A Phi^T
-            const int i = e / 21, j = e - 21 * (e / 21);
-            T s1 = 0, s2 = 0;
-            for (int k2 = 0; k2 < 12; ++k2) s1 += PG[i * 12 + k2] * G[j * 12 + k2];
-#pragma unroll 7
-            for (int k2 = 0; k2 < 21; ++k2) s2 += A[i * 21 + k2] * Phi[j * 21 + k2];
-            Fdt2[e] = s1;
-            Fdt3[e] = s2;
+        __syncthreads();
+        // ---- S3: rows 3 g .. 3 g + 2 for g = wv, wv + 4 ----
+        const T* cT = cumT + cur * PROP_MAT;
+        T* cTn = cumT + (cur ^ 1) * PROP_MAT;
+        for (int gi = 0; gi < 2; ++gi) {
+            const int g = wv + 4 * gi;
+            if (g >= 7 || rr >= 3) continue;
+            const int i = 3 * g + rr, j = jc;
+            T ph[21], row[21];
+            prop_row(Phi + i * PRS, ph);
+            prop_row(P11 + j * PRS, row);   // P11 is symmetric: column j = row j
+            T a = 0;
+#pragma unroll
+            for (int q = 0; q < 21; ++q) a += ph[q] * row[q];
+            A[i * PRS + j] = a;
+            prop_row(cT + j * PRS, row);     // column j of the cumulative Phi
+            T cn = 0;
+#pragma unroll
+            for (int q = 0; q < 21; ++q) cn += ph[q] * row[q];
+            cTn[j * PRS + i] = cn;
+            if (j < 12) {
+                T pg = 0;
+#pragma unroll
+                for (int q = 0; q < 21; ++q) pg += ph[q] * G[q * 12 + j];
+                const T qc = j < 3 ? prm.qc_gyro : (j < 6 ? prm.qc_gbias : (j < 9 ? prm.qc_acc : prm.qc_abias));
+                PG[i * 12 + j] = pg * qc;
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            prop_row(A + i * PRS, ph);
+            prop_row(Phi + j * PRS, row);
+            T t = 0;
+#pragma unroll
+            for (int q = 0; q < 21; ++q) t += ph[q] * row[q];          // (A Phi^T)[i][j]
+            T f = 0;
+#pragma unroll
+            for (int q = 0; q < 12; ++q) f += PG[i * 12 + q] * G[j * 12 + q];   // (Phi G Qc G^T)[i][j]
+            fr[i * PRS + j] = f;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            prop_row(fr + i * PRS, ph);
+            T qv = 0;
+#pragma unroll
+            for (int q = 0; q < 21; ++q) qv += ph[q] * row[q];         // (... Phi^T)[i][j]
+            P11n[i * PRS + j] = t + qv * dt;
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        for (int e = lane; e < 441; e += 64) {   // Q = Bm Phi^T dt ; P11' = A Phi^T + Q (into A)
-            const int i = e / 21, j = e - 21 * (e / 21);
-            T s1 = 0;
-#pragma unroll 7
-            for (int k2 = 0; k2 < 21; ++k2) s1 += Fdt2[i * 21 + k2] * Phi[j * 21 + k2];
-            A[e] = Fdt3[e] + s1 * dt;
+        __syncthreads();
+        // ---- S4 ----
+        for (int e = tid; e < 441; e += 256) {
+            const int i = e / 21, j = e - 21 * i;
+            P11[i * PRS + j] = (P11n[i * PRS + j] + P11n[j * PRS + i]) / T(2);
         }
-        mm21w(Phi, PhiT, Fdt2, lane);   // cumulative Phi (into Fdt2)
-        for (int e = lane; e < 441; e += 64) {
-            const int i = e / 21, j = e - 21 * (e / 21);
-            P11[e] = (A[e] + A[j * 21 + i]) / T(2);
-            PhiT[e] = Fdt2[e];
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        cur ^= 1;
+        __syncthreads();
     }
     // write back P11, IMU record; cross blocks with the cumulative Phi
-    for (int e = lane; e < 441; e += 64) P[(e / 21) * ld + e % 21] = P11[e];
-    for (int e = lane; e < IMU_STRIDE; e += 64) imu[e] = s_imu[e];
-    for (int j = 21 + lane; j < D; j += 64) {
+    const T* cT = cumT + cur * PROP_MAT;
+    for (int e = tid; e < 441; e += 256) P[(e / 21) * ld + e % 21] = P11[(e / 21) * PRS + e % 21];
+    for (int e = tid; e < IMU_STRIDE; e += 256) imu[e] = s_imu[e];
+    for (int j = 21 + tid; j < D; j += 256) {
         T col[21];
 #pragma unroll
         for (int m = 0; m < 21; ++m) col[m] = P[m * ld + j];
-#pragma unroll 1
-        for (int i = 0; i < 21; ++i) {   // not unrolled: keeps the 441 Phi entries out of registers
+#pragma unroll 3
+        for (int i = 0; i < 21; ++i) {
             T sacc = 0;
 #pragma unroll
-            for (int m = 0; m < 21; ++m) sacc += PhiT[i * 21 + m] * col[m];
+            for (int m = 0; m < 21; ++m) sacc += cT[m * PRS + i] * col[m];
             P[i * ld + j] = sacc;
             P[(size_t)j * ld + i] = sacc;
         }
@@ -1976,13 +2025,13 @@ template <typename T>
 void launch_propagate(hipStream_t s, const DevState<T>& st, const Params<T>& prm, int nfilt, const int* filters,
                       const int* smp_off, const T* samples) {
     if (nfilt <= 0) return;
-    const size_t lds = 4 * (size_t)PROP_LDS * sizeof(T);
+    const size_t lds = (size_t)PROP_LDS * sizeof(T);
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)k_propagate<T>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr = true;
     }
-    hipLaunchKernelGGL(k_propagate<T>, dim3((nfilt + 3) / 4), dim3(256), lds, s, st, prm, nfilt, filters, smp_off,
+    hipLaunchKernelGGL(k_propagate<T>, dim3(nfilt), dim3(256), lds, s, st, prm, nfilt, filters, smp_off,
                        samples);
 }
 template <typename T>
