@@ -15,10 +15,10 @@ from msckf_amd import _lib
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def header_symbols():
-    src = open(os.path.join(ROOT, "include", "msckf_hip.h")).read()
+def header_symbols(header="msckf_hip.h", prefix="msckf_"):
+    src = open(os.path.join(ROOT, "include", header)).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(msckf_[a-z_]+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(%s[a-z_]+)\s*\(" % prefix, src)))
 
 
 def test_library_exports_every_declared_symbol():
@@ -33,6 +33,18 @@ def test_library_exports_every_declared_symbol():
 
 def test_binding_matches_header():
     assert sorted(_lib.EXPORTED) == header_symbols()
+
+
+def test_frontend_exports_and_binding():
+    """include/msckf_frontend.h (GPU stereo front-end) is exported by the same
+    library and typed one to one by the binding."""
+    syms = header_symbols("msckf_frontend.h", "mfe_")
+    assert sorted(_lib.FRONTEND_EXPORTED) == syms and len(syms) == 8
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libmsckf_hip.so not built")
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    for s in syms:
+        assert hasattr(lib, s), s
 
 
 def test_load_library_types_functions():

@@ -80,6 +80,20 @@ _SIGS = {
 
 EXPORTED = tuple(_SIGS)
 
+_F = C.POINTER(C.c_float)
+# GPU stereo front-end (include/msckf_frontend.h), same library
+FRONTEND_SIGS = {
+    "mfe_create": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(_P)]),
+    "mfe_destroy": (C.c_int, [_P]),
+    "mfe_last_error": (C.c_char_p, []),
+    "mfe_upload": (C.c_int, [_P, C.c_int, _U8]),
+    "mfe_fast": (C.c_int, [_P, C.c_int, C.c_int, _U8, C.c_int, _F, _F, _I]),
+    "mfe_lk": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, _F, _F, _U8, C.c_int, C.c_int, C.c_int, C.c_double]),
+    "mfe_undistort": (C.c_int, [_P, C.c_int, _D, _D, _D, C.c_int, _D, _D, _D]),
+    "mfe_distort": (C.c_int, [_P, C.c_int, _D, _D, _D, C.c_int, _D]),
+}
+FRONTEND_EXPORTED = tuple(FRONTEND_SIGS)
+
 
 def load_library(path: str = LIB_PATH):
     """Load and type the shared library (no device work)."""
@@ -91,7 +105,7 @@ def load_library(path: str = LIB_PATH):
             raise MsckfError("HIP extension %s is missing -- build it with `make` "
                              "(or __graft_entry__.build()); there is no CPU fallback" % path)
         lib = C.CDLL(path)
-        for name, (res, args) in _SIGS.items():
+        for name, (res, args) in list(_SIGS.items()) + list(FRONTEND_SIGS.items()):
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
