@@ -71,7 +71,7 @@ struct msckf_ctx {
     DBuf<unsigned char> Hthin, dx, Lc, Vi, Sii, G, Tm, W, Wk;
     DBuf<int> info, afail;
     // feature batch
-    int nf = 0, maxM = 0;
+    int nf = 0, maxM = 0, max_nf = 0, max_obs = 0;   // per filter, of the loaded batch
     std::vector<int> h_feat_off;
     DBuf<int> feat_filter, feat_off, obs_off, obs_cam, row_off, gate_list;
     GateClasses gc;
@@ -329,6 +329,11 @@ int load_features(msckf_ctx* c, int nf, const int32_t* feat_off, int single_filt
     HIPC(hipStreamSynchronize(s));
     c->nf = nf;
     c->maxM = maxM;
+    c->max_nf = c->max_obs = 0;
+    for (int b = 0; b < c->B; ++b) {
+        c->max_nf = std::max(c->max_nf, h_off[b + 1] - h_off[b]);
+        if (h_off[b + 1] > h_off[b]) c->max_obs = std::max(c->max_obs, obs_off[h_off[b + 1]] - obs_off[h_off[b]]);
+    }
     c->h_feat_off = h_off;
     return 0;
 }
@@ -355,7 +360,7 @@ int run_update_chain(msckf_ctx* c, int row_cap, bool triangulate) {
     launch_select<T>(s, st, fb, ws, row_cap);
     c->timer.end(s);
     c->timer.begin(s, "compress");
-    launch_compress<T>(s, st, fb, ws);
+    launch_compress<T>(s, st, fb, ws, c->max_nf, c->max_obs);
     c->timer.end(s);
     launch_kalman<T>(s, st, prm, ws, &c->timer);
     HIPC(hipGetLastError());

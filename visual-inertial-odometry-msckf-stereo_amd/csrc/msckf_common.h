@@ -39,7 +39,11 @@ constexpr int OBS_HX = 0, OBS_V = 24, OBS_W = 36, OBS_QR = 54, OBS_R = 58, OBS_H
 // so that the projected block H0 = (Q^T Hx)[3:] satisfies
 //   H0^T H0 = blockdiag_i(Hx_i^T Hx_i) - G^T G,   H0^T r0 = sum_i UB_i.
 //   CAM  1   the observation's cam slot (exact in fp64)
-constexpr int OBG_G = 0, OBG_DS = 18, OBG_UB = 39, OBG_CAM = 45, OBG_STRIDE = 48;
+// Stride 46 doubles (368 B: 16-byte chunks for global_load_lds; 92 dwords, so
+// eight consecutive records start on eight different LDS bank quads -- a
+// 48-double stride put them on two and made k_info's record reads 4-way
+// bank-conflicted).
+constexpr int OBG_G = 0, OBG_DS = 18, OBG_UB = 39, OBG_CAM = 45, OBG_STRIDE = 46;
 
 template <typename T>
 struct Params {

@@ -1831,7 +1831,8 @@ constexpr int INFO_FB_MAX = 5;
 __host__ __device__ constexpr int info_slot_doubles(int Nmax) { return (Nmax * OBG_STRIDE + 127) / 128 * 128; }
 
 template <typename T, int BPT, int NT>
-__global__ void __launch_bounds__(NT) k_info(DevState<T> st, FeatBatch<T> fb, UpdWs<T> ws, int fbn) {
+__global__ void __launch_bounds__(NT) k_info(DevState<T> st, FeatBatch<T> fb, UpdWs<T> ws, int fbn, int maxnf,
+                                             int maxobs) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int b = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwave = NT >> 6;
@@ -1845,6 +1846,15 @@ __global__ void __launch_bounds__(NT) k_info(DevState<T> st, FeatBatch<T> fb, Up
     double* rec = reinterpret_cast<double*>(smem_raw);                      // [2][FB][SLOT]
     unsigned long long* mask = reinterpret_cast<unsigned long long*>(rec + (size_t)2 * INFO_FB * SLOT);   // [2][FB][2]
     int* pos = reinterpret_cast<int*>(mask + 4 * INFO_FB);                   // [2][FB][Nmax] cam -> record
+    // filter-resident feature metadata (maxobs > 0): every feature's cam mask,
+    // first record and record count (0 if not included), and the filter's
+    // obs_cam -- read once up front, so that staging a batch involves no
+    // dependent global loads (include -> obs_off -> obs_cam was three round
+    // trips on the critical path of every batch)
+    unsigned long long* fmask = reinterpret_cast<unsigned long long*>(pos + ((2 * INFO_FB * Nmax + 1) & ~1));
+    int* fo0 = reinterpret_cast<int*>(fmask + 2 * maxnf);
+    int* fM = fo0 + maxnf;
+    int* sobs = fM + maxnf;
 
     double a[BPT][6][6], bv[BPT][6];
     int I[BPT], J[BPT];
@@ -1877,13 +1887,45 @@ __global__ void __launch_bounds__(NT) k_info(DevState<T> st, FeatBatch<T> fb, Up
     // its M records (global_load_lds, 16 B per lane), a cam -> record table
     // and a cam bitmask.
     const int fbeg = fb.feat_off[b], fend = fb.feat_off[b + 1];
+    const int obeg = fb.obs_off[fbeg];
+    const bool pre = maxobs > 0;   // uniform
+    if (pre) {
+        const int nobs = fb.obs_off[fend] - obeg;
+        for (int e = tid; e < nobs; e += NT) sobs[e] = fb.obs_cam[obeg + e];
+        for (int f = fbeg + tid; f < fend; f += NT) {
+            const bool in = fb.include[f] != 0;
+            fo0[f - fbeg] = fb.obs_off[f];
+            fM[f - fbeg] = in ? fb.obs_off[f + 1] - fb.obs_off[f] : 0;
+        }
+        __syncthreads();
+        for (int f = tid; f < fend - fbeg; f += NT) {   // one thread per feature: its cam mask
+            unsigned long long m0 = 0, m1 = 0;
+            for (int o = 0; o < fM[f]; ++o) {
+                const int cam = sobs[fo0[f] - obeg + o];
+                if (cam < 64) m0 |= 1ull << cam;
+                else m1 |= 1ull << (cam - 64);
+            }
+            fmask[2 * f] = m0;
+            fmask[2 * f + 1] = m1;
+        }
+        __syncthreads();
+    }
     auto stage = [&](int f0, int buf) {
         for (int s = wave; s < INFO_FB; s += nwave) {
             const int f = f0 + s;
             int* ps = pos + (buf * INFO_FB + s) * Nmax;
             unsigned long long mk[2] = {0, 0};
             int o0 = 0, M = 0;
-            if (f < fend && fb.include[f]) {
+            if (pre) {
+                if (f < fend) {
+                    o0 = fo0[f - fbeg];
+                    M = fM[f - fbeg];
+                    for (int o = lane; o < M; o += 64) ps[sobs[o0 - obeg + o]] = o;
+                    if (lane < 2) mask[(buf * INFO_FB + s) * 2 + lane] = M ? fmask[2 * (f - fbeg) + lane] : 0ull;
+                } else if (lane < 2) {
+                    mask[(buf * INFO_FB + s) * 2 + lane] = 0ull;
+                }
+            } else if (f < fend && fb.include[f]) {
                 o0 = fb.obs_off[f];
                 M = fb.obs_off[f + 1] - o0;
                 for (int o = lane; o < M; o += 64) {
@@ -1893,7 +1935,7 @@ __global__ void __launch_bounds__(NT) k_info(DevState<T> st, FeatBatch<T> fb, Up
                 }
             }
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
+            for (int h = 0; h < 2 && !pre; ++h) {
                 unsigned lo = (unsigned)mk[h], hi = (unsigned)(mk[h] >> 32);
 #pragma unroll
                 for (int w = 32; w >= 1; w >>= 1) {
@@ -2214,13 +2256,17 @@ void launch_select(hipStream_t s, const DevState<T>& st, const FeatBatch<T>& fb,
 }
 
 template <typename T, int NT>
-static void launch_info_cfg(hipStream_t s, const DevState<T>& st, const FeatBatch<T>& fb, const UpdWs<T>& ws) {
+static void launch_info_cfg(hipStream_t s, const DevState<T>& st, const FeatBatch<T>& fb, const UpdWs<T>& ws,
+                            int maxnf, int maxobs) {
     // features staged per batch: INFO_FB_MAX, or as many as the double-buffered slots fit in LDS
     const size_t per = ((size_t)2 * info_slot_doubles(st.Nmax)) * sizeof(double) + 4 * sizeof(unsigned long long) +
                        2 * st.Nmax * sizeof(int);
     int fbn = INFO_FB_MAX;
-    while (fbn > 1 && fbn * per > 160 * 1024) --fbn;
-    const size_t lds = fbn * per;
+    while (fbn > 1 && fbn * per + 8 > 160 * 1024) --fbn;
+    // filter-resident metadata when it fits beside the staged batches
+    const size_t meta = (size_t)maxnf * (2 * sizeof(unsigned long long) + 2 * sizeof(int)) + (size_t)maxobs * sizeof(int);
+    const bool pre = maxobs > 0 && fbn * per + 8 + meta <= 160 * 1024;
+    const size_t lds = fbn * per + 8 + (pre ? meta : 0);
     const int TS = (st.Nmax + 7) / 8, ntl = TS * (TS + 1) / 2;
     const int parts = (ntl + (NT / 64) - 1) / (NT / 64);
     static size_t attr = 64 * 1024;   // dynamic LDS granted so far (default 64 KB)
@@ -2228,17 +2274,19 @@ static void launch_info_cfg(hipStream_t s, const DevState<T>& st, const FeatBatc
         (void)hipFuncSetAttribute((const void*)k_info<T, 1, NT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         attr = lds;
     }
-    hipLaunchKernelGGL((k_info<T, 1, NT>), dim3(st.B, parts), dim3(NT), lds, s, st, fb, ws, fbn);
+    hipLaunchKernelGGL((k_info<T, 1, NT>), dim3(st.B, parts), dim3(NT), lds, s, st, fb, ws, fbn, pre ? maxnf : 0,
+                       pre ? maxobs : 0);
 }
 
 template <typename T>
-void launch_compress(hipStream_t s, const DevState<T>& st, const FeatBatch<T>& fb, const UpdWs<T>& ws) {
+void launch_compress(hipStream_t s, const DevState<T>& st, const FeatBatch<T>& fb, const UpdWs<T>& ws, int maxnf,
+                     int maxobs) {
     // one wave per 8 x 8 tile of cam pairs
     const int TS = (st.Nmax + 7) / 8, ntl = TS * (TS + 1) / 2;
-    if (ntl <= 4) launch_info_cfg<T, 256>(s, st, fb, ws);
-    else if (ntl <= 8) launch_info_cfg<T, 512>(s, st, fb, ws);
-    else if (ntl <= 10) launch_info_cfg<T, 640>(s, st, fb, ws);
-    else launch_info_cfg<T, 1024>(s, st, fb, ws);   // > 10 tiles: several workgroups per filter
+    if (ntl <= 4) launch_info_cfg<T, 256>(s, st, fb, ws, maxnf, maxobs);
+    else if (ntl <= 8) launch_info_cfg<T, 512>(s, st, fb, ws, maxnf, maxobs);
+    else if (ntl <= 10) launch_info_cfg<T, 640>(s, st, fb, ws, maxnf, maxobs);
+    else launch_info_cfg<T, 1024>(s, st, fb, ws, maxnf, maxobs);   // > 10 tiles: several workgroups per filter
 }
 
 template <typename T>
@@ -2262,7 +2310,7 @@ void launch_kalman(hipStream_t s, const DevState<T>& st, const Params<T>& prm, c
     template void launch_feature<T>(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&, const SegClasses&); \
     template void launch_gate<T>(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&, const GateClasses&); \
     template void launch_select<T>(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const UpdWs<T>&, int); \
-    template void launch_compress<T>(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const UpdWs<T>&); \
+    template void launch_compress<T>(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const UpdWs<T>&, int, int); \
     template void launch_kalman<T>(hipStream_t, const DevState<T>&, const Params<T>&, const UpdWs<T>&, KernelTimer*);
 INSTANTIATE(float)
 INSTANTIATE(double)
