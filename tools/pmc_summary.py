@@ -7,7 +7,7 @@ FETCH.csv / WRITE.csv are the counter_collection CSVs of two separate
 `bench.py --steps K --warmup 0` command (the two TCC counters do not fit in
 one pass on gfx950).  Counter values are KiB per dispatch.  Kernels are
 grouped into the bench's timer stages; bytes_per_step = (FETCH + WRITE) * 1024
-summed over a stage's dispatches / K.  Per MI355X_MICROARCH.md, FETCH_SIZE on
+per dispatch, summed over the stage's kernels (each runs once per step).  Per MI355X_MICROARCH.md, FETCH_SIZE on
 gfx950 reads half of a 16-B-per-lane streaming read and other access widths
 are uncalibrated, so `fetch_x2_bytes_per_step` gives the upper estimate.
 """
@@ -52,7 +52,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("fetch")
     ap.add_argument("write")
-    ap.add_argument("--steps", type=int, required=True)
+    ap.add_argument("--steps", type=int, default=0,
+                    help="update steps in the passes (default: the dispatches of k_select of --dtype, one per step)")
     ap.add_argument("--dtype", default="fp32")
     ap.add_argument("-o", "--out", default="profiles/pmc_summary.json")
     ap.add_argument("--source", default="")
@@ -61,8 +62,14 @@ def main():
     a = ap.parse_args()
     fetch, nf = read(a.fetch)
     write, nw = read(a.write)
+    tname = "float" if a.dtype == "fp32" else "double"
+    if a.steps <= 0:   # every update runs k_select exactly once
+        a.steps = sum(c for n, c in nf.items() if "k_select<%s" % tname in n)
+        assert a.steps > 0, "no k_select dispatch of %s in %s" % (tname, a.fetch)
     stages = {}
     for name in sorted(set(fetch) | set(write)):
+        if "<%s" % ("double" if tname == "float" else "float") in name:
+            continue   # the other context's kernels (bench legs of the other scalar type)
         st = stage_of(name)
         if st is None:
             continue
@@ -72,9 +79,13 @@ def main():
         short = re.sub(r"\(.*", "", name).replace("void msckf::", "")
         d["kernels"][short] = {"dispatches": nf.get(name, nw.get(name, 0)),
                                "fetch_kib": fetch.get(name, 0.0), "write_kib": write.get(name, 0.0)}
+    # every kernel of a stage runs once per update step: per-dispatch averages
+    # (the bench's no-triangulation leg skips k_triangulate, so dispatch counts differ)
     for st, d in stages.items():
-        d["bytes_per_step"] = (d["fetch_kib"] + d["write_kib"]) * 1024 / a.steps
-        d["fetch_x2_bytes_per_step"] = (2 * d["fetch_kib"] + d["write_kib"]) * 1024 / a.steps
+        f = sum(k["fetch_kib"] / max(k["dispatches"], 1) for k in d["kernels"].values())
+        w = sum(k["write_kib"] / max(k["dispatches"], 1) for k in d["kernels"].values())
+        d["bytes_per_step"] = (f + w) * 1024
+        d["fetch_x2_bytes_per_step"] = (2 * f + w) * 1024
     json.dump({"dtype": a.dtype, "steps": a.steps, "workload": a.workload, "source": a.source, "unit": "bytes",
                "stages": stages}, open(a.out, "w"), indent=1, sort_keys=True)
     for st, d in sorted(stages.items(), key=lambda kv: -kv[1]["bytes_per_step"]):
