@@ -947,7 +947,7 @@ void launch_kalman_chol(hipStream_t s, const DevState<T>& st, const Params<T>& p
         else if (c.nt == 256) launch_c1<T, 256, 6>(s, st, ws, lds);
         else launch_c1<T, 512, 4>(s, st, ws, lds);
         if (Cq <= 16 * 8) launch_c2<T, 7, 2, 8>(s, st, ws);
-        else launch_c2<T, 7, 2, 12>(s, st, ws);
+        else launch_c2<T, 13, 1, 12>(s, st, ws);
     } else {
         launch_gchol<1, T>(s, st, ws);
     }
