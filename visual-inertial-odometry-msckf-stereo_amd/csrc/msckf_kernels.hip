@@ -27,22 +27,34 @@
 namespace msckf {
 
 // ===========================================================================
-// IMU propagation (process_model, msckf.py:291-368; jit_utils.py:6-135): one
-// 256-thread workgroup per listed filter; filter filters[w] takes samples
-// [smp_off[w], smp_off[w+1]) in order.  Per sample, between workgroup barriers:
-//   S0  wave 3 lane 0: the sample, bias-corrected rates, R (current q)
-//   S1  waves 0-2: F dt and G; then rows of F^2, F^3 and Phi (three rows per
-//       pass, 21 lanes per row: a row's products stay inside one wave) while
-//       wave 3 lane 0 runs the serial state prediction (RK4, quirk Q1) and the
-//       Phi edit terms (msckf.py:329-344)
-//   S2  the Phi edits
-//   S3  all waves, rows of A = Phi P11, Phi G Qc, (Phi G Qc) G^T, A Phi^T, the
-//       Q term and the cumulative Phi (jit_utils.py:130-135)
-//   S4  P11 = (A + A^T) / 2
-// The IMU x cam cross block is updated once with the product Phi_n ... Phi_1
-// (the per-sample full-P symmetrisation of msckf.py:362-363 is a no-op on the
-// cam x cam block and only re-rounds the cross block).  Every dot product runs
-// in the reference order (sum over k ascending).
+// IMU propagation (process_model, msckf.py:291-368; jit_utils.py:6-135): ONE
+// WAVE per listed filter (64-thread workgroups, ~20 KB of LDS in fp32: eight
+// filters resident per CU, the whole 2048-filter batch in one round, no
+// workgroup barriers -- the wave's own LDS ordering is the only sync).  Filter
+// filters[w] takes samples [smp_off[w], smp_off[w+1]) in order, in chunks of
+// PKC samples.  Only the quaternion recursion and the 21x21 covariance
+// recursion are serial, so a chunk runs in phases:
+//   A   one lane per sample: bias-corrected rates, the RK4 quaternion
+//       increments' 4x4 matrices (cos/sin of |w| dt / 2, / 4)
+//   B1  lane 0: the quaternion chain q_k -> dq_k -> q_{k+1}
+//   B2  one lane per sample: rotations, the RK4 slopes (quirk Q1), R_k
+//   B3  lane 0: the velocity / position sums
+//   B4  one lane per sample: the Phi edit terms (msckf.py:329-344)
+// then per sample, lane (g, c) = (lane / 21, lane % 21) owning rows 3 rb + g of
+// column c (or row c):
+//   C1..C5  F dt, F^2, Phi = I + F + F^2/2 + F^3/6 with the edits, Phi G Qc and
+//       the Q term (Phi G Qc G^T) Phi^T
+//   D1..D3  A = Phi P11 and the cumulative Phi, P11' = A Phi^T + Q dt,
+//       P11 = (P11' + P11'^T) / 2
+// Products run over the structurally non-zero 3x3 blocks only (skipped terms
+// are exact zeros: same sums, same order); the lane's Phi rows stay in
+// registers for C5, D1 and D2.  The IMU x cam cross block is updated once with
+// the product Phi_n ... Phi_1 (the per-sample full-P symmetrisation of
+// msckf.py:362-363 is a no-op on the cam x cam block and only re-rounds the
+// cross block); its columns are prefetched at the start (fp32) and its
+// transposed half is staged through LDS so that both halves are written in
+// contiguous rows.  Every dot product runs in the reference order (sum over k
+// ascending).
 // ===========================================================================
 template <typename T>
 __device__ __forceinline__ T skew_el(const T* w, int r, int c) {   // [w]x[r][c]
@@ -50,318 +62,485 @@ __device__ __forceinline__ T skew_el(const T* w, int r, int c) {   // [w]x[r][c]
                   : (r == 0 ? (c == 1 ? -w[2] : w[1]) : (r == 1 ? (c == 0 ? w[2] : -w[0]) : (c == 0 ? -w[1] : w[0])));
 }
 
-constexpr int PRS = 24;                 // LDS row stride of the 21-wide matrices (16-byte aligned rows)
-constexpr int PROP_MAT = 21 * PRS;
-// F, Phi, F^2, P11, P11', A, cum^T (x2), f rows; G, Phi G Qc (21 x 12); scalars; IMU record
-constexpr int PROP_LDS = 9 * PROP_MAT + 2 * 252 + 64 + IMU_STRIDE;   // T per workgroup
-enum PropScalar { PS_R = 0, PS_GYRO = 9, PS_ACC = 12, PS_DT = 15, PS_PHI00 = 16, PS_U = 25, PS_S = 28, PS_W1 = 31,
-                  PS_W2 = 34 };
+// LDS row strides of the 21-wide matrices and of Phi G Qc (21 x 12): a lane per
+// row (stride RS) hits distinct banks (25 dwords; 42 dwords per fp64 row)
+template <typename T> constexpr int prop_rs() { return sizeof(T) == 4 ? 25 : 21; }
+constexpr int PGS = 13;
+template <typename T> constexpr int prop_mat() { return 21 * prop_rs<T>(); }
+constexpr int PROP_SC = 104;   // per-sample scalars (PropSample)
+enum PropSample { PK_DT = 0, PK_W = 1, PK_A = 4, PK_M1 = 7, PK_M2 = 23, PK_Q = 39, PK_DQ = 43, PK_QN = 47,
+                  PK_H = 51, PK_VI = 60, PK_V = 63, PK_P = 66, PK_R = 69, PK_PHI00 = 78, PK_U = 87, PK_S = 90,
+                  PK_W1 = 93, PK_W2 = 96 };
+// structurally non-zero 3x3 column blocks of each row block (7 bits per row block)
+constexpr unsigned long long PM_F = 0x03ull | 0x09ull << 14 | 0x04ull << 28;              // F
+constexpr unsigned long long PM_F2 = 0x03ull | 0x03ull << 14 | 0x09ull << 28;             // F^2
+constexpr unsigned long long PM_PHI = 0x03ull | 0x02ull << 7 | 0x0Full << 14 | 0x08ull << 21 |
+                                      0x1Full << 28 | 0x20ull << 35 | 0x40ull << 42;     // Phi, cumulative Phi
 
 template <typename T>
-__device__ __forceinline__ void prop_row(const T* src, T (&v)[21]) {
-#pragma unroll
-    for (int k = 0; k < 21; ++k) v[k] = src[k];
+__host__ __device__ constexpr int prop_lds(int pkc) {   // T per workgroup
+    return 7 * prop_mat<T>() + pkc * PROP_SC + IMU_STRIDE;
 }
+template <typename T> constexpr int prop_pkc() { return sizeof(T) == 4 ? 12 : 10; }
 
-template <typename T>
-__global__ void __launch_bounds__(256) k_propagate(DevState<T> st, Params<T> prm, int nfilt,
-                                                   const int* __restrict__ filters,
-                                                   const int* __restrict__ smp_off,
-                                                   const T* __restrict__ samples_all) {
+// sum over the blocks of a (compile-time) mask, ascending: x[q] y[q]
+template <typename T, int N>
+__device__ __forceinline__ T prop_dot(const T* x, const T (&y)[N], unsigned mask) {
+    T s = 0;
+#pragma unroll
+    for (int m = 0; m < 7; ++m)
+        if (mask >> m & 1u) {
+#pragma unroll
+            for (int r = 0; r < 3; ++r) s += x[3 * m + r] * y[3 * m + r];
+        }
+    return s;
+}
+template <typename T, int N>
+__device__ __forceinline__ T prop_dot(const T (&x)[21], const T (&y)[N], unsigned mask) {
+    T s = 0;
+#pragma unroll
+    for (int m = 0; m < 7; ++m)
+        if (mask >> m & 1u) {
+#pragma unroll
+            for (int r = 0; r < 3; ++r) s += x[3 * m + r] * y[3 * m + r];
+        }
+    return s;
+}
+__device__ __forceinline__ void prop_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+template <typename T, int PKC>
+__global__ void __launch_bounds__(64) k_propagate(DevState<T> st, Params<T> prm, int nfilt,
+                                                  const int* __restrict__ filters,
+                                                  const int* __restrict__ smp_off,
+                                                  const T* __restrict__ samples_all) {
+    constexpr int RS = prop_rs<T>(), MAT = prop_mat<T>();
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lane = threadIdx.x;
     const int w = blockIdx.x;
     const int b = filters[w];
     const int n = smp_off[w + 1] - smp_off[w];
     const T* samples = samples_all + 7 * (size_t)smp_off[w];
     if (n <= 0) return;
-    T* F = reinterpret_cast<T*>(smem_raw);   // F dt
-    T* Phi = F + PROP_MAT;
-    T* F2 = Phi + PROP_MAT;
-    T* P11 = F2 + PROP_MAT;
-    T* P11n = P11 + PROP_MAT;
-    T* A = P11n + PROP_MAT;
-    T* cumT = A + PROP_MAT;                  // [2]: (Phi_k ... Phi_1)^T, ping-pong
-    T* fr = cumT + 2 * PROP_MAT;             // rows of (Phi G Qc) G^T
-    T* G = fr + PROP_MAT;                    // 21 x 12
-    T* PG = G + 252;                         // Phi G Qc
-    T* sc = PG + 252;                        // PropScalar
-    T* s_imu = sc + 64;
+    T* Pa = reinterpret_cast<T*>(smem_raw);  // P11 (ping-pong with Pb)
+    T* Pb = Pa + MAT;
+    T* cTa = Pb + MAT;                       // (Phi_k ... Phi_1)^T (ping-pong with cTb)
+    T* cTb = cTa + MAT;
+    T* PH = cTb + MAT;                       // Phi_k
+    T* QQ = PH + MAT;                        // F^2, then (Phi G Qc G^T) Phi^T
+    T* FP = QQ + MAT;                        // F dt, then Phi G Qc (21 x 12)
+    T* SK = FP + MAT;                        // [PKC][PROP_SC]
+    T* s_imu = SK + PKC * PROP_SC;
     T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
     const int ld = st.Dmax;
     T* imu = st.imu + (size_t)b * IMU_STRIDE;
     const int D = 21 + 6 * st.ncams[b];
-    for (int e = tid; e < IMU_STRIDE; e += 256) s_imu[e] = imu[e];
-    for (int e = tid; e < 441; e += 256) {
+    if (lane < IMU_STRIDE) s_imu[lane] = imu[lane];
+    for (int e = lane; e < 441; e += 64) {
         const int i = e / 21, j = e - 21 * i;
-        P11[i * PRS + j] = P[i * ld + j];
-        cumT[i * PRS + j] = i == j ? T(1) : T(0);
+        Pa[i * RS + j] = P[i * ld + j];
+        cTa[i * RS + j] = i == j ? T(1) : T(0);
     }
-    __syncthreads();
-    const int rr = lane / 21, jc = lane - 21 * rr;   // row of the 3-row group, column (lane 63 idle)
-    int cur = 0;
-    for (int k = 0; k < n; ++k) {
-        // ---- S0 ----
-        if (tid == 192) {
-            const T* smp = samples + 7 * k;
-            sc[PS_DT] = smp[0];
+    // the cross-block columns, prefetched: their load latency hides behind the samples
+    constexpr int NPRE = sizeof(T) == 4 ? 3 : 0;
+    T pre[NPRE > 0 ? NPRE : 1][21];
+#pragma unroll
+    for (int pp = 0; pp < NPRE; ++pp) {
+        const int j = 21 + 64 * pp + lane;
+#pragma unroll
+        for (int m = 0; m < 21; ++m) pre[pp][m] = j < D ? P[m * ld + j] : T(0);
+    }
+    prop_sync();
+    // matrix phases: lane (g, c), g = lane / 21 the row inside each 3-row block,
+    // c = lane % 21 a column (lane 63 idle)
+    const int g = lane / 21, c = lane - 21 * (lane / 21);
+    const bool act = lane < 63;
+    for (int k0 = 0; k0 < n; k0 += PKC) {
+        const int kc = min(PKC, n - k0);
+        // ---- A: one lane per sample ----
+        if (lane < kc) {
+            T* sk = SK + lane * PROP_SC;
+            const T* smp = samples + 7 * (k0 + lane);
+            const T dt = smp[0];
+            T wg[3], ac[3];
             for (int i = 0; i < 3; ++i) {
-                sc[PS_GYRO + i] = smp[1 + i] - s_imu[I_BG + i];
-                sc[PS_ACC + i] = smp[4 + i] - s_imu[I_BA + i];
+                wg[i] = smp[1 + i] - s_imu[I_BG + i];
+                ac[i] = smp[4 + i] - s_imu[I_BA + i];
             }
-            quat_to_rot(s_imu + I_Q, sc + PS_R);
-        }
-        __syncthreads();
-        const T dt = sc[PS_DT];
-        // ---- S1: F dt, G (jit_utils.py:25-34); R = R_w_i ----
-        if (wv < 3) {
-            const T* s_R = sc + PS_R;
-            const T* s_gyro = sc + PS_GYRO;
-            const T* s_acc = sc + PS_ACC;
-            for (int e = tid; e < 441; e += 192) {
-                const int i = e / 21, j = e - 21 * (e / 21);
-                const int bi = i / 3, bj = j / 3, r = i - 3 * bi, c = j - 3 * bj;
-                T f = 0;
-                if (bi == 0 && bj == 0) f = -skew_el(s_gyro, r, c);
-                else if (bi == 0 && bj == 1) f = r == c ? T(-1) : T(0);
-                else if (bi == 2 && bj == 0)   // -R^T [a]x
-                    f = -s_R[r] * skew_el(s_acc, 0, c) + -s_R[3 + r] * skew_el(s_acc, 1, c) + -s_R[6 + r] * skew_el(s_acc, 2, c);
-                else if (bi == 2 && bj == 3) f = -s_R[3 * c + r];
-                else if (bi == 4 && bj == 2) f = r == c ? T(1) : T(0);
-                F[i * PRS + j] = f * dt;
-            }
-            for (int e = tid; e < 252; e += 192) {
-                const int i = e / 12, j = e - 12 * (e / 12);
-                const int bi = i / 3, bj = j / 3, r = i - 3 * bi, c = j - 3 * bj;
-                T g = 0;
-                if (bi == bj && (bi == 0)) g = r == c ? T(-1) : T(0);
-                else if (bi == bj && (bi == 1 || bi == 3)) g = r == c ? T(1) : T(0);
-                else if (bi == 2 && bj == 2) g = -s_R[3 * c + r];
-                G[e] = g;
-            }
-        }
-        __syncthreads();
-        if (wv < 3) {   // rows 7 wv .. 7 wv + 6 of F^2, F^3, Phi
-            for (int p = 0; p < 3; ++p) {
-                if (rr >= 3 || 3 * p + rr >= 7) continue;
-                const int i = 7 * wv + 3 * p + rr;
-                T fi[21];
-                prop_row(F + i * PRS, fi);
-                T s2 = 0;
-#pragma unroll
-                for (int q = 0; q < 21; ++q) s2 += fi[q] * F[q * PRS + jc];
-                F2[i * PRS + jc] = s2;
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the row is this wave's: visible to its lanes
-                T f2i[21];
-                prop_row(F2 + i * PRS, f2i);
-                T s3 = 0;
-#pragma unroll
-                for (int q = 0; q < 21; ++q) s3 += f2i[q] * F[q * PRS + jc];
-                const T id = i == jc ? T(1) : T(0);
-                Phi[i * PRS + jc] = id + F[i * PRS + jc] + s2 / T(2) + s3 / T(6);
-            }
-        } else if (lane == 0) {
-            const T* s_gyro = sc + PS_GYRO;
-            const T* s_acc = sc + PS_ACC;
-            // ---- _predict_new_state (jit_utils.py:46-128), quirk Q1 ----
-            T* q = s_imu + I_Q;
-            T* v = s_imu + I_V;
-            T* p = s_imu + I_P;
-            const T* g = s_imu + I_G;
-            const T* w = s_gyro;
-            const T* acc = s_acc;
-            const bool alias = s_imu[I_ALIAS] != T(0);
-            T v_null[3], p_null[3];
-            for (int i = 0; i < 3; ++i) {   // Q5: entry values once aliased
-                v_null[i] = alias ? v[i] : s_imu[I_VN + i];
-                p_null[i] = alias ? p[i] : s_imu[I_PN + i];
-            }
-            T gn = sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
-            T Om[16] = {0, w[2], -w[1], w[0],
-                        -w[2], 0, w[0], w[1],
-                        w[1], -w[0], 0, w[2],
-                        -w[0], -w[1], -w[2], 0};
-            T dq[4], dq2[4];
+            sk[PK_DT] = dt;
+            for (int i = 0; i < 3; ++i) { sk[PK_W + i] = wg[i]; sk[PK_A + i] = ac[i]; }
+            const T gn = sqrt(wg[0] * wg[0] + wg[1] * wg[1] + wg[2] * wg[2]);
+            const T Om[16] = {0, wg[2], -wg[1], wg[0],
+                              -wg[2], 0, wg[0], wg[1],
+                              wg[1], -wg[0], 0, wg[2],
+                              -wg[0], -wg[1], -wg[2], 0};
             if (gn > T(1e-5)) {
-                T c1 = cos(gn * dt * T(0.5)), s1 = sin(gn * dt * T(0.5)) / gn;
-                T c2 = cos(gn * dt * T(0.25)), s2 = sin(gn * dt * T(0.25)) / gn;
-                for (int i = 0; i < 4; ++i) {
-                    T a1 = 0, a2 = 0;
-                    for (int j = 0; j < 4; ++j) {
-                        T id = (i == j) ? T(1) : T(0);
-                        a1 += (c1 * id + s1 * Om[4 * i + j]) * q[j];
-                        a2 += (c2 * id + s2 * Om[4 * i + j]) * q[j];
-                    }
-                    dq[i] = a1; dq2[i] = a2;
+                const T c1 = cos(gn * dt * T(0.5)), s1 = sin(gn * dt * T(0.5)) / gn;
+                const T c2 = cos(gn * dt * T(0.25)), s2 = sin(gn * dt * T(0.25)) / gn;
+                for (int e = 0; e < 16; ++e) {
+                    const T id = (e % 5 == 0) ? T(1) : T(0);
+                    sk[PK_M1 + e] = c1 * id + s1 * Om[e];
+                    sk[PK_M2 + e] = c2 * id + s2 * Om[e];
                 }
             } else {
-                T c1 = cos(gn * dt * T(0.5)), c2 = cos(gn * dt * T(0.25));
-                for (int i = 0; i < 4; ++i) {
-                    T a1 = 0, a2 = 0;
-                    for (int j = 0; j < 4; ++j) {
-                        T id = (i == j) ? T(1) : T(0);
-                        a1 += c1 * (id + Om[4 * i + j] * dt * T(0.5)) * q[j];
-                        a2 += c2 * (id + Om[4 * i + j] * dt * T(0.25)) * q[j];
-                    }
-                    dq[i] = a1; dq2[i] = a2;
+                const T c1 = cos(gn * dt * T(0.5)), c2 = cos(gn * dt * T(0.25));
+                for (int e = 0; e < 16; ++e) {
+                    const T id = (e % 5 == 0) ? T(1) : T(0);
+                    sk[PK_M1 + e] = c1 * (id + Om[e] * dt * T(0.5));
+                    sk[PK_M2 + e] = c2 * (id + Om[e] * dt * T(0.25));
                 }
             }
-            T nq = sqrt(dq[0] * dq[0] + dq[1] * dq[1] + dq[2] * dq[2] + dq[3] * dq[3]);
-            for (int i = 0; i < 4; ++i) dq[i] /= nq;
+        }
+        prop_sync();
+        // ---- B1: the quaternion chain (_predict_new_state, jit_utils.py:46-128) ----
+        if (lane == 0) {
+            T q[4] = {s_imu[I_Q], s_imu[I_Q + 1], s_imu[I_Q + 2], s_imu[I_Q + 3]};
+            for (int k = 0; k < kc; ++k) {
+                T* sk = SK + k * PROP_SC;
+                T dq[4];
+                for (int i = 0; i < 4; ++i) {
+                    T a1 = 0;
+                    for (int j = 0; j < 4; ++j) a1 += sk[PK_M1 + 4 * i + j] * q[j];
+                    dq[i] = a1;
+                }
+                const T nq = sqrt(dq[0] * dq[0] + dq[1] * dq[1] + dq[2] * dq[2] + dq[3] * dq[3]);
+                for (int i = 0; i < 4; ++i) dq[i] /= nq;
+                const T nn = sqrt(dq[0] * dq[0] + dq[1] * dq[1] + dq[2] * dq[2] + dq[3] * dq[3]);
+                for (int i = 0; i < 4; ++i) {
+                    sk[PK_Q + i] = q[i];
+                    sk[PK_DQ + i] = dq[i];
+                    q[i] = dq[i] / nn;
+                    sk[PK_QN + i] = q[i];
+                }
+            }
+        }
+        prop_sync();
+        // ---- B2: rotations and RK4 slopes, one lane per sample ----
+        if (lane < kc) {
+            T* sk = SK + lane * PROP_SC;
+            const T dt = sk[PK_DT];
+            const T* gv = s_imu + I_G;
+            T q[4], dq[4], dq2[4], acc[3];
+            for (int i = 0; i < 4; ++i) { q[i] = sk[PK_Q + i]; dq[i] = sk[PK_DQ + i]; }
+            for (int i = 0; i < 3; ++i) acc[i] = sk[PK_A + i];
+            for (int i = 0; i < 4; ++i) {
+                T a2 = 0;
+                for (int j = 0; j < 4; ++j) a2 += sk[PK_M2 + 4 * i + j] * q[j];
+                dq2[i] = a2;
+            }
             T S1[9];
             skew3(dq, S1);   // reused for dR_dt2 and k1 (Q1)
             T dRT[9], dR2T[9], Rk[9];
             {
-                T ww = dq[3];
+                const T ww = dq[3];
                 for (int i = 0; i < 3; ++i)
                     for (int j = 0; j < 3; ++j)   // transpose stored
                         dRT[3 * j + i] = (i == j ? 2 * ww * ww - 1 : T(0)) - 2 * ww * S1[3 * i + j] + (2 * dq[i]) * dq[j];
             }
-            T nq2 = sqrt(dq2[0] * dq2[0] + dq2[1] * dq2[1] + dq2[2] * dq2[2] + dq2[3] * dq2[3]);
+            const T nq2 = sqrt(dq2[0] * dq2[0] + dq2[1] * dq2[1] + dq2[2] * dq2[2] + dq2[3] * dq2[3]);
             for (int i = 0; i < 4; ++i) dq2[i] /= nq2;
             {
-                T ww = dq2[3];
+                const T ww = dq2[3];
                 for (int i = 0; i < 3; ++i)
                     for (int j = 0; j < 3; ++j)
                         dR2T[3 * j + i] = (i == j ? 2 * ww * ww - 1 : T(0)) - 2 * ww * S1[3 * i + j] + (2 * dq2[i]) * dq2[j];
             }
-            T nq0 = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
-            T qn[4] = {q[0] / nq0, q[1] / nq0, q[2] / nq0, q[3] / nq0};
+            const T nq0 = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+            const T qn[4] = {q[0] / nq0, q[1] / nq0, q[2] / nq0, q[3] / nq0};
             {
-                T ww = qn[3];
+                const T ww = qn[3];
                 for (int i = 0; i < 3; ++i)
                     for (int j = 0; j < 3; ++j)
                         Rk[3 * i + j] = (i == j ? 2 * ww * ww - 1 : T(0)) - 2 * ww * S1[3 * i + j] + (2 * qn[i]) * qn[j];
             }
-            T k1v[3], k2v[3], k3v[3], k4v[3], v1[3], v2[3], v3[3], tmp[3];
+            T k1v[3], k2v[3], k3v[3], k4v[3], tmp[3];
             mat3T_vec(Rk, acc, tmp);
-            for (int i = 0; i < 3; ++i) k1v[i] = tmp[i] + g[i];
-            for (int i = 0; i < 3; ++i) v1[i] = v[i] + k1v[i] * dt / T(2);
+            for (int i = 0; i < 3; ++i) k1v[i] = tmp[i] + gv[i];
             mat3_vec(dR2T, acc, tmp);
-            for (int i = 0; i < 3; ++i) k2v[i] = tmp[i] + g[i];
-            for (int i = 0; i < 3; ++i) v2[i] = v[i] + k2v[i] * dt / T(2);
-            for (int i = 0; i < 3; ++i) k3v[i] = tmp[i] + g[i];
-            for (int i = 0; i < 3; ++i) v3[i] = v[i] + k3v[i] * dt;
+            for (int i = 0; i < 3; ++i) k2v[i] = tmp[i] + gv[i];
+            for (int i = 0; i < 3; ++i) k3v[i] = tmp[i] + gv[i];
             mat3_vec(dRT, acc, tmp);
-            for (int i = 0; i < 3; ++i) k4v[i] = tmp[i] + g[i];
-            T nn = sqrt(dq[0] * dq[0] + dq[1] * dq[1] + dq[2] * dq[2] + dq[3] * dq[3]);
-            T vn[3], pn[3];
+            for (int i = 0; i < 3; ++i) k4v[i] = tmp[i] + gv[i];
             for (int i = 0; i < 3; ++i) {
-                vn[i] = v[i] + (k1v[i] + 2 * k2v[i] + 2 * k3v[i] + k4v[i]) * dt / T(6);
-                pn[i] = p[i] + (v[i] + 2 * v1[i] + 2 * v2[i] + v3[i]) * dt / T(6);
+                sk[PK_H + i] = k1v[i] * dt / T(2);
+                sk[PK_H + 3 + i] = k2v[i] * dt / T(2);
+                sk[PK_H + 6 + i] = k3v[i] * dt;
+                sk[PK_VI + i] = (k1v[i] + 2 * k2v[i] + 2 * k3v[i] + k4v[i]) * dt / T(6);
             }
-            for (int i = 0; i < 4; ++i) q[i] = dq[i] / nn;
-            for (int i = 0; i < 3; ++i) { v[i] = vn[i]; p[i] = pn[i]; }
-            // ---- Phi edit terms (msckf.py:329-344), applied in S2 ----
+            quat_to_rot(q, sk + PK_R);   // R_w_i at the step's start (F, G)
+        }
+        prop_sync();
+        // ---- B3: velocity and position ----
+        if (lane == 0) {
+            T v[3] = {s_imu[I_V], s_imu[I_V + 1], s_imu[I_V + 2]};
+            T p[3] = {s_imu[I_P], s_imu[I_P + 1], s_imu[I_P + 2]};
+            for (int k = 0; k < kc; ++k) {
+                T* sk = SK + k * PROP_SC;
+                const T dt = sk[PK_DT];
+                for (int i = 0; i < 3; ++i) {
+                    const T v1 = v[i] + sk[PK_H + i], v2 = v[i] + sk[PK_H + 3 + i], v3 = v[i] + sk[PK_H + 6 + i];
+                    const T pn = p[i] + (v[i] + 2 * v1 + 2 * v2 + v3) * dt / T(6);
+                    const T vn = v[i] + sk[PK_VI + i];
+                    sk[PK_V + i] = vn;
+                    sk[PK_P + i] = pn;
+                    v[i] = vn;
+                    p[i] = pn;
+                }
+            }
+        }
+        prop_sync();
+        // ---- B4: Phi edit terms (msckf.py:329-344), one lane per sample ----
+        if (lane < kc) {
+            T* sk = SK + lane * PROP_SC;
+            const T* skp = SK + (lane - 1) * PROP_SC;
+            const T dt = sk[PK_DT];
+            const T* gv = s_imu + I_G;
+            T q_null[4], v_null[3], p_null[3];
+            if (lane == 0) {   // the record's null state; Q5: entry values once aliased
+                const bool alias = s_imu[I_ALIAS] != T(0);
+                for (int i = 0; i < 4; ++i) q_null[i] = s_imu[I_QN + i];
+                for (int i = 0; i < 3; ++i) {
+                    v_null[i] = alias ? s_imu[I_V + i] : s_imu[I_VN + i];
+                    p_null[i] = alias ? s_imu[I_P + i] : s_imu[I_PN + i];
+                }
+            } else {           // the previous sample's result
+                for (int i = 0; i < 4; ++i) q_null[i] = skp[PK_QN + i];
+                for (int i = 0; i < 3; ++i) { v_null[i] = skp[PK_V + i]; p_null[i] = skp[PK_P + i]; }
+            }
+            T qk[4], vk[3], pk[3];
+            for (int i = 0; i < 4; ++i) qk[i] = sk[PK_QN + i];
+            for (int i = 0; i < 3; ++i) { vk[i] = sk[PK_V + i]; pk[i] = sk[PK_P + i]; }
             T Rkk1[9], Rq[9];
-            quat_to_rot(s_imu + I_QN, Rkk1);
-            quat_to_rot(q, Rq);
+            quat_to_rot(q_null, Rkk1);
+            quat_to_rot(qk, Rq);
             for (int i = 0; i < 3; ++i)
                 for (int j = 0; j < 3; ++j)
-                    sc[PS_PHI00 + 3 * i + j] = Rq[3 * i] * Rkk1[3 * j] + Rq[3 * i + 1] * Rkk1[3 * j + 1] + Rq[3 * i + 2] * Rkk1[3 * j + 2];
+                    sk[PK_PHI00 + 3 * i + j] = Rq[3 * i] * Rkk1[3 * j] + Rq[3 * i + 1] * Rkk1[3 * j + 1] + Rq[3 * i + 2] * Rkk1[3 * j + 2];
             T u[3];
-            mat3_vec(Rkk1, g, u);
-            T uu = u[0] * u[0] + u[1] * u[1] + u[2] * u[2];
-            T dv[3] = {v_null[0] - v[0], v_null[1] - v[1], v_null[2] - v[2]};
+            mat3_vec(Rkk1, gv, u);
+            const T uu = u[0] * u[0] + u[1] * u[1] + u[2] * u[2];
+            const T dv[3] = {v_null[0] - vk[0], v_null[1] - vk[1], v_null[2] - vk[2]};
             T Sk[9], w1[3], w2[3];
             skew3(dv, Sk);
-            mat3_vec(Sk, g, w1);
+            mat3_vec(Sk, gv, w1);
             T dp[3];
-            for (int i = 0; i < 3; ++i) dp[i] = dt * v_null[i] + p_null[i] - p[i];
+            for (int i = 0; i < 3; ++i) dp[i] = dt * v_null[i] + p_null[i] - pk[i];
             skew3(dp, Sk);
-            mat3_vec(Sk, g, w2);
+            mat3_vec(Sk, gv, w2);
             for (int i = 0; i < 3; ++i) {
-                sc[PS_U + i] = u[i];
-                sc[PS_S + i] = u[i] / uu;
-                sc[PS_W1 + i] = w1[i];
-                sc[PS_W2 + i] = w2[i];
+                sk[PK_U + i] = u[i];
+                sk[PK_S + i] = u[i] / uu;
+                sk[PK_W1 + i] = w1[i];
+                sk[PK_W2 + i] = w2[i];
             }
-            for (int i = 0; i < 4; ++i) s_imu[I_QN + i] = q[i];
-            for (int i = 0; i < 3; ++i) { s_imu[I_VN + i] = v[i]; s_imu[I_PN + i] = p[i]; }
+        }
+        prop_sync();
+        if (lane == 0) {   // the record after the chunk
+            const T* sk = SK + (kc - 1) * PROP_SC;
+            for (int i = 0; i < 4; ++i) { s_imu[I_Q + i] = sk[PK_QN + i]; s_imu[I_QN + i] = sk[PK_QN + i]; }
+            for (int i = 0; i < 3; ++i) {
+                s_imu[I_V + i] = sk[PK_V + i]; s_imu[I_VN + i] = sk[PK_V + i];
+                s_imu[I_P + i] = sk[PK_P + i]; s_imu[I_PN + i] = sk[PK_P + i];
+            }
             s_imu[I_ALIAS] = T(1);
         }
-        __syncthreads();
-        // ---- S2: Phi edits ----
-        if (tid < 9) {
-            Phi[(tid / 3) * PRS + tid % 3] = sc[PS_PHI00 + tid];
-        } else if (tid < 15) {   // rows 6..8 and 12..14, columns 0..2
-            const int q = tid - 9, blk = q / 3, i = q - 3 * blk, r = (blk == 0 ? 6 : 12) + i;
-            const T* wvv = sc + (blk == 0 ? PS_W1 : PS_W2);
-            T a1[3] = {Phi[r * PRS], Phi[r * PRS + 1], Phi[r * PRS + 2]};
-            const T au = a1[0] * sc[PS_U] + a1[1] * sc[PS_U + 1] + a1[2] * sc[PS_U + 2];
-            const T c = au - wvv[i];
-            for (int j = 0; j < 3; ++j) Phi[r * PRS + j] = a1[j] - c * sc[PS_S + j];
-        }
-        __syncthreads();
-        // ---- S3: rows 3 g .. 3 g + 2 for g = wv, wv + 4 ----
-        const T* cT = cumT + cur * PROP_MAT;
-        T* cTn = cumT + (cur ^ 1) * PROP_MAT;
-        for (int gi = 0; gi < 2; ++gi) {
-            const int g = wv + 4 * gi;
-            if (g >= 7 || rr >= 3) continue;
-            const int i = 3 * g + rr, j = jc;
-            T ph[21], row[21];
-            prop_row(Phi + i * PRS, ph);
-            prop_row(P11 + j * PRS, row);   // P11 is symmetric: column j = row j
-            T a = 0;
+        prop_sync();
+        for (int k = 0; k < kc; ++k) {
+            const T* sk = SK + k * PROP_SC;
+            const T dt = sk[PK_DT];
+            const T* R = sk + PK_R;
+            // ---- C1: F dt (jit_utils.py:25-34), rows 3 rb + g of column c ----
+            T fo[7] = {0, 0, 0, 0, 0, 0, 0};
+            if (act) {
+                const int bj = c / 3, cc = c - 3 * (c / 3);
+                const T* wg = sk + PK_W;
+                const T* ac = sk + PK_A;
+                const T f0 = bj == 0 ? -skew_el(wg, g, cc) : (bj == 1 ? (g == cc ? T(-1) : T(0)) : T(0));
+                const T f2 = bj == 0 ? -R[g] * skew_el(ac, 0, cc) + -R[3 + g] * skew_el(ac, 1, cc) + -R[6 + g] * skew_el(ac, 2, cc)
+                                     : (bj == 3 ? -R[3 * cc + g] : T(0));
+                const T f4 = (bj == 2 && g == cc) ? T(1) : T(0);
+                fo[0] = f0 * dt;
+                fo[2] = f2 * dt;
+                fo[4] = f4 * dt;
 #pragma unroll
-            for (int q = 0; q < 21; ++q) a += ph[q] * row[q];
-            A[i * PRS + j] = a;
-            prop_row(cT + j * PRS, row);     // column j of the cumulative Phi
-            T cn = 0;
-#pragma unroll
-            for (int q = 0; q < 21; ++q) cn += ph[q] * row[q];
-            cTn[j * PRS + i] = cn;
-            if (j < 12) {
-                T pg = 0;
-#pragma unroll
-                for (int q = 0; q < 21; ++q) pg += ph[q] * G[q * 12 + j];
-                const T qc = j < 3 ? prm.qc_gyro : (j < 6 ? prm.qc_gbias : (j < 9 ? prm.qc_acc : prm.qc_abias));
-                PG[i * 12 + j] = pg * qc;
+                for (int rb = 0; rb < 7; ++rb) FP[(3 * rb + g) * RS + c] = fo[rb];
             }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            prop_row(A + i * PRS, ph);
-            prop_row(Phi + j * PRS, row);
-            T t = 0;
+            prop_sync();
+            // ---- C2: F^2 ----
+            T fcol[12];   // F[q][c], q < 12 (F^2 and F^3 only reach these rows)
 #pragma unroll
-            for (int q = 0; q < 21; ++q) t += ph[q] * row[q];          // (A Phi^T)[i][j]
-            T f = 0;
+            for (int q = 0; q < 12; ++q) fcol[q] = act ? FP[q * RS + c] : T(0);
+            T f2o[7];
 #pragma unroll
-            for (int q = 0; q < 12; ++q) f += PG[i * 12 + q] * G[j * 12 + q];   // (Phi G Qc G^T)[i][j]
-            fr[i * PRS + j] = f;
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            prop_row(fr + i * PRS, ph);
-            T qv = 0;
+            for (int rb = 0; rb < 7; ++rb) {
+                const unsigned m = (unsigned)(PM_F >> (7 * rb)) & 0x7fu;
+                f2o[rb] = m ? prop_dot(FP + (3 * rb + g) * RS, fcol, m) : T(0);
+            }
+            prop_sync();   // every lane has read F before FP is reused
+            if (act) {
 #pragma unroll
-            for (int q = 0; q < 21; ++q) qv += ph[q] * row[q];         // (... Phi^T)[i][j]
-            P11n[i * PRS + j] = t + qv * dt;
+                for (int rb = 0; rb < 7; ++rb) QQ[(3 * rb + g) * RS + c] = f2o[rb];
+            }
+            prop_sync();
+            // ---- C3: Phi = I + F + F^2/2 + F^3/6, Phi[0:3, 0:3] edit ----
+            if (act) {
+#pragma unroll
+                for (int rb = 0; rb < 7; ++rb) {
+                    const int i = 3 * rb + g;
+                    const unsigned m = (unsigned)(PM_F2 >> (7 * rb)) & 0x7fu;
+                    const T s3 = m ? prop_dot(QQ + i * RS, fcol, m) : T(0);
+                    T ph = (i == c ? T(1) : T(0)) + fo[rb] + f2o[rb] / T(2) + s3 / T(6);
+                    if (rb == 0 && c < 3) ph = sk[PK_PHI00 + 3 * g + c];
+                    PH[i * RS + c] = ph;
+                }
+            }
+            prop_sync();
+            // ---- C3b: rows 6..8 and 12..14, columns 0..2 (msckf.py:339-344) ----
+            if (c < 3 && act) {
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    const int i = (e == 0 ? 6 : 12) + g;
+                    const T* wvv = sk + (e == 0 ? PK_W1 : PK_W2);
+                    const T a1[3] = {PH[i * RS], PH[i * RS + 1], PH[i * RS + 2]};
+                    const T au = a1[0] * sk[PK_U] + a1[1] * sk[PK_U + 1] + a1[2] * sk[PK_U + 2];
+                    const T cc = au - wvv[g];
+                    const T val = a1[c] - cc * sk[PK_S + c];
+                    asm volatile("" ::: "memory");   // all lanes read the row before it is edited
+                    PH[i * RS + c] = val;
+                }
+            }
+            prop_sync();
+            // this lane's rows 3 rb + g of Phi (non-zero blocks only): C5, D1 and D2 use them
+            T phr[7][21];
+#pragma unroll
+            for (int rb = 0; rb < 7; ++rb) {
+                const unsigned m = (unsigned)(PM_PHI >> (7 * rb)) & 0x7fu;
+#pragma unroll
+                for (int q = 0; q < 21; ++q)
+                    phr[rb][q] = (m >> (q / 3) & 1u) && act ? PH[(3 * rb + g) * RS + q] : T(0);
+            }
+            // ---- C4: Phi G Qc (G: jit_utils.py:30-34), row c, columns 3 mb + g ----
+            if (act) {
+                const T* ph = PH + c * RS;
+                FP[c * PGS + g] = ph[g] * T(-1) * prm.qc_gyro;
+                FP[c * PGS + 3 + g] = ph[3 + g] * T(1) * prm.qc_gbias;
+                FP[c * PGS + 6 + g] = (ph[6] * -R[3 * g] + ph[7] * -R[3 * g + 1] + ph[8] * -R[3 * g + 2]) * prm.qc_acc;
+                FP[c * PGS + 9 + g] = ph[9 + g] * T(1) * prm.qc_abias;
+            }
+            prop_sync();
+            // ---- C5: Q term row c: (Phi G Qc G^T)[c][q] Phi[j][q], j = 3 jb + g ----
+            if (act) {
+                const T* pg = FP + c * PGS;
+                T fr[12];
+#pragma unroll
+                for (int q = 0; q < 12; ++q) {
+                    const int r = q - 6;
+                    if (q < 3) fr[q] = pg[q] * T(-1);
+                    else if (q >= 6 && q < 9) fr[q] = pg[6] * -R[r] + pg[7] * -R[3 + r] + pg[8] * -R[6 + r];
+                    else fr[q] = pg[q] * T(1);
+                }
+#pragma unroll
+                for (int jb = 0; jb < 7; ++jb) {
+                    const int j = 3 * jb + g;
+                    const unsigned m = ((unsigned)(PM_PHI >> (7 * jb)) & 0x7fu) & 0x0Fu;   // G^T rows >= 12 are zero
+                    QQ[c * RS + j] = m ? prop_dot(phr[jb], fr, m) : T(0);
+                }
+            }
+            prop_sync();
+            // ---- D1: A = Phi P11 (column c), cumulative Phi (row c of its transpose) ----
+            if (act) {
+                T prow[21], crow[21];
+#pragma unroll
+                for (int q = 0; q < 21; ++q) { prow[q] = Pa[c * RS + q]; crow[q] = cTa[c * RS + q]; }   // P11 symmetric
+#pragma unroll
+                for (int rb = 0; rb < 7; ++rb) {
+                    const int i = 3 * rb + g;
+                    const unsigned m = (unsigned)(PM_PHI >> (7 * rb)) & 0x7fu;
+                    Pb[i * RS + c] = prop_dot(phr[rb], prow, m);
+                    cTb[c * RS + i] = prop_dot(phr[rb], crow, m);
+                }
+            }
+            prop_sync();
+            // ---- D2: A Phi^T + Q dt (row c) ----
+            if (act) {
+                T arow[21];
+#pragma unroll
+                for (int q = 0; q < 21; ++q) arow[q] = Pb[c * RS + q];
+#pragma unroll
+                for (int jb = 0; jb < 7; ++jb) {
+                    const int j = 3 * jb + g;
+                    const unsigned m = (unsigned)(PM_PHI >> (7 * jb)) & 0x7fu;
+                    Pa[c * RS + j] = prop_dot(phr[jb], arow, m) + QQ[c * RS + j] * dt;
+                }
+            }
+            prop_sync();
+            // ---- D3: P11 = (P11' + P11'^T) / 2 (msckf.py:362-363) ----
+            if (act) {
+#pragma unroll
+                for (int jb = 0; jb < 7; ++jb) {
+                    const int j = 3 * jb + g;
+                    Pb[c * RS + j] = (Pa[c * RS + j] + Pa[j * RS + c]) / T(2);
+                }
+            }
+            prop_sync();
+            T* t = Pa; Pa = Pb; Pb = t;
+            t = cTa; cTa = cTb; cTb = t;
         }
-        __syncthreads();
-        // ---- S4 ----
-        for (int e = tid; e < 441; e += 256) {
-            const int i = e / 21, j = e - 21 * i;
-            P11[i * PRS + j] = (P11n[i * PRS + j] + P11n[j * PRS + i]) / T(2);
-        }
-        cur ^= 1;
-        __syncthreads();
     }
-    // write back P11, IMU record; cross blocks with the cumulative Phi
-    const T* cT = cumT + cur * PROP_MAT;
-    for (int e = tid; e < 441; e += 256) P[(e / 21) * ld + e % 21] = P11[(e / 21) * PRS + e % 21];
-    for (int e = tid; e < IMU_STRIDE; e += 256) imu[e] = s_imu[e];
-    for (int j = 21 + tid; j < D; j += 256) {
-        T col[21];
+    // write back P11 and the IMU record; the cross blocks with the cumulative Phi
+    for (int e = lane; e < 441; e += 64) {
+        const int i = e / 21, j = e - 21 * i;
+        P[i * ld + j] = Pa[i * RS + j];
+        PH[i * RS + j] = cTa[j * RS + i];   // cumulative Phi, row-major
+    }
+    if (lane < IMU_STRIDE) imu[lane] = s_imu[lane];
+    prop_sync();
+    // 64 columns x 21 of the new cross block: over both P11 and both cumulative-Phi
+    // buffers (free now; PH, after them, holds the cumulative Phi)
+    T* xb = reinterpret_cast<T*>(smem_raw);
+    static_assert(4 * MAT >= 64 * 21, "cross-block staging");
 #pragma unroll
-        for (int m = 0; m < 21; ++m) col[m] = P[m * ld + j];
-#pragma unroll 3
-        for (int i = 0; i < 21; ++i) {
-            T sacc = 0;
+    for (int pp = 0; pp < NPRE + 1; ++pp) {
+        if (pp == NPRE) break;
+        const int j = 21 + 64 * pp + lane;
+        if (21 + 64 * pp >= D) break;
+        if (j < D) {
 #pragma unroll
-            for (int m = 0; m < 21; ++m) sacc += cT[m * PRS + i] * col[m];
-            P[i * ld + j] = sacc;
-            P[(size_t)j * ld + i] = sacc;
+            for (int i = 0; i < 21; ++i) {
+                const unsigned msk = (unsigned)(PM_PHI >> (7 * (i / 3))) & 0x7fu;
+                const T sacc = prop_dot(PH + i * RS, pre[pp], msk);
+                P[i * ld + j] = sacc;
+                xb[lane * 21 + i] = sacc;
+            }
         }
+        prop_sync();
+        const int j0 = 21 + 64 * pp, nj = min(64, D - j0);
+        for (int e = lane; e < 21 * nj; e += 64) {   // rows j of the transposed block, contiguous
+            const int jj = e / 21, i = e - 21 * jj;
+            P[(size_t)(j0 + jj) * ld + i] = xb[e];
+        }
+        prop_sync();
+    }
+    for (int j0 = 21 + 64 * NPRE; j0 < D; j0 += 64) {
+        const int j = j0 + lane;
+        if (j < D) {
+            T col[21];
+#pragma unroll
+            for (int m = 0; m < 21; ++m) col[m] = P[m * ld + j];
+#pragma unroll
+            for (int i = 0; i < 21; ++i) {
+                const unsigned msk = (unsigned)(PM_PHI >> (7 * (i / 3))) & 0x7fu;
+                const T sacc = prop_dot(PH + i * RS, col, msk);
+                P[i * ld + j] = sacc;
+                xb[lane * 21 + i] = sacc;
+            }
+        }
+        prop_sync();
+        const int nj = min(64, D - j0);
+        for (int e = lane; e < 21 * nj; e += 64) {   // rows j of the transposed block, contiguous
+            const int jj = e / 21, i = e - 21 * jj;
+            P[(size_t)(j0 + jj) * ld + i] = xb[e];
+        }
+        prop_sync();
     }
 }
 
@@ -2067,13 +2246,14 @@ template <typename T>
 void launch_propagate(hipStream_t s, const DevState<T>& st, const Params<T>& prm, int nfilt, const int* filters,
                       const int* smp_off, const T* samples) {
     if (nfilt <= 0) return;
-    const size_t lds = (size_t)PROP_LDS * sizeof(T);
+    constexpr int PKC = prop_pkc<T>();
+    const size_t lds = (size_t)prop_lds<T>(PKC) * sizeof(T);
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_propagate<T>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)k_propagate<T, PKC>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr = true;
     }
-    hipLaunchKernelGGL(k_propagate<T>, dim3(nfilt), dim3(256), lds, s, st, prm, nfilt, filters, smp_off,
+    hipLaunchKernelGGL((k_propagate<T, PKC>), dim3(nfilt), dim3(64), lds, s, st, prm, nfilt, filters, smp_off,
                        samples);
 }
 template <typename T>
