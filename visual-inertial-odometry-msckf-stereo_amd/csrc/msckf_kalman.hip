@@ -128,11 +128,12 @@ __global__ void __launch_bounds__(64 * NW) k_kal_c2(DevState<T> st, UpdWs<T> ws)
         if (r >= C || k >= C) return r == k ? 1.0 : 0.0;
         return k <= r ? L[(size_t)r * ldt + k] : 0.0;
     };
-    // diagonal block inverses: the block goes to a per-wave LDS scratch (img is
-    // free until the main loop), lane j < 16 solves column j by forward
-    // substitution straight into LI (rolled loops: this runs once per filter)
+    // diagonal block inverses: the block and its reciprocal diagonal go to a
+    // per-wave LDS scratch (img is free until the main loop), lane j < 16
+    // solves column j by forward substitution in registers (the divisions off
+    // the dependent chain), then stores it to LI
     for (int J = wv; J < nT; J += NW) {
-        double* blk = img + wv * 256;
+        double* blk = img + wv * 272;   // 16 x 16 block + reciprocal diagonal
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int e = lane + 64 * q, i = e >> 4, k = e & 15;
@@ -140,15 +141,21 @@ __global__ void __launch_bounds__(64 * NW) k_kal_c2(DevState<T> st, UpdWs<T> ws)
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        if (lane < 16) {
-            double* xj = LI + J * 256 + 16 * lane;   // Linv[i][lane] at xj[i]
-#pragma unroll 1
+        if (lane < 16) blk[256 + lane] = 1.0 / blk[17 * lane];   // reciprocal diagonal, in parallel
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        if (lane < 16) {   // column lane of the inverse, kept in registers
+            double x[16];
+#pragma unroll
             for (int i = 0; i < 16; ++i) {
                 double sv = i == lane ? 1.0 : 0.0;
-#pragma unroll 1
-                for (int k = lane; k < i; ++k) sv -= blk[16 * i + k] * xj[k];
-                xj[i] = i < lane ? 0.0 : sv / blk[17 * i];
+#pragma unroll
+                for (int k = 0; k < i; ++k) sv -= k >= lane ? blk[16 * i + k] * x[k] : 0.0;
+                x[i] = i < lane ? 0.0 : sv * blk[256 + i];
             }
+            double* xj = LI + J * 256 + 16 * lane;   // Linv[i][lane] at xj[i]
+#pragma unroll
+            for (int i = 0; i < 16; ++i) xj[i] = x[i];
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
@@ -161,24 +168,51 @@ __global__ void __launch_bounds__(64 * NW) k_kal_c2(DevState<T> st, UpdWs<T> ws)
         return 0.0;
     };
     v4d yk[CT][NTM];
+    // -L_T[16J : 16J+16, 0 : 16J] is software-pipelined: block row J + 1 is
+    // loaded into registers while step J runs its MFMAs, and stored to LDS
+    // after step J's closing barrier
+    constexpr int PFN = (256 * (NTM - 1) + NT - 1) / NT;
+    double pf[PFN];
+    auto fetch = [&](int J) {
+        const int w = 16 * J;
+#pragma unroll
+        for (int q = 0; q < PFN; ++q) {
+            const int e = tid + NT * q, i = e / w, col = e - i * w;
+            pf[q] = e < 16 * w ? -Lv(16 * J + i, col) : 0.0;
+        }
+    };
+    auto put = [&](int J) {
+        const int w = 16 * J;
+#pragma unroll
+        for (int q = 0; q < PFN; ++q) {
+            const int e = tid + NT * q, i = e / w, col = e - i * w;
+            if (e < 16 * w) img[col * C2S + i] = pf[q];
+        }
+    };
+    __syncthreads();   // the diagonal-block scratch in img is dead
+    if (nT > 1) fetch(1);
+    v4d xn[CT];   // this lane's X^T[J] elements of each tile
+#pragma unroll
+    for (int t = 0; t < CT; ++t) {
+        const int ct = wv + NW * t;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) xn[t][q] = ct < nE ? Xv(16 * ct + lc, lr + 4 * q) : 0.0;
+    }
 #pragma unroll
     for (int J = 0; J < NTM; ++J) {
         if (J >= nT) continue;   // uniform; continue (not break) keeps the loop unrollable
-        if (J > 0) {   // stage -L_T[16J : 16J+16, 0 : 16J]
-            const int w = 16 * J;
-            for (int e = tid; e < 16 * w; e += NT) {
-                const int i = e / w, col = e - i * w;
-                img[col * C2S + i] = -Lv(16 * J + i, col);
-            }
-        }
+        if (J > 0) put(J);
         __syncthreads();
+        if (J + 1 < nT) fetch(J + 1);
 #pragma unroll
         for (int t = 0; t < CT; ++t) {
             const int ct = wv + NW * t;
             if (ct >= nE) continue;
-            v4d a0, a1 = v4d{0.0, 0.0, 0.0, 0.0};
+            v4d a0 = xn[t], a1 = v4d{0.0, 0.0, 0.0, 0.0};
+            if (J + 1 < nT) {   // X^T[J + 1] for the next step, loaded under this one
 #pragma unroll
-            for (int q = 0; q < 4; ++q) a0[q] = Xv(16 * ct + lc, 16 * J + lr + 4 * q);
+                for (int q = 0; q < 4; ++q) xn[t][q] = Xv(16 * ct + lc, 16 * (J + 1) + lr + 4 * q);
+            }
 #pragma unroll
             for (int K = 0; K < J; ++K) {
 #pragma unroll
@@ -885,7 +919,7 @@ static void launch_c1(hipStream_t s, const DevState<T>& st, const UpdWs<T>& ws, 
 }
 template <typename T, int NW, int CT, int NTM>
 static void launch_c2(hipStream_t s, const DevState<T>& st, const UpdWs<T>& ws) {
-    constexpr int IMG = 16 * NTM * C2S > NW * 256 ? 16 * NTM * C2S : NW * 256;
+    constexpr int IMG = 16 * NTM * C2S > NW * 272 ? 16 * NTM * C2S : NW * 272;
     const size_t lds = (NTM * 256 + IMG) * sizeof(double);
     static bool attr = false;
     if (!attr) {
