@@ -2196,6 +2196,211 @@ __global__ void __launch_bounds__(NT) k_info(DevState<T> st, FeatBatch<T> fb, Up
     if (tid == 0 && blockIdx.y == 0) info[1] = C;
 }
 
+// ---------------------------------------------------------------------------
+// Information assembly on fp64 MFMA (windows up to 32 cams).  With Gall the
+// stacked G blocks of the filter's included features (3 rows per feature, 6
+// columns per cam slot),
+//     A = blockdiag_i(Hx_i^T Hx_i) - Gall^T Gall,   b = sum_i UB_i,
+// and Gall^T Gall is a rank-k update of the lower 16 x 16 tiles of A: the
+// included features are staged KF at a time as dense rows of Gall in LDS,
+// each wave accumulates six of the (at most 78) tiles with
+// v_mfma_f64_16x16x4f64 over 4-row k-steps, and a k-step only updates the
+// tiles both of whose column ranges its features touch (per-feature tile
+// masks).  The chunk's G blocks are fetched into registers under the previous
+// chunk's MFMAs, and its block-diagonal / b terms under its own.  The block
+// diagonal and b are summed per (cam, element) by one thread each, in feature
+// order.  Output as k_info: [A | b] in H_thin, info[1] = C.
+// ---------------------------------------------------------------------------
+typedef double v4d __attribute__((ext_vector_type(4)));
+constexpr int IM_NW = 14, IM_PPW = 6, IM_GS = 208;   // waves, tiles per wave, LDS row stride (doubles)
+constexpr int IM_KF = 8;                              // features per staged chunk (3 rows each)
+
+__host__ __device__ constexpr size_t info_mfma_lds(int maxnf, int maxobs) {
+    return (size_t)3 * IM_KF * IM_GS * sizeof(double) + (3 * IM_KF / 4) * sizeof(unsigned) +
+           (size_t)(32 * IM_KF + 4 * maxnf + maxobs + 1) * sizeof(int);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(64 * IM_NW) k_info_mfma(DevState<T> st, FeatBatch<T> fb, UpdWs<T> ws, int maxnf,
+                                                          int maxobs) {
+    constexpr int NT = 64 * IM_NW, KF = IM_KF, KR = 3 * KF, NKS = KR / 4;
+    static_assert(KR % 4 == 0 && 27 * 32 <= NT && 78 <= IM_NW * IM_PPW, "k_info_mfma shape");
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, lc = lane & 15, lr = lane >> 4;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    int* info = ws.info + 4 * b;
+    if (info[0] == 0) {   // nothing stacked: empty update
+        if (tid == 0) info[1] = 0;
+        return;
+    }
+    const int nc = st.ncams[b], C = 6 * nc, Cmax = ws.Cmax;
+    const int TT = (C + 15) >> 4, npair = TT * (TT + 1) / 2;
+    double* buf = reinterpret_cast<double*>(smem_raw);              // [KR][IM_GS] dense rows of Gall
+    unsigned* kmask = reinterpret_cast<unsigned*>(buf + KR * IM_GS);  // [NKS] tiles touched per k-step
+    int* posc = reinterpret_cast<int*>(kmask + NKS);                 // [KF][32] cam -> record (-1)
+    int* flist = posc + 32 * KF;                                     // [maxnf] included features, in order
+    unsigned* ftm = reinterpret_cast<unsigned*>(flist + maxnf);      // [maxnf] their tile masks
+    int* fo0 = reinterpret_cast<int*>(ftm + maxnf);                  // [maxnf] first record
+    int* fM = fo0 + maxnf;                                           // [maxnf] records (0: not included)
+    int* sobs = fM + maxnf;                                          // [maxobs] obs_cam of the filter
+    int* s_n = sobs + maxobs;
+    const int fbeg = fb.feat_off[b], fend = fb.feat_off[b + 1], nf = fend - fbeg;
+    const int obeg = fb.obs_off[fbeg], nobs = fb.obs_off[fend] - obeg;
+    for (int e = tid; e < nobs; e += NT) sobs[e] = fb.obs_cam[obeg + e];
+    for (int f = tid; f < nf; f += NT) {
+        fo0[f] = fb.obs_off[fbeg + f];
+        fM[f] = fb.include[fbeg + f] ? fb.obs_off[fbeg + f + 1] - fo0[f] : 0;
+    }
+    for (int e = tid; e < KR * IM_GS; e += NT) buf[e] = 0.0;
+    for (int e = tid; e < 32 * KF; e += NT) posc[e] = -1;
+    __syncthreads();
+    if (wv == 0) {   // the included features, in order
+        int base = 0;
+        for (int f0 = 0; f0 < nf; f0 += 64) {
+            const int f = f0 + lane;
+            const bool in = f < nf && fM[f] > 0;
+            const unsigned long long bal = __ballot(in);
+            if (in) flist[base + __popcll(bal & ((1ull << lane) - 1ull))] = f;
+            base += __popcll(bal);
+        }
+        if (lane == 0) *s_n = base;
+    }
+    __syncthreads();
+    const int nl = *s_n;
+    for (int i = tid; i < nl; i += NT) {
+        const int f = flist[i];
+        unsigned m = 0;
+        for (int o = 0; o < fM[f]; ++o) {
+            const int c = sobs[fo0[f] - obeg + o];
+            m |= (1u << ((6 * c) >> 4)) | (1u << ((6 * c + 5) >> 4));
+        }
+        ftm[i] = m;
+    }
+    // this wave's tiles (lower, row-major order p -> (ti, tj))
+    int pti[IM_PPW], ptj[IM_PPW];
+    bool pv[IM_PPW];
+    v4d acc[IM_PPW];
+#pragma unroll
+    for (int q = 0; q < IM_PPW; ++q) {
+        const int p = IM_PPW * wv + q;
+        int ti = (int)((sqrtf(8.0f * (float)p + 1.0f) - 1.0f) * 0.5f);
+        while (ti * (ti + 1) / 2 > p) --ti;
+        while ((ti + 1) * (ti + 2) / 2 <= p) ++ti;
+        pti[q] = __builtin_amdgcn_readfirstlane(ti);
+        ptj[q] = __builtin_amdgcn_readfirstlane(p - ti * (ti + 1) / 2);
+        pv[q] = p < npair;
+        acc[q] = v4d{0.0, 0.0, 0.0, 0.0};
+    }
+    // (cam, element) owner of the block diagonal / b: element < 21 packed lower DS, else UB
+    const bool dbo = tid < 27 * nc;
+    const int dc = tid / 27, de = tid - 27 * (tid / 27);
+    const int deoff = de < 21 ? OBG_DS + de : OBG_UB + (de - 21);
+    double dsum = 0.0;
+    // staging slot: chunk feature ss, its record so (tid < 32 KF)
+    const int ss = tid >> 5, so = tid & 31;
+    double g[18];
+    int gcol = -1;
+    auto fetch = [&](int l0) {
+        gcol = -1;
+        if (tid < 32 * KF && l0 + ss < nl) {
+            const int f = flist[l0 + ss];
+            if (so < fM[f]) {
+                const int o = fo0[f] + so;
+                gcol = 6 * sobs[o - obeg];
+                const double* r = fb.obs_g + (size_t)o * OBG_STRIDE + OBG_G;
+#pragma unroll
+                for (int k = 0; k < 18; ++k) g[k] = r[k];
+            }
+        }
+    };
+    __syncthreads();   // ftm complete
+    fetch(0);
+    for (int l0 = 0; l0 < nl; l0 += KF) {
+        // ---- stage the chunk (buf is all zero, posc all -1 here) ----
+        const int mycol = gcol;
+        if (mycol >= 0) {
+#pragma unroll
+            for (int r = 0; r < 3; ++r)
+#pragma unroll
+                for (int u = 0; u < 6; ++u) buf[(3 * ss + r) * IM_GS + mycol + u] = g[6 * r + u];
+            posc[32 * ss + mycol / 6] = so;
+        }
+        for (int k = tid; k < NKS; k += NT) {
+            unsigned m = 0;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = l0 + (4 * k + r) / 3;
+                if (i < nl) m |= ftm[i];
+            }
+            kmask[k] = m;
+        }
+        __syncthreads();
+        fetch(l0 + KF);   // the next chunk's G blocks, under this chunk's MFMAs
+        double dv[KF];
+#pragma unroll
+        for (int s = 0; s < KF; ++s) {
+            dv[s] = 0.0;
+            if (dbo && l0 + s < nl) {
+                const int o = posc[32 * s + dc];
+                if (o >= 0) dv[s] = fb.obs_g[(size_t)(fo0[flist[l0 + s]] + o) * OBG_STRIDE + deoff];
+            }
+        }
+        // ---- rank-KR update of this wave's tiles ----
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+            const unsigned km = kmask[ks];
+            const double* brow = buf + (4 * ks + lr) * IM_GS + lc;
+#pragma unroll
+            for (int q = 0; q < IM_PPW; ++q)
+                if (pv[q] && ((km >> pti[q]) & (km >> ptj[q]) & 1u))
+                    acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(brow[16 * pti[q]], brow[16 * ptj[q]], acc[q], 0, 0, 0);
+        }
+#pragma unroll
+        for (int s = 0; s < KF; ++s) dsum += dv[s];
+        __syncthreads();
+        // ---- back to all-zero rows / empty table ----
+        if (mycol >= 0) {
+#pragma unroll
+            for (int r = 0; r < 3; ++r)
+#pragma unroll
+                for (int u = 0; u < 6; ++u) buf[(3 * ss + r) * IM_GS + mycol + u] = 0.0;
+            posc[32 * ss + mycol / 6] = -1;
+        }
+        __syncthreads();
+    }
+    KT* F = ws.Hthin + (size_t)b * Cmax * (Cmax + 1);
+    const int ldf = Cmax + 1;
+#pragma unroll
+    for (int q = 0; q < IM_PPW; ++q) {
+        if (!pv[q]) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int row = 16 * pti[q] + lr + 4 * r, col = 16 * ptj[q] + lc;
+            if (row < C && col < C) {
+                const double v = -acc[q][r];
+                F[(size_t)row * ldf + col] = v;
+                F[(size_t)col * ldf + row] = v;
+            }
+        }
+    }
+    __syncthreads();   // the tiles' stores are visible to the block-diagonal owners
+    if (dbo) {
+        if (de < 21) {
+            int x = (int)((sqrtf(8.0f * (float)de + 1.0f) - 1.0f) * 0.5f);
+            while (x * (x + 1) / 2 > de) --x;
+            while ((x + 1) * (x + 2) / 2 <= de) ++x;
+            const int y = de - x * (x + 1) / 2;
+            const size_t i0 = (size_t)(6 * dc + x) * ldf + 6 * dc + y, i1 = (size_t)(6 * dc + y) * ldf + 6 * dc + x;
+            const double v = F[i0] + dsum;
+            F[i0] = v;
+            if (x != y) F[i1] = v;
+        } else {
+            F[(size_t)(6 * dc + de - 21) * ldf + Cmax] = dsum;
+        }
+    }
+    if (tid == 0) info[1] = C;
+}
+
 // State correction (msckf.py:566-595).
 template <typename T>
 __global__ void __launch_bounds__(64) k_correct(DevState<T> st, UpdWs<T> ws) {
@@ -2461,6 +2666,17 @@ static void launch_info_cfg(hipStream_t s, const DevState<T>& st, const FeatBatc
 template <typename T>
 void launch_compress(hipStream_t s, const DevState<T>& st, const FeatBatch<T>& fb, const UpdWs<T>& ws, int maxnf,
                      int maxobs) {
+    // windows up to 32 cams: fp64 MFMA tiles (k_info_mfma)
+    const size_t lds_m = info_mfma_lds(maxnf, maxobs);
+    if (st.Nmax <= 32 && maxobs > 0 && lds_m <= 160 * 1024) {
+        static size_t attr = 64 * 1024;
+        if (lds_m > attr) {
+            (void)hipFuncSetAttribute((const void*)k_info_mfma<T>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_m);
+            attr = lds_m;
+        }
+        hipLaunchKernelGGL((k_info_mfma<T>), dim3(st.B), dim3(64 * IM_NW), lds_m, s, st, fb, ws, maxnf, maxobs);
+        return;
+    }
     // one wave per 8 x 8 tile of cam pairs
     const int TS = (st.Nmax + 7) / 8, ntl = TS * (TS + 1) / 2;
     if (ntl <= 4) launch_info_cfg<T, 256>(s, st, fb, ws, maxnf, maxobs);
