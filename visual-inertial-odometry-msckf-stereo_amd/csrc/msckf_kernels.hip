@@ -2207,7 +2207,8 @@ __global__ void __launch_bounds__(NT) k_info(DevState<T> st, FeatBatch<T> fb, Up
 // v_mfma_f64_16x16x4f64 over 4-row k-steps, and a k-step only updates the
 // tiles both of whose column ranges its features touch (per-feature tile
 // masks).  The chunk's G blocks are fetched into registers under the previous
-// chunk's MFMAs, and its block-diagonal / b terms under its own.  The block
+// chunk's MFMAs, and its block-diagonal / b terms under its own; two barriers
+// per chunk (a feature slot's rows are only touched by one wave).  The block
 // diagonal and b are summed per (cam, element) by one thread each, in feature
 // order.  Output as k_info: [A | b] in H_thin, info[1] = C.
 // ---------------------------------------------------------------------------
@@ -2366,7 +2367,11 @@ __global__ void __launch_bounds__(64 * IM_NW) k_info_mfma(DevState<T> st, FeatBa
                 for (int u = 0; u < 6; ++u) buf[(3 * ss + r) * IM_GS + mycol + u] = 0.0;
             posc[32 * ss + mycol / 6] = -1;
         }
-        __syncthreads();
+        // no barrier before the next scatter: the rows of feature slot ss are written,
+        // cleared and re-written only by the 32 lanes (tid >> 5 == ss) of one wave, in
+        // program order (in-order LDS), and kmask is rewritten by wave 0 after every wave
+        // passed the barrier above
+        asm volatile("" ::: "memory");
     }
     KT* F = ws.Hthin + (size_t)b * Cmax * (Cmax + 1);
     const int ldf = Cmax + 1;
