@@ -252,11 +252,11 @@ __global__ void __launch_bounds__(64 * NW) k_kal_c2(DevState<T> st, UpdWs<T> ws)
 // registers (Nmax > 36): the same partial Cholesky, in place on a row-major
 // global workspace (rows < ncol: the square lower part; rows >= ncol: extra
 // rows with ncol columns), right-looking and blocked by GNB = 64 pivots.  Each
-// panel step is three launches over all filters: factor the 16 x 16 diagonal
+// panel step is three launches over all filters: factor the GNB x GNB diagonal
 // block (one wave per filter), the panel rows below it (one row per thread,
 // many workgroups per filter), and the trailing update A -= W W^T on the
 // matrix cores (64 x 64 fp64 MFMA tiles, gemm64 below).  The trailing matrix
-// makes one round trip per 16 pivots instead of one per pivot.
+// makes one round trip per GNB = 64 pivots instead of one per pivot.
 // ===========================================================================
 constexpr int GNB = 64;   // pivots per panel (50x400 / 80x1000 updates/s: 16: 24.1k / 4.98k, 32: 26.3k / 5.27k, 48: 26.8k / 5.21k, 64: 27.5k / 5.20k)
 
