@@ -78,7 +78,7 @@ struct msckf_ctx {
     SegClasses sc;
     DBuf<int> seg_list;
     DBuf<long long> ysq_off;
-    DBuf<unsigned char> obs_z, chi2, p_w, obs_ws, obs_g, tau, ysq, gamma;
+    DBuf<unsigned char> obs_z, chi2, p_w, obs_ws, obs_ht, obs_g, tau, ysq, gamma;
     DBuf<uint8_t> valid, accept, include;
     // misc scratch
     DBuf<unsigned char> scratch;
@@ -155,6 +155,7 @@ FeatBatch<T> feat_batch(msckf_ctx* c) {
     f.p_w = reinterpret_cast<T*>(c->p_w.p);
     f.valid = c->valid.p;
     f.obs_ws = reinterpret_cast<T*>(c->obs_ws.p);
+    f.obs_ht = reinterpret_cast<T*>(c->obs_ht.p);
     f.obs_g = reinterpret_cast<double*>(c->obs_g.p);
     f.compact = feature_needs_compact(c->maxM) ? 1 : 0;
     f.tau = reinterpret_cast<T*>(c->tau.p);
@@ -247,7 +248,8 @@ int load_features(msckf_ctx* c, int nf, const int32_t* feat_off, int single_filt
     HIPC(c->obs_z.ensure((nobs * 4 + 4) * ts));
     HIPC(c->chi2.ensure((nf + 1) * ts));
     HIPC(c->p_w.ensure((nf * 3 + 3) * ts));
-    HIPC(c->obs_ws.ensure((nobs * OBS_WS + OBS_WS) * ts));
+    HIPC(c->obs_ws.ensure(((feature_needs_compact(maxM) ? nobs : 0) * OBS_WS + OBS_WS) * ts));
+    HIPC(c->obs_ht.ensure((nobs * OBS_HTS + OBS_HTS) * ts));
     HIPC(c->obs_g.ensure((nobs + 1) * OBG_STRIDE * sizeof(double)));
     HIPC(c->tau.ensure((nf * 4 + 4) * ts));
     {   // the (4M)^2 global gating scratch is only needed by features too large
@@ -738,7 +740,7 @@ int msckf_destroy(msckf_ctx_t* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (auto* b : {&c->P, &c->imu, &c->cams, &c->P_snap, &c->imu_snap, &c->cams_snap, &c->Hthin, &c->Lc, &c->Vi, &c->Sii, &c->G, &c->Tm, &c->W, &c->Wk,
-                    &c->dx, &c->obs_z, &c->chi2, &c->p_w, &c->obs_ws, &c->obs_g, &c->tau, &c->ysq, &c->gamma, &c->scratch})
+                    &c->dx, &c->obs_z, &c->chi2, &c->p_w, &c->obs_ws, &c->obs_ht, &c->obs_g, &c->tau, &c->ysq, &c->gamma, &c->scratch})
         b->release();
     for (auto* b : {&c->ncams, &c->ncams_snap, &c->info, &c->afail, &c->feat_filter, &c->feat_off, &c->obs_off, &c->obs_cam,
                     &c->row_off, &c->iscratch, &c->gate_list, &c->seg_list})

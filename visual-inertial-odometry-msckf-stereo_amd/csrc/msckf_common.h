@@ -26,9 +26,12 @@ enum CamField { C_Q = 0, C_P = 4, C_QN = 7 };
 //   Qr  4    rows of Q^T r
 //   R   4    the observation's residual r_i (before projection)
 // obs_ws record per observation (T): Hx (4x6), V, W, Q^T r, r -- written only
-// when a compact-factor consumer runs (workgroup gating, QR merge) -- and the
-// rank-3 reduced rows for the register-tile gating: Ht (3x6), [r~ (3) | r_n].
-constexpr int OBS_HX = 0, OBS_V = 24, OBS_W = 36, OBS_QR = 54, OBS_R = 58, OBS_HT = 62, OBS_RT = 80, OBS_WS = 84;
+// when a compact-factor consumer runs (large-track gating).
+constexpr int OBS_HX = 0, OBS_V = 24, OBS_W = 36, OBS_QR = 54, OBS_R = 58, OBS_WS = 62;
+// obs_ht record per observation (T), always written: the rank-3 reduced rows
+// of the gating, Ht (3x6) and [r~ (3) | r_n] -- a dense 24-element stride, so
+// that k_feature's stores and the gate's loads are contiguous.
+constexpr int OBS_HT = 0, OBS_RT = 18, OBS_HTS = 24;
 
 // Per-observation Gram terms written by the feature kernel (always fp64),
 // consumed by the information assembly (k_info).  With G = the top 3 rows of
@@ -76,7 +79,8 @@ struct FeatBatch {
     const long long* ysq_off; // [nf+1] offsets of the (4M)^2 gating scratch
     T* p_w;                   // [nf][3]
     uint8_t* valid;           // [nf] triangulation validity (1 if p_w given)
-    T* obs_ws;                // [sum M][OBS_WS]
+    T* obs_ws;                // [sum M][OBS_WS] (compact-factor consumers only)
+    T* obs_ht;                // [sum M][OBS_HTS] gating rows
     double* obs_g;            // [sum M][OBG_STRIDE] Gram terms (fp64)
     int compact;              // write V / W / Q^T r / tau (LDS gate fallback, QR path)
     T* tau;                   // [nf][4]

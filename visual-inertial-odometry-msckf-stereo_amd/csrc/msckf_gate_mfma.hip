@@ -221,14 +221,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_wav
     float* stage = area;                   // [capb][9] Y blocks of one pass (row-major lower block order)
     float* pan = area;                     // [16 NB][4] panel rows (after the Y phase)
     int* slot = reinterpret_cast<int*>(area + gm_area(Mmax, capb));
-    const float* ws = fb.obs_ws + (size_t)o0 * OBS_WS;
+    const float* ws = fb.obs_ht + (size_t)o0 * OBS_HTS;
     for (int e = lane; e < 18 * M; e += 64) {
         const int o = e / 18;
-        ht[e] = ws[(size_t)o * OBS_WS + OBS_HT + (e - 18 * o)];
+        ht[e] = ws[(size_t)o * OBS_HTS + OBS_HT + (e - 18 * o)];
     }
     float rn2 = 0;
     for (int e = lane; e < 4 * M; e += 64) {
-        const float v = ws[(size_t)(e >> 2) * OBS_WS + OBS_RT + (e & 3)];
+        const float v = ws[(size_t)(e >> 2) * OBS_HTS + OBS_RT + (e & 3)];
         rt[e] = v;
         if ((e & 3) == 3) rn2 += v * v;
     }
@@ -430,12 +430,12 @@ __global__ void __launch_bounds__(256) k_gate_mfma_wg(DevState<float> st, Params
     float* pan = ht + gm_head(Mmax);               // [2][16 GW_NB][4]
     float* stage = pan + gw_pan();                 // [capb][9]
     int* slot = reinterpret_cast<int*>(stage + ((9 * capb + 3) & ~3));
-    const float* ws = fb.obs_ws + (size_t)o0 * OBS_WS;
+    const float* ws = fb.obs_ht + (size_t)o0 * OBS_HTS;
     for (int e = tid; e < 18 * M; e += 256) {
         const int o = e / 18;
-        ht[e] = ws[(size_t)o * OBS_WS + OBS_HT + (e - 18 * o)];
+        ht[e] = ws[(size_t)o * OBS_HTS + OBS_HT + (e - 18 * o)];
     }
-    for (int e = tid; e < 4 * M; e += 256) rt[e] = ws[(size_t)(e >> 2) * OBS_WS + OBS_RT + (e & 3)];
+    for (int e = tid; e < 4 * M; e += 256) rt[e] = ws[(size_t)(e >> 2) * OBS_HTS + OBS_RT + (e & 3)];
     for (int i = tid; i < M; i += 256) slot[i] = fb.obs_cam[o0 + i];
     __syncthreads();
     float rn2 = 0;

@@ -1059,7 +1059,7 @@ __global__ void __launch_bounds__(256, OPL == 1 ? 3 : 1) k_feature(DevState<T> s
             }
             const CT wr = nv[0] * r[s][0] + nv[1] * r[s][1] + nv[2] * r[s][2] + nv[3] * r[s][3];
             for (int a = 0; a < 4; ++a) rt4[a] = r[s][a] - beta * nv[a] * wr;
-            T* wsr = fb.obs_ws + (size_t)(o0 + i) * OBS_WS;
+            T* wsr = fb.obs_ht + (size_t)(o0 + i) * OBS_HTS;
             store_pairs(wsr + OBS_HT, Ht, 18);
             store_pairs(wsr + OBS_RT, rt4, 4);
         }
@@ -1489,14 +1489,14 @@ __global__ void __launch_bounds__(256) k_gate_wave(DevState<T> st, Params<T> prm
     T* wd = area;                              // [nT][GB]  panel rows: raw tile rows, then W D^-1
     T* wt = area + GB * gate_nt(Mmax);         // [nT][GB]  W^T per 4-row block: wt[blk][4 c + y] = W[4 blk + y][c]
     int* slot = reinterpret_cast<int*>(reinterpret_cast<T*>(smem_raw) + wpb * gate_wave_lds_T<T>(Mmax, capb)) + wv * Mmax;
-    const T* ws = fb.obs_ws + (size_t)o0 * OBS_WS;
+    const T* ws = fb.obs_ht + (size_t)o0 * OBS_HTS;
     for (int e = lane; e < 18 * M; e += 64) {
         const int o = e / 18;
-        ht[e] = ws[(size_t)o * OBS_WS + OBS_HT + (e - 18 * o)];
+        ht[e] = ws[(size_t)o * OBS_HTS + OBS_HT + (e - 18 * o)];
     }
     T rn2 = 0;
     for (int e = lane; e < 4 * M; e += 64) {
-        const T v = ws[(size_t)(e >> 2) * OBS_WS + OBS_RT + (e & 3)];
+        const T v = ws[(size_t)(e >> 2) * OBS_HTS + OBS_RT + (e & 3)];
         rt[e] = v;
         if ((e & 3) == 3) rn2 += v * v;
     }
@@ -1818,14 +1818,14 @@ __global__ void __launch_bounds__(NT) k_gate_big(DevState<T> st, Params<T> prm, 
     double* corner = rr + 4 * M;                         // [16], then the |r_n|^2 partials
     int* slot = reinterpret_cast<int*>(corner + 16 + NT / 64);   // [M]
     double* lds = reinterpret_cast<double*>(slot + ((M + 3) & ~3));   // rchol panel buffers
-    const T* ws = fb.obs_ws + (size_t)o0 * OBS_WS;
+    const T* ws = fb.obs_ht + (size_t)o0 * OBS_HTS;
     for (int e = threadIdx.x; e < 18 * M; e += NT) {
         const int o = e / 18;
-        ht[e] = (double)ws[(size_t)o * OBS_WS + OBS_HT + (e - 18 * o)];
+        ht[e] = (double)ws[(size_t)o * OBS_HTS + OBS_HT + (e - 18 * o)];
     }
     double rn2 = 0;
     for (int e = threadIdx.x; e < 4 * M; e += NT) {
-        const double v = (double)ws[(size_t)(e >> 2) * OBS_WS + OBS_RT + (e & 3)];
+        const double v = (double)ws[(size_t)(e >> 2) * OBS_HTS + OBS_RT + (e & 3)];
         rr[e] = v;
         if ((e & 3) == 3) rn2 += v * v;
     }
