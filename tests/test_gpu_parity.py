@@ -358,6 +358,26 @@ def test_gate_fp32_gamma_vs_oracle(N, F, B):
     assert np.quantile(e, 0.99) < 1e-2, np.quantile(e, 0.99)
 
 
+@pytest.mark.parametrize("N,F,B", [(40, 150, 2)])
+def test_gate_fp64_gamma_vs_oracle(N, F, B):
+    """fp64 gating against the oracle's gamma (msckf.py:606-614), relative
+    1e-9: the one-wave fp64 MFMA kernel (v_mfma_f64_16x16x4_f64, its own
+    accumulator row layout) for every class up to 6 blocks (M <= 30, single- and
+    multi-pass Y staging), k_gate_wave for 31 <= M <= 40; decisions identical."""
+    problems = [synth.make_update_problem(N, F, seed=700 + b) for b in range(B)]
+    ctx, ds, feat_off, acc, gam, pw, valid, rows = _batched(problems, np.float64)
+    n = 0
+    for b, d in enumerate(ds):
+        st, acc_o, tri_p, tri_ok, gam_o = oracle_update(d)
+        sl = slice(feat_off[b], feat_off[b + 1])
+        np.testing.assert_array_equal(valid[sl], tri_ok)
+        ok = tri_ok.astype(bool)
+        np.testing.assert_allclose(gam[sl][ok], gam_o[ok], rtol=1e-9)
+        np.testing.assert_array_equal(acc[sl], acc_o)
+        n += int(ok.sum())
+    assert n > 200
+
+
 def test_gate_fp32_scrambled_observation_order():
     """gamma is invariant under a permutation of a feature's observations (an
     orthogonal row map of the stacked system, quirk Q4), so scrambling them

@@ -62,6 +62,10 @@ struct DBuf {   // grow-only device buffer
 struct msckf_ctx {
     int device = 0, scalar = 8, B = 1, Nmax = 0, Dmax = 0, Cmax = 0;
     hipStream_t stream = nullptr;
+    // Kalman stage A reads only P: it runs on `side` under triangulation, the
+    // Jacobians and gating (fork / join events on the main stream)
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     msckf_config_t cfg{};
     std::vector<int> h_ncams;
     // state
@@ -352,6 +356,14 @@ int run_update_chain(msckf_ctx* c, int row_cap, bool triangulate) {
         launch_triangulate<T>(s, st, prm, fb, c->sc);
         c->timer.end(s);
     }
+    // stage A (register-tile windows) under the Jacobians and gating
+    const bool early_a = kalman_chol_supported(c->Cmax);
+    if (early_a) {
+        HIPC(hipEventRecord(c->ev_fork, s));
+        HIPC(hipStreamWaitEvent(c->side, c->ev_fork, 0));
+        launch_kalman_a_reg<T>(c->side, st, ws, &c->timer);
+        HIPC(hipEventRecord(c->ev_join, c->side));
+    }
     c->timer.begin(s, "feature_jacobian");
     launch_feature<T>(s, st, prm, fb, c->sc);
     c->timer.end(s);
@@ -364,6 +376,7 @@ int run_update_chain(msckf_ctx* c, int row_cap, bool triangulate) {
     c->timer.begin(s, "compress");
     launch_compress<T>(s, st, fb, ws, c->max_nf, c->max_obs);
     c->timer.end(s);
+    if (early_a) HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
     launch_kalman<T>(s, st, prm, ws, &c->timer);
     HIPC(hipGetLastError());
     return 0;
@@ -722,7 +735,13 @@ int msckf_create(const msckf_config_t* cfg, int hip_device, int scalar_bytes, in
     c->Cmax = 6 * n_cam_capacity;
     c->cfg = *cfg;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming);
     if (e != hipSuccess) {
+        if (c->stream) (void)hipStreamDestroy(c->stream);
+        if (c->side) (void)hipStreamDestroy(c->side);
+        if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
         delete c;
         FAIL(-2, "hipStreamCreate: %s", hipGetErrorString(e));
     }
@@ -739,6 +758,7 @@ int msckf_destroy(msckf_ctx_t* c) {
     if (!c) return 0;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->side) (void)hipStreamSynchronize(c->side);
     for (auto* b : {&c->P, &c->imu, &c->cams, &c->P_snap, &c->imu_snap, &c->cams_snap, &c->Hthin, &c->Lc, &c->Vi, &c->Sii, &c->G, &c->Tm, &c->W, &c->Wk,
                     &c->dx, &c->obs_z, &c->chi2, &c->p_w, &c->obs_ws, &c->obs_ht, &c->obs_g, &c->tau, &c->ysq, &c->gamma, &c->scratch})
         b->release();
@@ -750,6 +770,9 @@ int msckf_destroy(msckf_ctx_t* c) {
     c->accept.release();
     c->include.release();
     if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->side) (void)hipStreamDestroy(c->side);
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     delete c;
     return 0;
 }

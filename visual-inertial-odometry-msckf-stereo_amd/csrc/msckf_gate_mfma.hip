@@ -32,14 +32,40 @@ namespace {
 
 using F4 = float __attribute__((ext_vector_type(4)));
 using F2 = float __attribute__((ext_vector_type(2)));
+using D4 = double __attribute__((ext_vector_type(4)));
+using D2 = double __attribute__((ext_vector_type(2)));
+
+// Per-type pieces of the one-wave kernel (fp32 contexts: v_mfma_f32_16x16x4_f32;
+// fp64 contexts: v_mfma_f64_16x16x4_f64).  The A / B operand layouts agree (A:
+// row l & 15, k = l >> 4; B: k = l >> 4, column l & 15), the result layouts do
+// not: lane l holds column l & 15 and rows RG (l >> 4) + RS i, i = 0..3 -- f32:
+// 4 (l >> 4) + i, f64: (l >> 4) + 4 i (tools/probes/mfma_f64_layout.hip).
+template <typename T> struct GM;
+template <> struct GM<float> {
+    using V4 = F4;
+    using V2 = F2;
+    static constexpr int RS = 1, RG = 4;
+    __device__ static F4 mfma(float a, float b, F4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
+};
+template <> struct GM<double> {
+    using V4 = D4;
+    using V2 = D2;
+    static constexpr int RS = 4, RG = 1;
+    __device__ static D4 mfma(double a, double b, D4 c) { return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0); }
+};
+__device__ __forceinline__ float gfma(float a, float b, float c) { return fmaf(a, b, c); }
+__device__ __forceinline__ double gfma(double a, double b, double c) { return fma(a, b, c); }
 
 __host__ __device__ constexpr int gm_nb(int M) { return (3 * M + 4 + 15) / 16; }
 __host__ __device__ constexpr int gm_head(int Mmax) { return (22 * Mmax + 3) & ~3; }   // Ht rows + [r~ | r_n]
-__host__ __device__ constexpr int gm_area(int Mmax, int capb) {   // Y staging / panel + junk panel
-    return 9 * capb > 128 * gm_nb(Mmax) + 16 ? ((9 * capb + 3) & ~3) : 128 * gm_nb(Mmax) + 16;
+// Y staging / panel + the junk panel (written up to 128 NB + 12 RS - 1 by the
+// lanes that own no pivot column)
+__host__ __device__ constexpr int gm_area(int Mmax, int capb, int RS = 1) {
+    return 9 * capb > 128 * gm_nb(Mmax) + 16 * RS ? ((9 * capb + 3) & ~3) : 128 * gm_nb(Mmax) + 16 * RS;
 }
-__host__ __device__ constexpr int gm_wave_floats(int Mmax, int capb) {   // + two int offset tables
-    return gm_head(Mmax) + gm_area(Mmax, capb) + 2 * ((Mmax + 3) & ~3);
+// elements of T per wave (the two int offset tables take T-sized slots)
+__host__ __device__ constexpr int gm_wave_floats(int Mmax, int capb, int RS = 1) {
+    return gm_head(Mmax) + gm_area(Mmax, capb, RS) + 2 * ((Mmax + 3) & ~3);
 }
 #ifndef GATE_BIF_BIG
 #define GATE_BIF_BIG 3
@@ -68,12 +94,14 @@ static_assert(gm_class_exact(), "gating size classes must match the MFMA block c
 // explicit LDS waits (one wave's LDS operations complete in issue order): the
 // whole elimination is one basic block, so the scheduler can overlap the next
 // step's panel dump / reads / 4x4 factor with this step's MFMA tail.
-template <int NB>
-__device__ __forceinline__ bool gm_eliminate(F4 (&acc)[NB * (NB + 1) / 2], float* pan, int lane) {
+template <typename T, int NB>
+__device__ __forceinline__ bool gm_eliminate(typename GM<T>::V4 (&acc)[NB * (NB + 1) / 2], T* pan, int lane) {
+    using V4 = typename GM<T>::V4;
+    constexpr int RS = GM<T>::RS, RG = GM<T>::RG;
     const int col_l = lane & 15, rg = lane >> 4;
     const int csel = rg;   // pivot column of this lane's operands
     // this lane's B-operand element of block row RB: panel row 16 RB + col_l, column csel
-    const float* bsrc = pan + 4 * col_l + csel;
+    const T* bsrc = pan + 4 * col_l + csel;
     const bool owner[4] = {(col_l >> 2) == 0, (col_l >> 2) == 1, (col_l >> 2) == 2, (col_l >> 2) == 3};
     bool ok = true;
 #pragma unroll
@@ -87,72 +115,72 @@ __device__ __forceinline__ bool gm_eliminate(F4 (&acc)[NB * (NB + 1) / 2], float
             //    one dword column per lane: no bank conflicts) -- no divergent
             //    branch in the step
             {
-                float* d = owner[sc] ? pan + 4 * (16 * KB + 4 * rg) + (col_l & 3) : pan + 64 * NB + lane;
+                T* d = owner[sc] ? pan + 4 * (16 * KB + RG * rg) + (col_l & 3) : pan + 64 * NB + lane;
 #pragma unroll
                 for (int RB = KB; RB < NB; ++RB) {
-                    const F4 v = acc[bidx(RB, KB)];
-                    float* dd = d + 64 * (RB - KB);
-                    dd[0] = v[0]; dd[4] = v[1]; dd[8] = v[2]; dd[12] = v[3];
+                    const V4 v = acc[bidx(RB, KB)];
+                    T* dd = d + 64 * (RB - KB);
+                    dd[0] = v[0]; dd[4 * RS] = v[1]; dd[8 * RS] = v[2]; dd[12 * RS] = v[3];
                 }
             }
             // 2. every lane factors the diagonal 4x4 A_d = L D L^T (lower entries only)
-            const F4 r0 = *reinterpret_cast<const F4*>(pan + 4 * p0);
-            const F4 r1 = *reinterpret_cast<const F4*>(pan + 4 * p0 + 4);
-            const F4 r2 = *reinterpret_cast<const F4*>(pan + 4 * p0 + 8);
-            const F4 r3 = *reinterpret_cast<const F4*>(pan + 4 * p0 + 12);
-            F4 xr[NB];   // this lane's panel row of every block row
-            float bv[NB];
+            const V4 r0 = *reinterpret_cast<const V4*>(pan + 4 * p0);
+            const V4 r1 = *reinterpret_cast<const V4*>(pan + 4 * p0 + 4);
+            const V4 r2 = *reinterpret_cast<const V4*>(pan + 4 * p0 + 8);
+            const V4 r3 = *reinterpret_cast<const V4*>(pan + 4 * p0 + 12);
+            V4 xr[NB];   // this lane's panel row of every block row
+            T bv[NB];
 #pragma unroll
             for (int RB = KB; RB < NB; ++RB) {
-                xr[RB] = *reinterpret_cast<const F4*>(pan + 4 * (16 * RB + col_l));
+                xr[RB] = *reinterpret_cast<const V4*>(pan + 4 * (16 * RB + col_l));
                 bv[RB] = bsrc[64 * RB];
             }
-            const float d0 = r0.x, e0 = pivot_rcp(d0);
-            const float l10 = r1.x * e0, l20 = r2.x * e0, l30 = r3.x * e0;
-            const float d1 = r1.y - l10 * r1.x, e1 = pivot_rcp(d1);
-            const float m21 = r2.y - l20 * r1.x, m31 = r3.y - l30 * r1.x;
-            const float l21 = m21 * e1, l31 = m31 * e1;
-            const float d2 = r2.z - l20 * r2.x - l21 * m21, e2 = pivot_rcp(d2);
-            const float m32 = r3.z - l30 * r2.x - l31 * m21;
-            const float l32 = m32 * e2;
-            const float d3 = r3.w - l30 * r3.x - l31 * m31 - l32 * m32;
-            ok = ok && (d0 > 0.f) && (d1 > 0.f) && (d2 > 0.f) && (d3 > 0.f);
-            const float e3 = pivot_rcp(d3);
+            const T d0 = r0.x, e0 = pivot_rcp(d0);
+            const T l10 = r1.x * e0, l20 = r2.x * e0, l30 = r3.x * e0;
+            const T d1 = r1.y - l10 * r1.x, e1 = pivot_rcp(d1);
+            const T m21 = r2.y - l20 * r1.x, m31 = r3.y - l30 * r1.x;
+            const T l21 = m21 * e1, l31 = m31 * e1;
+            const T d2 = r2.z - l20 * r2.x - l21 * m21, e2 = pivot_rcp(d2);
+            const T m32 = r3.z - l30 * r2.x - l31 * m21;
+            const T l32 = m32 * e2;
+            const T d3 = r3.w - l30 * r3.x - l31 * m31 - l32 * m32;
+            ok = ok && (d0 > T(0)) && (d1 > T(0)) && (d2 > T(0)) && (d3 > T(0));
+            const T e3 = pivot_rcp(d3);
             // 3. the rank-4 update is C -= X A_d^-1 X^T, X = the panel columns: the
             //    B operand is X itself (lane: row 16 RB + col_l, pivot csel), the A
             //    operand X m with m = -(column csel of A_d^-1 = L^-T D^-1 L^-1).  Rows
             //    of finished pivots are not masked: exact elimination leaves them
             //    zero, and they only ever feed finished rows / columns.
-            const float i10 = -l10, i21 = -l21, i32 = -l32;
-            const float i20 = -l20 - l21 * i10, i31 = -l31 - l32 * i21;
-            const float i30 = -l30 - l31 * i10 - l32 * i20;
+            const T i10 = -l10, i21 = -l21, i32 = -l32;
+            const T i20 = -l20 - l21 * i10, i31 = -l31 - l32 * i21;
+            const T i30 = -l30 - l31 * i10 - l32 * i20;
             // h_j = (L^-1)[j][csel]; u_j = h_j / d_j
-            const float u0 = csel == 0 ? e0 : 0.f;
-            const float u1 = (csel == 1 ? 1.f : (csel == 0 ? i10 : 0.f)) * e1;
-            const float u2 = (csel == 2 ? 1.f : (csel == 1 ? i21 : (csel == 0 ? i20 : 0.f))) * e2;
-            const float u3 = (csel == 3 ? 1.f : (csel == 2 ? i32 : (csel == 1 ? i31 : i30))) * e3;
-            const float mm3 = -u3;
-            const float mm2 = -fmaf(i32, u3, u2);
-            const float mm1 = -fmaf(i31, u3, fmaf(i21, u2, u1));
-            const float mm0 = -fmaf(i30, u3, fmaf(i20, u2, fmaf(i10, u1, u0)));
-            float av[NB];
+            const T u0 = csel == 0 ? e0 : T(0);
+            const T u1 = (csel == 1 ? T(1) : (csel == 0 ? i10 : T(0))) * e1;
+            const T u2 = (csel == 2 ? T(1) : (csel == 1 ? i21 : (csel == 0 ? i20 : T(0)))) * e2;
+            const T u3 = (csel == 3 ? T(1) : (csel == 2 ? i32 : (csel == 1 ? i31 : i30))) * e3;
+            const T mm3 = -u3;
+            const T mm2 = -gfma(i32, u3, u2);
+            const T mm1 = -gfma(i31, u3, gfma(i21, u2, u1));
+            const T mm0 = -gfma(i30, u3, gfma(i20, u2, gfma(i10, u1, u0)));
+            T av[NB];
 #pragma unroll
             for (int RB = KB; RB < NB; ++RB) {
-                const F4 x = xr[RB];
-                av[RB] = fmaf(x.w, mm3, fmaf(x.z, mm2, fmaf(x.y, mm1, x.x * mm0)));
+                const V4 x = xr[RB];
+                av[RB] = gfma(x.w, mm3, gfma(x.z, mm2, gfma(x.y, mm1, x.x * mm0)));
             }
             // 4. trailing rank-4 update of the lower block triangle right of the panel
             //    (after a block's last step its own column is finished: skipped)
             if (sc < 3) {
 #pragma unroll
                 for (int RB = KB; RB < NB; ++RB)
-                    acc[bidx(RB, KB)] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[RB], bv[KB], acc[bidx(RB, KB)], 0, 0, 0);
+                    acc[bidx(RB, KB)] = GM<T>::mfma(av[RB], bv[KB], acc[bidx(RB, KB)]);
             }
 #pragma unroll
             for (int CB = KB + 1; CB < NB; ++CB)
 #pragma unroll
                 for (int RB = CB; RB < NB; ++RB)
-                    acc[bidx(RB, CB)] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[RB], bv[CB], acc[bidx(RB, CB)], 0, 0, 0);
+                    acc[bidx(RB, CB)] = GM<T>::mfma(av[RB], bv[CB], acc[bidx(RB, CB)]);
         }
     }
     return !ok;
@@ -160,30 +188,34 @@ __device__ __forceinline__ bool gm_eliminate(F4 (&acc)[NB * (NB + 1) / 2], float
 
 // gamma from the B rows' 4x4 Schur block (negated [[H_f~^T Y~^-1 H_f~, .],
 // [., r~^T Y~^-1 r~]]): rows / cols 12..15 of block (nb-1, nb-1), lanes 60..63.
-template <int NB>
-__device__ __forceinline__ void gm_finish(const F4 (&acc)[NB * (NB + 1) / 2], float* pan, int nb, int lane, bool fail,
-                                          float rn2, float s2, const FeatBatch<float>& fb, int f) {
+template <typename T, int NB>
+__device__ __forceinline__ void gm_finish(const typename GM<T>::V4 (&acc)[NB * (NB + 1) / 2], T* pan, int nb, int lane,
+                                          bool fail, T rn2, T s2, const FeatBatch<T>& fb, int f) {
+    constexpr int RS = GM<T>::RS, RG = GM<T>::RG;
     const int col_l = lane & 15, rg = lane >> 4;
 #pragma unroll
     for (int RB = 0; RB < NB; ++RB)
-        if (RB == nb - 1 && rg == 3 && col_l >= 12) {
-            const F4 v = acc[bidx(RB, RB)];
+        if (RB == nb - 1 && col_l >= 12) {
+            const typename GM<T>::V4 v = acc[bidx(RB, RB)];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) pan[4 * i + (col_l - 12)] = v[i];
+            for (int i = 0; i < 4; ++i) {
+                const int row = RG * rg + RS * i;   // rows 12..15 of the block: the B rows
+                if (row >= 12) pan[4 * (row - 12) + (col_l - 12)] = v[i];
+            }
         }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (lane == 0) {
-        const float* a = pan;
-        const float d0 = a[0];
-        const float l10 = a[4] / d0, l20 = a[8] / d0, l30 = a[12] / d0;
-        const float d1 = a[5] - l10 * l10 * d0;
-        const float l21 = (a[9] - l20 * l10 * d0) / d1;
-        const float l31 = (a[13] - l30 * l10 * d0) / d1;
-        const float d2 = a[10] - l20 * l20 * d0 - l21 * l21 * d1;
-        const float l32 = (a[14] - l30 * l20 * d0 - l31 * l21 * d1) / d2;
-        const float d3 = a[15] - l30 * l30 * d0 - l31 * l31 * d1 - l32 * l32 * d2;
-        float gam = -d3 + rn2 / s2;
-        if (fail || !(d0 < 0.f) || !(d1 < 0.f) || !(d2 < 0.f) || !(gam == gam)) gam = INFINITY;
+        const T* a = pan;
+        const T d0 = a[0];
+        const T l10 = a[4] / d0, l20 = a[8] / d0, l30 = a[12] / d0;
+        const T d1 = a[5] - l10 * l10 * d0;
+        const T l21 = (a[9] - l20 * l10 * d0) / d1;
+        const T l31 = (a[13] - l30 * l10 * d0) / d1;
+        const T d2 = a[10] - l20 * l20 * d0 - l21 * l21 * d1;
+        const T l32 = (a[14] - l30 * l20 * d0 - l31 * l21 * d1) / d2;
+        const T d3 = a[15] - l30 * l30 * d0 - l31 * l31 * d1 - l32 * l32 * d2;
+        T gam = -d3 + rn2 / s2;
+        if (fail || !(d0 < T(0)) || !(d1 < T(0)) || !(d2 < T(0)) || !(gam == gam)) gam = T(INFINITY);
         fb.gamma[f] = gam;
         fb.accept[f] = (gam < fb.chi2[f]) ? 1 : 0;
     }
@@ -192,13 +224,18 @@ __device__ __forceinline__ void gm_finish(const F4 (&acc)[NB * (NB + 1) / 2], fl
 
 // waves per SIMD the accumulators (4 NB (NB + 1) / 2 registers) leave room for
 // (single-pass Y staging keeps two or three pair blocks in flight: one wave less)
-__host__ __device__ constexpr int gm_waves(int NB, bool MP) {
-    return (NB <= 2 && MP) ? 5 : (NB <= 4 ? 4 : (NB <= 6 ? 3 : 2));
+// (fp64: 8 NB (NB + 1) / 2 accumulator registers)
+__host__ __device__ constexpr int gm_waves(int NB, bool MP, int ts = 4) {
+    return ts == 8 ? (NB <= 2 ? 3 : (NB <= 5 ? 2 : 1))
+                   : ((NB <= 2 && MP) ? 5 : (NB <= 4 ? 4 : (NB <= 6 ? 3 : 2)));
 }
 
-template <int NB, bool MP>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_waves(NB, MP)))) k_gate_mfma(DevState<float> st, Params<float> prm, FeatBatch<float> fb,
+template <typename T, int NB, bool MP>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_waves(NB, MP, sizeof(T))))) k_gate_mfma(DevState<T> st, Params<T> prm, FeatBatch<T> fb,
                                                    const int* __restrict__ flist, int nlist, int Mmax, int capb) {
+    using V4 = typename GM<T>::V4;
+    using V2 = typename GM<T>::V2;
+    constexpr int RS = GM<T>::RS, RG = GM<T>::RG;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wpb = blockDim.x >> 6;
     // wave-uniform by construction; readfirstlane tells the compiler, so every
@@ -215,20 +252,20 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_wav
     const int M = __builtin_amdgcn_readfirstlane(fb.obs_off[f + 1]) - o0, M3 = 3 * M;
     constexpr int nb = NB;                 // the size class: gm_nb(M) == NB (gm_class_exact)
     const int nB = 16 * nb - 4;            // first B row
-    float* ht = reinterpret_cast<float*>(smem_raw) + (size_t)wv * gm_wave_floats(Mmax, capb);
-    float* rt = ht + 18 * Mmax;            // [Mmax][4]: r~ (3), r_n
-    float* area = ht + gm_head(Mmax);
-    float* stage = area;                   // [capb][9] Y blocks of one pass (row-major lower block order)
-    float* pan = area;                     // [16 NB][4] panel rows (after the Y phase)
-    int* slot = reinterpret_cast<int*>(area + gm_area(Mmax, capb));
-    const float* ws = fb.obs_ht + (size_t)o0 * OBS_HTS;
+    T* ht = reinterpret_cast<T*>(smem_raw) + (size_t)wv * gm_wave_floats(Mmax, capb, RS);
+    T* rt = ht + 18 * Mmax;                // [Mmax][4]: r~ (3), r_n
+    T* area = ht + gm_head(Mmax);
+    T* stage = area;                       // [capb][9] Y blocks of one pass (row-major lower block order)
+    T* pan = area;                         // [16 NB][4] panel rows (after the Y phase)
+    int* slot = reinterpret_cast<int*>(area + gm_area(Mmax, capb, RS));
+    const T* ws = fb.obs_ht + (size_t)o0 * OBS_HTS;
     for (int e = lane; e < 18 * M; e += 64) {
         const int o = e / 18;
         ht[e] = ws[(size_t)o * OBS_HTS + OBS_HT + (e - 18 * o)];
     }
-    float rn2 = 0;
+    T rn2 = 0;
     for (int e = lane; e < 4 * M; e += 64) {
-        const float v = ws[(size_t)(e >> 2) * OBS_HTS + OBS_RT + (e & 3)];
+        const T v = ws[(size_t)(e >> 2) * OBS_HTS + OBS_RT + (e & 3)];
         rt[e] = v;
         if ((e & 3) == 3) rn2 += v * v;
     }
@@ -243,7 +280,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_wav
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 
     constexpr int NBLK = NB * (NB + 1) / 2;
-    F4 acc[NBLK];
+    V4 acc[NBLK];
     // Matrix assembly into the C-layout blocks of block rows [R0, R1): every
     // element written exactly once -- Y entries (lower, s2 on the diagonal) from
     // the pass's pair stage (kbase = its first pair), B rows [H_f~^T ; r~^T]
@@ -251,41 +288,48 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_wav
     // zeros.  The stage offset of Y[q][p] separates into a row part and a
     // column part: 9 (a (a + 1) / 2 + b) + 3 c_q + c_p with a = q / 3, b = p / 3.
     const int pad_lo = M3;
-    const float s2 = prm.sigma2;
+    const T s2 = prm.sigma2;
     auto assemble = [&](int R0, int R1, int kbase) {
         int col_l = lane & 15, rg = lane >> 4;   // opaque copies: index math stays in the pass loop
         asm volatile("" : "+v"(col_l), "+v"(rg));
 #pragma unroll
         for (int RB = 0; RB < NB; ++RB) {
             if (RB < R0 || RB >= R1) continue;   // uniform
-            const bool brow = RB == nb - 1 && rg == 3;   // this lane's 4 rows are the B rows
+            const bool brow = RB == nb - 1 && rg == 3;   // (f32) this lane's 4 rows are the B rows
             int rofs[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const int q = 16 * RB + 4 * rg + i, oa = q / 3;
+                const int q = 16 * RB + RG * rg + RS * i, oa = q / 3;
                 rofs[i] = 9 * (oa * (oa + 1) / 2 - kbase) + 3 * (q - 3 * oa);
             }
 #pragma unroll
             for (int CB = 0; CB <= RB; ++CB) {
                 const int p = 16 * CB + col_l, ob = p / 3, cp = p - 3 * ob;
-                float bval[4] = {0.f, 0.f, 0.f, 0.f};
+                T bval[4] = {T(0), T(0), T(0), T(0)};
                 if (RB == nb - 1) {   // uniform
-                    const bool pv = brow && p < M3;
-                    const int o = pv ? ob : 0;
+                    if constexpr (RS == 1) {
+                        const bool pv = brow && p < M3;
+                        const int o = pv ? ob : 0;
 #pragma unroll
-                    for (int i = 0; i < 3; ++i) bval[i] = pv ? -ht[18 * o + 6 * cp + 3 + i] : 0.f;
-                    bval[3] = pv ? rt[4 * o + cp] : 0.f;
+                        for (int i = 0; i < 3; ++i) bval[i] = pv ? -ht[18 * o + 6 * cp + 3 + i] : T(0);
+                        bval[3] = pv ? rt[4 * o + cp] : T(0);
+                    } else {   // f64: element 3 of every lane is B row rg (rows 12..15)
+                        const bool pv = p < M3;
+                        const int o = pv ? ob : 0;
+                        const T hv = ht[rg < 3 ? 18 * o + 6 * cp + 3 + rg : 18 * Mmax + 4 * o + cp];
+                        bval[3] = pv ? (rg < 3 ? -hv : hv) : T(0);
+                    }
                 }
-                F4 a;
+                V4 a;
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    const int q = 16 * RB + 4 * rg + i;
+                    const int q = 16 * RB + RG * rg + RS * i;
                     const bool take = q < pad_lo && (RB > CB || q >= p);
-                    const float y = stage[take ? rofs[i] + 9 * ob + cp : 0];
-                    float v = bval[i];
+                    const T y = stage[take ? rofs[i] + 9 * ob + cp : 0];
+                    T v = bval[i];
                     if (RB == CB) {
-                        v = (q == p && q >= pad_lo && q < nB) ? 1.f : v;
-                        v = take ? y + (q == p ? s2 : 0.f) : v;
+                        v = (q == p && q >= pad_lo && q < nB) ? T(1) : v;
+                        v = take ? y + (q == p ? s2 : T(0)) : v;
                     } else {
                         v = take ? y : v;
                     }
@@ -304,11 +348,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_wav
     // passes aligned to block rows [R0, R1) (observation rows [16 R0 / 3,
     // (16 R1 - 1) / 3], those straddling a boundary twice), so that every
     // accumulator block is assembled once, never read back.
-    const float* P = st.P + (size_t)b * st.Dmax * st.Dmax;
+    const T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
     const int ldp = st.Dmax;
     // pair blocks per lane in flight: the Y phase's VGPRs are free up to the
     // elimination's peak once the accumulators outgrow them (NB >= 5)
-    constexpr int BIF = MP ? 1 : (NB >= 5 ? GATE_BIF_BIG : 2);
+    constexpr int BIF = (MP || sizeof(T) == 8) ? 1 : (NB >= 5 ? GATE_BIF_BIG : 2);
     auto npairs = [&](int lo, int hi) { return hi < lo ? 0 : (hi + 1) * (hi + 2) / 2 - lo * (lo + 1) / 2; };
     for (int R0 = 0; R0 < nb;) {
         const int alo = (16 * R0) / 3;
@@ -321,7 +365,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_wav
         }
         const int kbase = alo * (alo + 1) / 2, nbp = npairs(alo, ahi);
         for (int k0 = 0; k0 < nbp; k0 += 64 * BIF) {
-            float Pl[BIF][36];
+            T Pl[BIF][36];
             int oa[BIF], ob[BIF];
 #pragma unroll
             for (int j = 0; j < BIF; ++j) {
@@ -334,14 +378,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_wav
                 if ((a + 1) * (a + 2) / 2 <= k) ++a;
                 oa[j] = a;
                 ob[j] = k - a * (a + 1) / 2;
-                const float* Pb = P + (slot[oa[j]] + coff[ob[j]]);
+                const T* Pb = P + (slot[oa[j]] + coff[ob[j]]);
 #pragma unroll
                 for (int u = 0; u < 6; ++u) {
                     if (kk < nbp) {
-                        __builtin_memcpy(Pl[j] + 6 * u, Pb + u * ldp, 6 * sizeof(float));
+                        __builtin_memcpy(Pl[j] + 6 * u, Pb + u * ldp, 6 * sizeof(T));
                     } else {
 #pragma unroll
-                        for (int c2 = 0; c2 < 6; ++c2) Pl[j][6 * u + c2] = 0.f;
+                        for (int c2 = 0; c2 < 6; ++c2) Pl[j][6 * u + c2] = T(0);
                     }
                 }
             }
@@ -349,30 +393,30 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_wav
             for (int j = 0; j < BIF; ++j) {
                 const int kk = k0 + 64 * j + lane;
                 if (kk >= nbp) continue;
-                const float* Ha = ht + 18 * oa[j];
-                const float* Hb = ht + 18 * ob[j];
-                float* dst = stage + 9 * kk;
-                F2 hb01[6];   // (Hb[0][u], Hb[1][u])
+                const T* Ha = ht + 18 * oa[j];
+                const T* Hb = ht + 18 * ob[j];
+                T* dst = stage + 9 * kk;
+                V2 hb01[6];   // (Hb[0][u], Hb[1][u])
 #pragma unroll
-                for (int u = 0; u < 6; ++u) hb01[u] = F2{Hb[u], Hb[6 + u]};
+                for (int u = 0; u < 6; ++u) hb01[u] = V2{Hb[u], Hb[6 + u]};
 #pragma unroll
                 for (int x = 0; x < 3; ++x) {
-                    F2 t2[3] = {F2{0, 0}, F2{0, 0}, F2{0, 0}};   // Ha[x] P as three column pairs
+                    V2 t2[3] = {V2{0, 0}, V2{0, 0}, V2{0, 0}};   // Ha[x] P as three column pairs
 #pragma unroll
                     for (int u = 0; u < 6; ++u) {
-                        const float h = Ha[6 * x + u];
+                        const T h = Ha[6 * x + u];
 #pragma unroll
                         for (int c = 0; c < 3; ++c)
-                            t2[c] = __builtin_elementwise_fma(F2{h, h}, F2{Pl[j][6 * u + 2 * c], Pl[j][6 * u + 2 * c + 1]},
+                            t2[c] = __builtin_elementwise_fma(V2{h, h}, V2{Pl[j][6 * u + 2 * c], Pl[j][6 * u + 2 * c + 1]},
                                                               t2[c]);
                     }
-                    const float t1[6] = {t2[0].x, t2[0].y, t2[1].x, t2[1].y, t2[2].x, t2[2].y};
-                    F2 y01 = {0, 0};
-                    float y2 = 0;
+                    const T t1[6] = {t2[0].x, t2[0].y, t2[1].x, t2[1].y, t2[2].x, t2[2].y};
+                    V2 y01 = {0, 0};
+                    T y2 = 0;
 #pragma unroll
                     for (int u = 0; u < 6; ++u) {
-                        y01 = __builtin_elementwise_fma(F2{t1[u], t1[u]}, hb01[u], y01);
-                        y2 = fmaf(t1[u], Hb[12 + u], y2);
+                        y01 = __builtin_elementwise_fma(V2{t1[u], t1[u]}, hb01[u], y01);
+                        y2 = gfma(t1[u], Hb[12 + u], y2);
                     }
                     dst[3 * x] = y01.x;
                     dst[3 * x + 1] = y01.y;
@@ -388,8 +432,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_wav
     }
 
     // ---- blocked LDL^T, 4 pivots per step, MFMA trailing updates ----
-    const bool fail = gm_eliminate<NB>(acc, pan, lane);
-    gm_finish<NB>(acc, pan, NB, lane, fail, rn2, s2, fb, f);
+    const bool fail = gm_eliminate<T, NB>(acc, pan, lane);
+    gm_finish<T, NB>(acc, pan, NB, lane, fail, rn2, s2, fb, f);
 }
 
 // ---------------------------------------------------------------------------
@@ -647,21 +691,21 @@ __global__ void __launch_bounds__(256) k_gate_mfma_wg(DevState<float> st, Params
     }
 }
 
-template <int NB, bool MP>
-void launch_cfg(hipStream_t s, const DevState<float>& st, const Params<float>& prm, const FeatBatch<float>& fb,
+template <typename T, int NB, bool MP>
+void launch_cfg(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const FeatBatch<T>& fb,
                 const int* list, int cnt, int Mmax, int capb, int wpb, size_t lds) {
     static size_t attr = 64 * 1024;
     if (lds > attr) {
-        (void)hipFuncSetAttribute((const void*)k_gate_mfma<NB, MP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)hipFuncSetAttribute((const void*)k_gate_mfma<T, NB, MP>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)lds);
         attr = lds;
     }
-    hipLaunchKernelGGL((k_gate_mfma<NB, MP>), dim3((cnt + wpb - 1) / wpb), dim3(64 * wpb), lds, s, st, prm, fb, list,
-                       cnt, Mmax, capb);
+    hipLaunchKernelGGL((k_gate_mfma<T, NB, MP>), dim3((cnt + wpb - 1) / wpb), dim3(64 * wpb), lds, s, st, prm, fb,
+                       list, cnt, Mmax, capb);
 }
 
-template <int NB>
-void launch_nb(hipStream_t s, const DevState<float>& st, const Params<float>& prm, const FeatBatch<float>& fb,
+template <typename T, int NB>
+void launch_nb(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const FeatBatch<T>& fb,
                const int* list, int cnt, int Mmax) {
     // Y staging capacity: all M (M + 1) / 2 pair blocks in one pass unless four
     // waves would then need more than 36 KB; otherwise passes (of
@@ -669,24 +713,27 @@ void launch_nb(hipStream_t s, const DevState<float>& st, const Params<float>& pr
     // phase's registers (one pair in flight per lane, 82-88 VGPRs), so the
     // classes with nb >= 4 gain a wave per SIMD.  Measured at 30x200 (gate
     // ms): budget 80: 3.46, 60: 3.28, 50: 3.10, 36: 3.05, 20 / 12: 3.06-3.10.
-    constexpr int single_kb = 36;
+    // (fp64: twice the bytes per element, and at most two waves per SIMD above NB = 3)
+    constexpr int single_kb = 36 * (int)sizeof(T) / 4;
+    constexpr int RS = GM<T>::RS;
     const int nbk = Mmax * (Mmax + 1) / 2;
     const int cmin = 6 * Mmax < nbk ? 6 * Mmax : nbk;   // one block row (up to six observation rows) per pass
-    auto per_wave = [&](int cb) { return (size_t)gm_wave_floats(Mmax, cb) * sizeof(float); };
+    auto per_wave = [&](int cb) { return (size_t)gm_wave_floats(Mmax, cb, RS) * sizeof(T); };
     int capb = nbk;
     if (4 * per_wave(capb) > (size_t)single_kb * 1024)
         for (int parts = 2; 4 * per_wave(capb) > (size_t)single_kb * 512 && capb > cmin; ++parts)
             capb = (nbk + parts - 1) / parts > cmin ? (nbk + parts - 1) / parts : cmin;
     const size_t pw = per_wave(capb);
     const int wpb = 4 * pw <= 160 * 1024 ? 4 : (2 * pw <= 160 * 1024 ? 2 : 1);
-    if (capb < nbk) launch_cfg<NB, true>(s, st, prm, fb, list, cnt, Mmax, capb, wpb, wpb * pw);
-    else launch_cfg<NB, false>(s, st, prm, fb, list, cnt, Mmax, capb, wpb, wpb * pw);
+    if (capb < nbk) launch_cfg<T, NB, true>(s, st, prm, fb, list, cnt, Mmax, capb, wpb, wpb * pw);
+    else launch_cfg<T, NB, false>(s, st, prm, fb, list, cnt, Mmax, capb, wpb, wpb * pw);
 }
 
 
 }  // namespace
 
-bool gate_mfma_fits(int maxM) { return maxM >= 1 && gm_nb(maxM) <= 8; }
+// fp64 up to NB = 6 (M <= 30): beyond it the accumulators spill (k_gate_wave then)
+bool gate_mfma_fits(int maxM, int ts) { return maxM >= 1 && gm_nb(maxM) <= (ts == 8 ? 6 : 8); }
 bool gate_mfma_wg_fits(int maxM) { return maxM >= 1 && gm_nb(maxM) <= GW_NB; }
 
 void launch_gate_mfma_wg(hipStream_t s, const DevState<float>& st, const Params<float>& prm,
@@ -707,19 +754,28 @@ void launch_gate_mfma_wg(hipStream_t s, const DevState<float>& st, const Params<
     hipLaunchKernelGGL(k_gate_mfma_wg, dim3(cnt), dim3(256), lds, s, st, prm, fb, list, maxM, capb);
 }
 
-void launch_gate_mfma(hipStream_t s, const DevState<float>& st, const Params<float>& prm, const FeatBatch<float>& fb,
+template <typename T>
+void launch_gate_mfma(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const FeatBatch<T>& fb,
                       const int* list, int cnt, int maxM) {
     if (cnt <= 0) return;
     switch (gm_nb(maxM)) {
-        case 1: launch_nb<1>(s, st, prm, fb, list, cnt, maxM); break;
-        case 2: launch_nb<2>(s, st, prm, fb, list, cnt, maxM); break;
-        case 3: launch_nb<3>(s, st, prm, fb, list, cnt, maxM); break;
-        case 4: launch_nb<4>(s, st, prm, fb, list, cnt, maxM); break;
-        case 5: launch_nb<5>(s, st, prm, fb, list, cnt, maxM); break;
-        case 6: launch_nb<6>(s, st, prm, fb, list, cnt, maxM); break;
-        case 7: launch_nb<7>(s, st, prm, fb, list, cnt, maxM); break;
-        default: launch_nb<8>(s, st, prm, fb, list, cnt, maxM); break;
+        case 1: launch_nb<T, 1>(s, st, prm, fb, list, cnt, maxM); break;
+        case 2: launch_nb<T, 2>(s, st, prm, fb, list, cnt, maxM); break;
+        case 3: launch_nb<T, 3>(s, st, prm, fb, list, cnt, maxM); break;
+        case 4: launch_nb<T, 4>(s, st, prm, fb, list, cnt, maxM); break;
+        case 5: launch_nb<T, 5>(s, st, prm, fb, list, cnt, maxM); break;
+        case 6: launch_nb<T, 6>(s, st, prm, fb, list, cnt, maxM); break;
+        default:
+            if constexpr (sizeof(T) == 4) {
+                if (gm_nb(maxM) == 7) launch_nb<T, 7>(s, st, prm, fb, list, cnt, maxM);
+                else launch_nb<T, 8>(s, st, prm, fb, list, cnt, maxM);
+            }
+            break;
     }
 }
+template void launch_gate_mfma<float>(hipStream_t, const DevState<float>&, const Params<float>&,
+                                      const FeatBatch<float>&, const int*, int, int);
+template void launch_gate_mfma<double>(hipStream_t, const DevState<double>&, const Params<double>&,
+                                       const FeatBatch<double>&, const int*, int, int);
 
 }  // namespace msckf

@@ -34,9 +34,10 @@ typedef double v4d __attribute__((ext_vector_type(4)));
 template <typename T, int NT, int TPL>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 ? 2 : 1))) k_kal_a(DevState<T> st, UpdWs<T> ws) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    // launched before k_select (side stream): every filter is factored, the
+    // status goes to afail only, and k_kal_c1 turns it into info[3] for the
+    // filters that do update
     const int b = blockIdx.x;
-    const int* info = ws.info + 4 * b;
-    if (info[0] == 0) return;
     const int C = 6 * st.ncams[b], Cp = round4(C);
     const int nrow = (Cp + KW) / 4;
     const T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
@@ -56,10 +57,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 2
     };
     auto trail = [&](int i, int j, double v) { Sii[(i - Cp) * KW + (j - Cp)] = v; };
     const bool ok = rchol_core<NT, TPL>(nrow, nrow, Cp / 4, reinterpret_cast<double*>(smem_raw), load, panel, trail);
-    if (threadIdx.x == 0) {
-        ws.afail[b] = ok ? 0 : 1;   // read by k_kal_c1
-        if (!ok) ws.info[4 * b + 3] = -1;
-    }
+    if (threadIdx.x == 0) ws.afail[b] = ok ? 0 : 1;   // read by k_kal_c1
 }
 
 // ---- stage C (register-tile windows, C <= 192) ----
@@ -942,24 +940,30 @@ static void launch_b(hipStream_t s, const DevState<T>& st, const Params<T>& prm,
 }
 
 template <typename T>
+void launch_kalman_a_reg(hipStream_t s, const DevState<T>& st, const UpdWs<T>& ws, KernelTimer* kt) {
+    const int Cp = (ws.Cmax + 3) & ~3;
+    const int nrow = (Cp + KW) / 4;   // stage A, 4x4 register tiles
+    RcholCfg c;
+    pick_rchol(nrow * (nrow + 1) / 2, c);
+    const size_t lds = rchol_lds_doubles(nrow) * sizeof(double);
+    kt->begin(s, "kalman_a");
+    if (c.nt == 256 && c.tpl == 4) launch_a_cfg<T, 256, 4>(s, st, ws, lds);
+    else if (c.nt == 256) launch_a_cfg<T, 256, 6>(s, st, ws, lds);
+    else launch_a_cfg<T, 512, 4>(s, st, ws, lds);
+    kt->end(s);
+}
+
+template <typename T>
 void launch_kalman_chol(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const UpdWs<T>& ws,
                         KernelTimer* kt) {
     const int Cp = (ws.Cmax + 3) & ~3, Cmax = ws.Cmax;
     const bool reg = kalman_chol_supported(Cmax);   // else large window: global-memory stages A and C
     const int Cq = (Cmax + 15) & ~15;
-    kt->begin(s, "kalman_a");
-    if (reg) {   // stage A, 4x4 register tiles
-        const int nrow = (Cp + KW) / 4;
-        RcholCfg c;
-        pick_rchol(nrow * (nrow + 1) / 2, c);
-        const size_t lds = rchol_lds_doubles(nrow) * sizeof(double);
-        if (c.nt == 256 && c.tpl == 4) launch_a_cfg<T, 256, 4>(s, st, ws, lds);
-        else if (c.nt == 256) launch_a_cfg<T, 256, 6>(s, st, ws, lds);
-        else launch_a_cfg<T, 512, 4>(s, st, ws, lds);
-    } else {
+    if (!reg) {   // (register-tile stage A: launch_kalman_a_reg, on the side stream)
+        kt->begin(s, "kalman_a");
         launch_gchol<0, T>(s, st, ws);
+        kt->end(s);
     }
-    kt->end(s);
     kt->begin(s, "kalman_b");
     if (Cq <= 16 * 8) {
         launch_b<T, 8, 4, 2, 8>(s, st, prm, ws, (4 * 16 * (size_t)Cq + 32) * sizeof(double));
@@ -1000,6 +1004,8 @@ void launch_kalman_chol(hipStream_t s, const DevState<T>& st, const Params<T>& p
     kt->end(s);
 }
 
+template void launch_kalman_a_reg<float>(hipStream_t, const DevState<float>&, const UpdWs<float>&, KernelTimer*);
+template void launch_kalman_a_reg<double>(hipStream_t, const DevState<double>&, const UpdWs<double>&, KernelTimer*);
 template void launch_kalman_chol<float>(hipStream_t, const DevState<float>&, const Params<float>&,
                                         const UpdWs<float>&, KernelTimer*);
 template void launch_kalman_chol<double>(hipStream_t, const DevState<double>&, const Params<double>&,

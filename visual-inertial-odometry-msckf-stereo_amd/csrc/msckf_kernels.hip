@@ -2593,11 +2593,11 @@ void launch_gate(hipStream_t s, const DevState<T>& st, const Params<T>& prm, con
         if (cnt == 0) continue;
         const int maxM = gc.maxM[c];
         const int* list = gc.list + gc.off[c];
-        if constexpr (sizeof(T) == 4) {   // fp32: MFMA tiles (msckf_gate_mfma.hip)
-            if (c < GateClasses::NC - 2 && gate_mfma_fits(maxM)) {
-                launch_gate_mfma(s, st, prm, fb, list, cnt, maxM);
-                continue;
-            }
+        if (c < GateClasses::NC - 2 && gate_mfma_fits(maxM, (int)sizeof(T))) {   // MFMA tiles (msckf_gate_mfma.hip)
+            launch_gate_mfma<T>(s, st, prm, fb, list, cnt, maxM);
+            continue;
+        }
+        if constexpr (sizeof(T) == 4) {   // fp32 large tracks: MFMA tiles, one workgroup per feature
             if (c == GateClasses::NC - 2 && gate_mfma_wg_fits(maxM)) {
                 launch_gate_mfma_wg(s, st, prm, fb, list, cnt, maxM);
                 continue;

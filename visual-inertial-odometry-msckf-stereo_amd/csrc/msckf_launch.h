@@ -103,10 +103,12 @@ struct GateClasses {
 };
 template <typename T>
 void launch_gate(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&, const GateClasses&);
-// fp32 gating on MFMA tiles (msckf_gate_mfma.hip), one wavefront per feature, M <= 40.
-bool gate_mfma_fits(int maxM);
-void launch_gate_mfma(hipStream_t, const DevState<float>&, const Params<float>&, const FeatBatch<float>&,
-                      const int* list, int cnt, int maxM);
+// Gating on MFMA tiles (msckf_gate_mfma.hip), one wavefront per feature, M <= 40
+// (fp32: v_mfma_f32_16x16x4_f32, fp64: v_mfma_f64_16x16x4_f64).
+bool gate_mfma_fits(int maxM, int scalar_bytes);
+template <typename T>
+void launch_gate_mfma(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&, const int* list, int cnt,
+                      int maxM);
 // fp32 gating of large tracks (40 < M <= 82) on MFMA tiles, one 4-wave workgroup per feature
 bool gate_mfma_wg_fits(int maxM);
 void launch_gate_mfma_wg(hipStream_t, const DevState<float>&, const Params<float>&, const FeatBatch<float>&,
@@ -119,6 +121,11 @@ void launch_compress(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const
 bool feature_needs_compact(int maxM);
 bool kalman_chol_supported(int Cmax);
 size_t kalman_global_ws_doubles(int Cmax);
+// Stage A of the register-tile windows (kalman_chol_supported) reads only P and
+// writes only Lc / Vi / Sii / afail, so it is launched on a side stream at the
+// start of the update chain; launch_kalman_chol then skips it.
+template <typename T>
+void launch_kalman_a_reg(hipStream_t, const DevState<T>&, const UpdWs<T>&, KernelTimer*);
 template <typename T>
 void launch_kalman_chol(hipStream_t, const DevState<T>&, const Params<T>&, const UpdWs<T>&, KernelTimer*);
 template <typename T>
