@@ -128,11 +128,11 @@ __device__ __forceinline__ bool gm_eliminate(typename GM<T>::V4 (&acc)[NB * (NB 
             const V4 r1 = *reinterpret_cast<const V4*>(pan + 4 * p0 + 4);
             const V4 r2 = *reinterpret_cast<const V4*>(pan + 4 * p0 + 8);
             const V4 r3 = *reinterpret_cast<const V4*>(pan + 4 * p0 + 12);
-            V4 xr[NB];   // this lane's panel row of every block row
+            V4 xr[NB];   // this lane's panel row of every block row (f32; f64 reads them as it goes)
             T bv[NB];
 #pragma unroll
             for (int RB = KB; RB < NB; ++RB) {
-                xr[RB] = *reinterpret_cast<const V4*>(pan + 4 * (16 * RB + col_l));
+                if constexpr (RS == 1) xr[RB] = *reinterpret_cast<const V4*>(pan + 4 * (16 * RB + col_l));
                 bv[RB] = bsrc[64 * RB];
             }
             const T d0 = r0.x, e0 = pivot_rcp(d0);
@@ -163,6 +163,20 @@ __device__ __forceinline__ bool gm_eliminate(typename GM<T>::V4 (&acc)[NB * (NB 
             const T mm2 = -gfma(i32, u3, u2);
             const T mm1 = -gfma(i31, u3, gfma(i21, u2, u1));
             const T mm0 = -gfma(i30, u3, gfma(i20, u2, gfma(i10, u1, u0)));
+            if constexpr (RS == 4) {
+                // f64: one block row at a time -- its panel row, its A operand, its
+                // blocks' updates -- so that the accumulators (8 per block) and
+                // the step's operands fit two waves per SIMD
+#pragma unroll
+                for (int RB = KB; RB < NB; ++RB) {
+                    const V4 x = *reinterpret_cast<const V4*>(pan + 4 * (16 * RB + col_l));
+                    const T a = gfma(x.w, mm3, gfma(x.z, mm2, gfma(x.y, mm1, x.x * mm0)));
+#pragma unroll
+                    for (int CB = KB; CB <= RB; ++CB)
+                        if (CB > KB || sc < 3) acc[bidx(RB, CB)] = GM<T>::mfma(a, bv[CB], acc[bidx(RB, CB)]);
+                }
+                continue;
+            }
             T av[NB];
 #pragma unroll
             for (int RB = KB; RB < NB; ++RB) {
@@ -226,7 +240,7 @@ __device__ __forceinline__ void gm_finish(const typename GM<T>::V4 (&acc)[NB * (
 // (single-pass Y staging keeps two or three pair blocks in flight: one wave less)
 // (fp64: 8 NB (NB + 1) / 2 accumulator registers)
 __host__ __device__ constexpr int gm_waves(int NB, bool MP, int ts = 4) {
-    return ts == 8 ? (NB <= 2 ? 3 : (NB <= 5 ? 2 : 1))
+    return ts == 8 ? (NB <= 3 ? 3 : 2)
                    : ((NB <= 2 && MP) ? 5 : (NB <= 4 ? 4 : (NB <= 6 ? 3 : 2)));
 }
 
@@ -364,6 +378,48 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_wav
             ahi = ah2;
         }
         const int kbase = alo * (alo + 1) / 2, nbp = npairs(alo, ahi);
+        if constexpr (RS == 4 && MP) {
+            // f64, staged in passes (earlier passes' accumulators live): one pair
+            // per lane, P streamed a row at a time into Ha P (3 x 6) -- 36 + 12
+            // registers instead of the 6 x 6 block's 72
+            for (int kk = lane; kk < nbp; kk += 64) {
+                const int k = kbase + kk;
+                int a = (int)((__builtin_amdgcn_sqrtf(8.0f * (float)k + 1.0f) - 1.0f) * 0.5f);
+                if (a * (a + 1) / 2 > k) --a;
+                if ((a + 1) * (a + 2) / 2 <= k) ++a;
+                const int bo = k - a * (a + 1) / 2;
+                const T* Pb = P + (slot[a] + coff[bo]);
+                const T* Ha = ht + 18 * a;
+                const T* Hb = ht + 18 * bo;
+                T t[3][6];
+#pragma unroll
+                for (int x = 0; x < 3; ++x)
+#pragma unroll
+                    for (int c = 0; c < 6; ++c) t[x][c] = T(0);
+#pragma unroll
+                for (int u = 0; u < 6; ++u) {
+                    T pr[6];
+                    __builtin_memcpy(pr, Pb + u * ldp, 6 * sizeof(T));
+#pragma unroll
+                    for (int x = 0; x < 3; ++x) {
+                        const T h = Ha[6 * x + u];
+#pragma unroll
+                        for (int c = 0; c < 6; ++c) t[x][c] = gfma(h, pr[c], t[x][c]);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);   // one P row in flight
+                }
+                T* dst = stage + 9 * kk;
+#pragma unroll
+                for (int x = 0; x < 3; ++x)
+#pragma unroll
+                    for (int y = 0; y < 3; ++y) {
+                        T v = 0;
+#pragma unroll
+                        for (int u = 0; u < 6; ++u) v = gfma(t[x][u], Hb[6 * y + u], v);
+                        dst[3 * x + y] = v;
+                    }
+            }
+        } else
         for (int k0 = 0; k0 < nbp; k0 += 64 * BIF) {
             T Pl[BIF][36];
             int oa[BIF], ob[BIF];
