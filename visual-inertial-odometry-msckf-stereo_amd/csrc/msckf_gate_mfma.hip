@@ -94,10 +94,17 @@ static_assert(gm_class_exact(), "gating size classes must match the MFMA block c
 // explicit LDS waits (one wave's LDS operations complete in issue order): the
 // whole elimination is one basic block, so the scheduler can overlap the next
 // step's panel dump / reads / 4x4 factor with this step's MFMA tail.
+// Register-lean variants (block rows streamed through the elimination, P rows
+// through the multi-pass Y phase): the f64 classes.  (f32 NB = 5 / 6 streamed at
+// four waves per SIMD measured no faster -- 2.68 ms -- or slower with NB = 6's
+// spill -- 2.92 ms -- than the wide version at three.)
+__host__ __device__ constexpr bool gm_stream(int NB, int ts) { return ts == 8; }
+
 template <typename T, int NB>
 __device__ __forceinline__ bool gm_eliminate(typename GM<T>::V4 (&acc)[NB * (NB + 1) / 2], T* pan, int lane) {
     using V4 = typename GM<T>::V4;
     constexpr int RS = GM<T>::RS, RG = GM<T>::RG;
+    constexpr bool STREAM = gm_stream(NB, sizeof(T));
     const int col_l = lane & 15, rg = lane >> 4;
     const int csel = rg;   // pivot column of this lane's operands
     // this lane's B-operand element of block row RB: panel row 16 RB + col_l, column csel
@@ -132,7 +139,7 @@ __device__ __forceinline__ bool gm_eliminate(typename GM<T>::V4 (&acc)[NB * (NB 
             T bv[NB];
 #pragma unroll
             for (int RB = KB; RB < NB; ++RB) {
-                if constexpr (RS == 1) xr[RB] = *reinterpret_cast<const V4*>(pan + 4 * (16 * RB + col_l));
+                if constexpr (!STREAM) xr[RB] = *reinterpret_cast<const V4*>(pan + 4 * (16 * RB + col_l));
                 bv[RB] = bsrc[64 * RB];
             }
             const T d0 = r0.x, e0 = pivot_rcp(d0);
@@ -163,10 +170,10 @@ __device__ __forceinline__ bool gm_eliminate(typename GM<T>::V4 (&acc)[NB * (NB 
             const T mm2 = -gfma(i32, u3, u2);
             const T mm1 = -gfma(i31, u3, gfma(i21, u2, u1));
             const T mm0 = -gfma(i30, u3, gfma(i20, u2, gfma(i10, u1, u0)));
-            if constexpr (RS == 4) {
-                // f64: one block row at a time -- its panel row, its A operand, its
-                // blocks' updates -- so that the accumulators (8 per block) and
-                // the step's operands fit two waves per SIMD
+            if constexpr (STREAM) {
+                // one block row at a time -- its panel row, its A operand, its
+                // blocks' updates -- so that the accumulators and the step's
+                // operands fit two waves per SIMD
 #pragma unroll
                 for (int RB = KB; RB < NB; ++RB) {
                     const V4 x = *reinterpret_cast<const V4*>(pan + 4 * (16 * RB + col_l));
@@ -250,6 +257,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_wav
     using V4 = typename GM<T>::V4;
     using V2 = typename GM<T>::V2;
     constexpr int RS = GM<T>::RS, RG = GM<T>::RG;
+    constexpr bool GM_STREAM = gm_stream(NB, sizeof(T));
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wpb = blockDim.x >> 6;
     // wave-uniform by construction; readfirstlane tells the compiler, so every
@@ -378,10 +386,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_wav
             ahi = ah2;
         }
         const int kbase = alo * (alo + 1) / 2, nbp = npairs(alo, ahi);
-        if constexpr (RS == 4 && MP) {
-            // f64, staged in passes (earlier passes' accumulators live): one pair
-            // per lane, P streamed a row at a time into Ha P (3 x 6) -- 36 + 12
-            // registers instead of the 6 x 6 block's 72
+        if constexpr (MP && GM_STREAM) {
+            // staged in passes (earlier passes' accumulators live): one pair per
+            // lane, P streamed a row at a time into Ha P (3 x 6) -- 18 + 6
+            // elements in registers instead of the 6 x 6 block's 36
             for (int kk = lane; kk < nbp; kk += 64) {
                 const int k = kbase + kk;
                 int a = (int)((__builtin_amdgcn_sqrtf(8.0f * (float)k + 1.0f) - 1.0f) * 0.5f);
@@ -391,11 +399,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_wav
                 const T* Pb = P + (slot[a] + coff[bo]);
                 const T* Ha = ht + 18 * a;
                 const T* Hb = ht + 18 * bo;
-                T t[3][6];
+                V2 t[3][3];   // Ha[x] P as three column pairs
 #pragma unroll
                 for (int x = 0; x < 3; ++x)
 #pragma unroll
-                    for (int c = 0; c < 6; ++c) t[x][c] = T(0);
+                    for (int c = 0; c < 3; ++c) t[x][c] = V2{0, 0};
 #pragma unroll
                 for (int u = 0; u < 6; ++u) {
                     T pr[6];
@@ -404,20 +412,26 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_wav
                     for (int x = 0; x < 3; ++x) {
                         const T h = Ha[6 * x + u];
 #pragma unroll
-                        for (int c = 0; c < 6; ++c) t[x][c] = gfma(h, pr[c], t[x][c]);
+                        for (int c = 0; c < 3; ++c)
+                            t[x][c] = __builtin_elementwise_fma(V2{h, h}, V2{pr[2 * c], pr[2 * c + 1]}, t[x][c]);
                     }
                     __builtin_amdgcn_sched_barrier(0);   // one P row in flight
                 }
                 T* dst = stage + 9 * kk;
 #pragma unroll
-                for (int x = 0; x < 3; ++x)
+                for (int x = 0; x < 3; ++x) {
+                    const T t1[6] = {t[x][0].x, t[x][0].y, t[x][1].x, t[x][1].y, t[x][2].x, t[x][2].y};
+                    V2 y01 = {0, 0};
+                    T y2 = 0;
 #pragma unroll
-                    for (int y = 0; y < 3; ++y) {
-                        T v = 0;
-#pragma unroll
-                        for (int u = 0; u < 6; ++u) v = gfma(t[x][u], Hb[6 * y + u], v);
-                        dst[3 * x + y] = v;
+                    for (int u = 0; u < 6; ++u) {
+                        y01 = __builtin_elementwise_fma(V2{t1[u], t1[u]}, V2{Hb[u], Hb[6 + u]}, y01);
+                        y2 = gfma(t1[u], Hb[12 + u], y2);
                     }
+                    dst[3 * x] = y01.x;
+                    dst[3 * x + 1] = y01.y;
+                    dst[3 * x + 2] = y2;
+                }
             }
         } else
         for (int k0 = 0; k0 < nbp; k0 += 64 * BIF) {
