@@ -48,7 +48,7 @@ N_CHECK = 4                   # distinct problems the accuracy block compares wi
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=2048, help="independent filters per GPU per step")
     ap.add_argument("--N", type=int, default=30)
