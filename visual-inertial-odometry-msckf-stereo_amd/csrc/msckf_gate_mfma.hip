@@ -280,25 +280,40 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_wav
     T* stage = area;                       // [capb][9] Y blocks of one pass (row-major lower block order)
     T* pan = area;                         // [16 NB][4] panel rows (after the Y phase)
     int* slot = reinterpret_cast<int*>(area + gm_area(Mmax, capb, RS));
-    const T* ws = fb.obs_ht + (size_t)o0 * OBS_HTS;
-    for (int e = lane; e < 18 * M; e += 64) {
-        const int o = e / 18;
-        ht[e] = ws[(size_t)o * OBS_HTS + OBS_HT + (e - 18 * o)];
-    }
+    // The feature's gating records ([M][OBS_HTS] from k_feature: Ht 3 x 6, r~, r_n)
+    // as element pairs, and its cam slots: every global load issued before the
+    // first wait (one round trip instead of one per loop trip), then scattered
+    // into the LDS rows ht [M][18] / rt [M][4].
+    int* coff = slot + ((Mmax + 3) & ~3);
     T rn2 = 0;
-    for (int e = lane; e < 4 * M; e += 64) {
-        const T v = ws[(size_t)(e >> 2) * OBS_HTS + OBS_RT + (e & 3)];
-        rt[e] = v;
-        if ((e & 3) == 3) rn2 += v * v;
+    {
+        constexpr int MCAP = (16 * NB - 4) / 3;   // the class's largest M (gm_class_exact)
+        constexpr int NCH = (12 * MCAP + 63) / 64;
+        static_assert(OBS_HT == 0 && OBS_RT == 18 && OBS_HTS == 24, "record layout");
+        const V2* src = reinterpret_cast<const V2*>(fb.obs_ht + (size_t)o0 * OBS_HTS);
+        V2 cv[NCH];
+#pragma unroll
+        for (int j = 0; j < NCH; ++j) {
+            const int k = lane + 64 * j;
+            cv[j] = k < 12 * M ? src[k] : V2{0, 0};
+        }
+        const int sl = lane < M ? fb.obs_cam[o0 + lane] : 0;
+#pragma unroll
+        for (int j = 0; j < NCH; ++j) {
+            const int k = lane + 64 * j, o = k / 12, e = 2 * (k - 12 * o);   // elements e, e + 1 of record o
+            if (k < 12 * M) {
+                if (e < OBS_RT) *reinterpret_cast<V2*>(ht + 18 * o + e) = cv[j];
+                else if (e < OBS_RT + 4) *reinterpret_cast<V2*>(rt + 4 * o + (e - OBS_RT)) = cv[j];
+                if (e == OBS_RT + 2) rn2 += cv[j].y * cv[j].y;   // r_n
+            }
+        }
+        // P offsets of the observations' cam blocks: row part (21 + 6 s) ldp + 21, column part 6 s
+        if (lane < M) {
+            slot[lane] = (21 + 6 * sl) * st.Dmax + 21;
+            coff[lane] = 6 * sl;
+        }
     }
     rn2 = wave_sum(rn2);
-    // P offsets of the observations' cam blocks: row part (21 + 6 s) ldp + 21, column part 6 s
-    int* coff = slot + ((Mmax + 3) & ~3);
-    for (int i = lane; i < M; i += 64) {
-        const int sl = fb.obs_cam[o0 + i];
-        slot[i] = (21 + 6 * sl) * st.Dmax + 21;
-        coff[i] = 6 * sl;
-    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 
     constexpr int NBLK = NB * (NB + 1) / 2;
