@@ -559,13 +559,26 @@ __global__ void __launch_bounds__(256) k_gate_mfma_wg(DevState<float> st, Params
     float* pan = ht + gm_head(Mmax);               // [2][16 GW_NB][4]
     float* stage = pan + gw_pan();                 // [capb][9]
     int* slot = reinterpret_cast<int*>(stage + ((9 * capb + 3) & ~3));
-    const float* ws = fb.obs_ht + (size_t)o0 * OBS_HTS;
-    for (int e = tid; e < 18 * M; e += 256) {
-        const int o = e / 18;
-        ht[e] = ws[(size_t)o * OBS_HTS + OBS_HT + (e - 18 * o)];
+    {   // records as element pairs and cam slots, all loads issued before the first wait (as k_gate_mfma)
+        constexpr int NCH = (12 * 84 + 255) / 256;   // gm_nb(M) <= GW_NB: M <= 84
+        const F2* src = reinterpret_cast<const F2*>(fb.obs_ht + (size_t)o0 * OBS_HTS);
+        F2 cv[NCH];
+#pragma unroll
+        for (int j = 0; j < NCH; ++j) {
+            const int k = tid + 256 * j;
+            cv[j] = k < 12 * M ? src[k] : F2{0, 0};
+        }
+        const int sl = tid < M ? fb.obs_cam[o0 + tid] : 0;
+#pragma unroll
+        for (int j = 0; j < NCH; ++j) {
+            const int k = tid + 256 * j, o = k / 12, e = 2 * (k - 12 * o);
+            if (k < 12 * M) {
+                if (e < OBS_RT) *reinterpret_cast<F2*>(ht + 18 * o + e) = cv[j];
+                else if (e < OBS_RT + 4) *reinterpret_cast<F2*>(rt + 4 * o + (e - OBS_RT)) = cv[j];
+            }
+        }
+        if (tid < M) slot[tid] = sl;
     }
-    for (int e = tid; e < 4 * M; e += 256) rt[e] = ws[(size_t)(e >> 2) * OBS_HTS + OBS_RT + (e & 3)];
-    for (int i = tid; i < M; i += 256) slot[i] = fb.obs_cam[o0 + i];
     __syncthreads();
     float rn2 = 0;
     for (int e = 4 * lane + 3; e < 4 * M; e += 256) rn2 += rt[e] * rt[e];
