@@ -2247,10 +2247,26 @@ __global__ void __launch_bounds__(64 * IM_NW) k_info_mfma(DevState<T> st, FeatBa
     int* s_n = sobs + maxobs;
     const int fbeg = fb.feat_off[b], fend = fb.feat_off[b + 1], nf = fend - fbeg;
     const int obeg = fb.obs_off[fbeg], nobs = fb.obs_off[fend] - obeg;
-    for (int e = tid; e < nobs; e += NT) sobs[e] = fb.obs_cam[obeg + e];
+    // the filter's obs_cam and feature metadata: four trips' loads issued before
+    // their LDS stores (one memory round trip per 4 NT entries, not per NT)
+    for (int e0 = 0; e0 < nobs; e0 += 4 * NT) {
+        int v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int e = e0 + NT * u + tid;
+            v[u] = e < nobs ? fb.obs_cam[obeg + e] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int e = e0 + NT * u + tid;
+            if (e < nobs) sobs[e] = v[u];
+        }
+    }
     for (int f = tid; f < nf; f += NT) {
-        fo0[f] = fb.obs_off[fbeg + f];
-        fM[f] = fb.include[fbeg + f] ? fb.obs_off[fbeg + f + 1] - fo0[f] : 0;
+        const int a0 = fb.obs_off[fbeg + f], a1 = fb.obs_off[fbeg + f + 1];
+        const bool inc = fb.include[fbeg + f];
+        fo0[f] = a0;
+        fM[f] = inc ? a1 - a0 : 0;
     }
     for (int e = tid; e < KR * IM_GS; e += NT) buf[e] = 0.0;
     for (int e = tid; e < 32 * KF; e += NT) posc[e] = -1;
