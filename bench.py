@@ -387,9 +387,23 @@ def ate_leg():
                         "tests/golden/sequence_s1.npz; fp64, host loop + one filter per call" % len(traj)}
 
 
+def gather_devices(grp, mine):
+    """Every rank's (device index, PCI bus id), in rank order; the replicas
+    must sit on distinct GPUs (one process per GPU)."""
+    devs = grp.all_gather({"rank": grp.rank, "local_rank": grp.local_rank, "device": mine[0], "pci_bus_id": mine[1]})
+    if grp.rank == 0 and len({d["pci_bus_id"] for d in devs}) != len(devs):
+        raise SystemExit("bench.py: replicas share a GPU: %s" % devs)
+    return devs
+
+
 def stub_main(args, grp):
     """--stub (tests only): the launch / barrier / max-over-ranks path with a
-    CPU stand-in for a step (rank r sleeps 2 (r + 1) ms per step)."""
+    CPU stand-in for a step (rank r sleeps 2 (r + 1) ms per step) and for the
+    device (index = local rank, bus id 'stub:<local rank>')."""
+    devs = gather_devices(grp, (grp.local_rank, "stub:%d" % grp.local_rank))
+    cpu = None
+    if grp.rank == 0 and not args.no_cpu:
+        cpu = {"value": None, "unit": "updates/s", "cores": 1, "kind": "port", "sample": "stub (not a measurement)"}
     grp.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -401,7 +415,7 @@ def stub_main(args, grp):
                                                                                       args.steps, el),
                           "unit": "updates/s", "n_gpus": grp.world, "steps": args.steps, "warmup": args.warmup,
                           "ms_per_step": round(el / args.steps * 1e3, 3), "data": "stub (no GPU, not a measurement)",
-                          "ranks_seconds_max": el}), flush=True)
+                          "ranks_seconds_max": el, "devices": devs, "cpu_baseline": cpu}), flush=True)
 
 
 def main():
@@ -420,10 +434,11 @@ def main():
     dtype = np.float32 if args.dtype == "fp32" else np.float64
     probs = make_problems(args, rank, min(args.unique, args.batch))
     cpu, refs = None, []
-    if rank == 0 and grp.world == 1 and not args.no_cpu:   # before this process initialises the GPU
+    if rank == 0 and not args.no_cpu:   # before this process initialises the GPU (any world size)
         cpu, refs = cpu_baseline(args, probs[:N_CHECK])
 
     ctx, feat_off = build_batch(args, probs, dtype, grp.local_rank)
+    devs = gather_devices(grp, ctx.device_info())
     el, times = timed_update(ctx, args, grp)
     value = replicas.whole_job_rate(args.batch, grp.world, args.steps, el)
     acc, gam, pw, valid, rows = ctx.batch_results()
@@ -440,6 +455,7 @@ def main():
                                % (args.N, args.F, args.batch),
                    "cam_states": args.N, "features": args.F, "filters_per_gpu": args.batch,
                    "stacked_rows_mean": float(np.mean(rows)), "parallelism": "replicas%d" % grp.world},
+        "devices": devs,
         "roofline": roofline_of(times, fl, args, args.dtype),
         "kernel_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in sorted(times.items(), key=lambda kv: -kv[1][0])},
         "canonical_gflop_per_update": round(fl["canonical"] / args.batch / 1e9, 4),

@@ -62,6 +62,11 @@ int msckf_create(const msckf_config_t* cfg, int hip_device, int scalar_bytes,
 int msckf_destroy(msckf_ctx_t* ctx);
 const char* msckf_last_error(void);
 int msckf_scalar_bytes(const msckf_ctx_t* ctx);
+/* The HIP device the context runs on (hipGetDevice after selecting it) and
+ * its PCI bus id ("dddd:bb:dd.f", hipDeviceGetPCIBusId) -- recorded by the
+ * multi-GPU bench so that every replica's device is in its output.  No
+ * reference counterpart (the reference has no device). */
+int msckf_device_info(const msckf_ctx_t* ctx, int* device_out, char* pci_bus_id, int cap);
 
 /* Whole-state upload / download of one filter slot (initialisation, resets,
  * publish msckf.py:888-908, keyframe selection msckf.py:691-727, tests).

@@ -297,7 +297,7 @@ def check_fp32_batch(problems, cap):
         thr = np.array([chi2_threshold(m - 1) for m in problems[b].track_lengths()])
         flip = both & (acc[sl] != acc_o)
         assert (np.abs(gam_o[flip] / thr[flip] - 1) < 0.05).all(), (gam_o[flip], thr[flip])
-        assert flip.mean() <= 0.02
+        assert flip.mean() <= 0.01
         d32 = rounded(d)
         st_f, acc_f, _, _, _ = oracle_update(d32, tri=(pw[sl], valid[sl]), accept=acc[sl] & valid[sl], sigma2=s2)
         imu, cams, P = ctx.get_state(b)
@@ -330,7 +330,7 @@ def test_batched_fp32_50x400_vs_oracle():
 def test_batched_fp32_80x1000_vs_oracle():
     """BASELINE config 5 shape (80 cams x 1000 features, fp32): tracks up to
     80 observations (two per lane in k_feature), 16-block workgroup gating."""
-    problems = [synth.make_update_problem(80, 1000, seed=260)]
+    problems = [synth.make_update_problem(80, 1000, seed=260 + b) for b in range(2)]
     check_fp32_batch(problems, 80)
 
 
@@ -341,7 +341,9 @@ def test_gate_fp32_gamma_vs_oracle(N, F, B):
     single- and multi-pass Y staging); N = 82: also the four-wave workgroup
     kernel for 40 < M <= 82 (up to 16 blocks, Y staged in passes).  Tolerance:
     fp32 with the saddle point's conditioning (~1e3) -- median relative error
-    <= 1e-4, 99th percentile <= 1e-2."""
+    <= 1e-4, 99th percentile <= 1e-3; decisions: at most 1 % of the features
+    differ, and only where the oracle's gamma is within 5 % of the threshold."""
+    from msckf_amd import chi2_threshold
     problems = [synth.make_update_problem(N, F, seed=300 + b) for b in range(B)]
     ctx, ds, feat_off, acc, gam, pw, valid, rows = _batched(problems, np.float32)
     errs = []
@@ -352,13 +354,18 @@ def test_gate_fp32_gamma_vs_oracle(N, F, B):
         g, go = gam[sl][ok], gam_o[ok]
         assert np.isfinite(g).all()
         errs.append(np.abs(g - go) / np.maximum(np.abs(go), 1e-6))
+        thr = np.array([chi2_threshold(m - 1) for m in problems[b].track_lengths()])[ok]
+        flip = acc[sl][ok].astype(bool) != acc_o[ok].astype(bool)
+        assert flip.mean() <= 0.01, flip.mean()
+        assert (np.abs(go[flip] / thr[flip] - 1) < 0.05).all()
     e = np.concatenate(errs)
     assert e.size > 40
+    print("fp32 gamma rel err: median %.2e p99 %.2e max %.2e" % (np.median(e), np.quantile(e, 0.99), e.max()))
     assert np.median(e) < 1e-4, np.median(e)
-    assert np.quantile(e, 0.99) < 1e-2, np.quantile(e, 0.99)
+    assert np.quantile(e, 0.99) < 1e-3, np.quantile(e, 0.99)
 
 
-@pytest.mark.parametrize("N,F,B", [(40, 150, 2)])
+@pytest.mark.parametrize("N,F,B", [(40, 150, 2), (82, 50, 1)])
 def test_gate_fp64_gamma_vs_oracle(N, F, B):
     """fp64 gating against the oracle's gamma (msckf.py:606-614), relative
     1e-9: the one-wave fp64 MFMA kernel (v_mfma_f64_16x16x4_f64, its own
@@ -375,7 +382,7 @@ def test_gate_fp64_gamma_vs_oracle(N, F, B):
         np.testing.assert_allclose(gam[sl][ok], gam_o[ok], rtol=1e-9)
         np.testing.assert_array_equal(acc[sl], acc_o)
         n += int(ok.sum())
-    assert n > 200
+    assert n > 40
 
 
 def test_gate_fp32_scrambled_observation_order():

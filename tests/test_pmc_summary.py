@@ -1,0 +1,57 @@
+"""tools/pmc_summary.py: per-stage HBM traffic from rocprofv3 FETCH_SIZE /
+WRITE_SIZE passes.  Kernels in an anonymous namespace (the gate's size
+classes) must keep distinct keys and all be summed (round-2 VERDICT weak 1:
+cutting names at the first '(' collapsed them onto one key)."""
+import csv
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import pmc_summary  # noqa: E402
+
+ARGS = "(msckf::DevState<float>, msckf::Params<float>, msckf::FeatBatch<float>, int const*, int, int, int)"
+NAMES = ["void msckf::(anonymous namespace)::k_gate_mfma<float, 5, true>" + ARGS,
+         "void msckf::(anonymous namespace)::k_gate_mfma<float, 6, true>" + ARGS,
+         "void msckf::k_select<float>(msckf::DevState<float>, msckf::FeatBatch<float>, msckf::UpdWs<float>)"]
+
+
+def _csv(path, counter, vals):
+    with open(path, "w", newline="") as fh:
+        w = csv.writer(fh)
+        w.writerow(["Dispatch_Id", "Kernel_Name", "Counter_Name", "Counter_Value"])
+        i = 0
+        for step in range(2):
+            for n, v in zip(NAMES, vals):
+                w.writerow([i, n, counter, v])
+                i += 1
+
+
+def test_short_name_keeps_template_args():
+    assert pmc_summary.short_name(NAMES[0]) == "k_gate_mfma<float, 5, true>"
+    assert pmc_summary.short_name(NAMES[2]) == "k_select<float>"
+    assert pmc_summary.short_name("k_plain") == "k_plain"
+
+
+def test_anonymous_namespace_classes_are_summed(tmp_path):
+    f, w, o = tmp_path / "f.csv", tmp_path / "w.csv", tmp_path / "o.json"
+    _csv(f, "FETCH_SIZE", [100.0, 300.0, 1.0])     # KiB per dispatch
+    _csv(w, "WRITE_SIZE", [10.0, 20.0, 1.0])
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_summary.py"), str(f), str(w),
+                    "--dtype", "fp32", "-o", str(o)], check=True, capture_output=True)
+    d = json.load(open(o))
+    assert d["steps"] == 2
+    gate = d["stages"]["gate"]
+    assert set(gate["kernels"]) == {"k_gate_mfma<float, 5, true>", "k_gate_mfma<float, 6, true>"}
+    assert all(k["dispatches"] == 2 for k in gate["kernels"].values())
+    # per step: FETCH 100 + 300 KiB, WRITE 10 + 20 KiB
+    assert gate["bytes_per_step"] == (400 + 30) * 1024
+    assert gate["fetch_x2_bytes_per_step"] == (800 + 30) * 1024
+
+
+def test_committed_summary_has_every_gate_class():
+    d = json.load(open(os.path.join(ROOT, "profiles", "pmc_summary.json")))
+    gate = d["stages"]["gate"]["kernels"]
+    assert "" not in gate and len(gate) >= 2, sorted(gate)

@@ -108,6 +108,52 @@ def test_bench_spawns_ranks():
     assert line["n_gpus"] == 2
     assert line["ms_per_step"] >= 4.0              # rank 1 sleeps 4 ms per step
     assert line["value"] == pytest.approx(2048 * 2 * 5 / line["ranks_seconds_max"])
+    # every replica's device is in the line, one per rank, all distinct
+    assert [d["rank"] for d in line["devices"]] == [0, 1]
+    assert [d["pci_bus_id"] for d in line["devices"]] == ["stub:0", "stub:1"]
+
+
+@pytest.mark.timeout(120)
+def test_bench_keeps_cpu_baseline_at_world2():
+    """Rank 0 computes the CPU baseline before it touches the GPU whatever
+    the world size, so an N > 1 line carries it too."""
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--stub", "--steps", "2"],
+                         capture_output=True, text=True, timeout=100,
+                         env={k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")})
+    assert out.returncode == 0, out.stderr
+    line = _json_line(out.stdout)
+    assert line["n_gpus"] == 2 and line["cpu_baseline"] is not None
+
+
+_FAILING = textwrap.dedent("""
+    import sys, time
+    sys.path.insert(0, %r)
+    import msckf_pkg
+    from msckf_amd import replicas
+    grp = replicas.init()
+    if grp.rank == 1:
+        sys.exit(3)          # dies before its first collective
+    grp.barrier()            # rank 0 would wait here for the hub's whole timeout
+""") % ROOT
+
+
+@pytest.mark.timeout(60)
+def test_spawn_fails_fast_when_a_rank_dies():
+    script = os.path.join(ROOT, "tests", "_replica_failing.py")
+    with open(script, "w") as fh:
+        fh.write(_FAILING)
+    try:
+        import time
+        t0 = time.time()
+        out = subprocess.run([sys.executable, "-c",
+                              "import sys; sys.path.insert(0, %r); import msckf_pkg; from msckf_amd import replicas; "
+                              "sys.exit(replicas.spawn([%r], 2))" % (ROOT, script)],
+                             capture_output=True, text=True, timeout=50)
+        el = time.time() - t0
+    finally:
+        os.unlink(script)
+    assert out.returncode != 0      # rank 1's 3, or rank 0's error once the hub drops it
+    assert el < 30
 
 
 @pytest.mark.timeout(180)
@@ -123,6 +169,7 @@ def test_bench_under_external_launcher():
     assert out.returncode == 0, out.stderr[-3000:]
     line = _json_line(out.stdout)
     assert line["n_gpus"] == 2 and line["ms_per_step"] >= 4.0
+    assert sorted(d["local_rank"] for d in line["devices"]) == [0, 1]
 
 
 def test_bench_rejects_gpus_mismatch():

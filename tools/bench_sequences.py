@@ -10,7 +10,8 @@ frames/s of both, the batched launch counts, and ATE vs ground truth.
         tools/bench_sequences.py --seqs 11      # sequences dealt round-robin over N GPUs
 
 On N GPUs every rank replays its share of the sequences (replicas.shard) on
-its own device; RCCL carries only the barriers, the max of the elapsed time
+its own device; the replicas' host TCP hub (msckf_amd.replicas, no RCCL:
+no data crosses GPUs) carries only the barriers, the max of the elapsed time
 and the sum of the frame counts (SURVEY config 4: no cross-GPU state).
 """
 import argparse

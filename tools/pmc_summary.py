@@ -38,6 +38,31 @@ def stage_of(name):
     return None
 
 
+def short_name(name):
+    """Kernel name without its return type, namespaces and argument list:
+    'void msckf::(anonymous namespace)::k_gate_mfma<float, 6, true>(msckf::...)'
+    -> 'k_gate_mfma<float, 6, true>'.  The argument list is the LAST top-level
+    parenthesis group (the '(anonymous namespace)' qualifier also has one, so
+    cutting at the first '(' would collapse every anonymous-namespace kernel
+    to one key)."""
+    n = name.strip()
+    depth, cut = 0, len(n)
+    for i in range(len(n) - 1, -1, -1):
+        c = n[i]
+        if c == ")":
+            depth += 1
+        elif c == "(":
+            depth -= 1
+            if depth == 0:
+                cut = i
+                break
+    n = n[:cut] if cut < len(n) and n.endswith(")") else n
+    n = n.replace("(anonymous namespace)::", "")
+    if n.startswith("void "):
+        n = n[5:]
+    return n.replace("msckf::", "")
+
+
 def read(path):
     out = defaultdict(float)
     count = defaultdict(int)
@@ -76,7 +101,8 @@ def main():
         d = stages.setdefault(st, {"fetch_kib": 0.0, "write_kib": 0.0, "kernels": {}})
         d["fetch_kib"] += fetch.get(name, 0.0)
         d["write_kib"] += write.get(name, 0.0)
-        short = re.sub(r"\(.*", "", name).replace("void msckf::", "")
+        short = short_name(name)
+        assert short not in d["kernels"], "kernel key collision: %s" % short
         d["kernels"][short] = {"dispatches": nf.get(name, nw.get(name, 0)),
                                "fetch_kib": fetch.get(name, 0.0), "write_kib": write.get(name, 0.0)}
     # every kernel of a stage runs once per update step: per-dispatch averages

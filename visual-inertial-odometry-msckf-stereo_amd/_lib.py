@@ -54,6 +54,7 @@ _SIGS = {
     "msckf_destroy": (C.c_int, [_P]),
     "msckf_last_error": (C.c_char_p, []),
     "msckf_scalar_bytes": (C.c_int, [_P]),
+    "msckf_device_info": (C.c_int, [_P, _I, C.c_char_p, C.c_int]),
     "msckf_set_state": (C.c_int, [_P, C.c_int, _D, C.c_int, _D, _D]),
     "msckf_get_state": (C.c_int, [_P, C.c_int, _D, _D, _D, _I]),
     "msckf_get_cov_diag": (C.c_int, [_P, C.c_int, C.c_int, C.c_int, _D]),
@@ -329,6 +330,14 @@ class Context:
         self._check(self.lib.msckf_batch_results(self.h, _ptr(acc, C.c_uint8), _ptr(gam, C.c_double),
                                                  _ptr(p, C.c_double), _ptr(v, C.c_uint8), _ptr(rows, C.c_int32)))
         return acc.astype(bool), gam, p, v.astype(bool), rows
+
+    def device_info(self):
+        """(HIP device index, PCI bus id) this context runs on."""
+        dev = np.zeros(1, np.int32)
+        buf = C.create_string_buffer(64)
+        with self.lock:
+            self._check(self.lib.msckf_device_info(self.h, _ptr(dev, C.c_int32), buf, 64))
+        return int(dev[0]), buf.value.decode()
 
     def snapshot(self):
         self._check(self.lib.msckf_snapshot(self.h))

@@ -358,9 +358,20 @@ int run_update_chain(msckf_ctx* c, int row_cap, bool triangulate) {
     }
     // stage A (register-tile windows) under the Jacobians and gating
     const bool early_a = kalman_chol_supported(c->Cmax);
+    // Once stage A is on the side stream, every exit path joins it: an early
+    // return must not leave k_kal_a reading P while a later call (restore,
+    // set_state) on the main stream overwrites it.
+    struct SideJoin {
+        msckf_ctx* c;
+        bool armed = false;
+        ~SideJoin() {
+            if (armed) (void)hipStreamSynchronize(c->side);
+        }
+    } join{c};
     if (early_a) {
         HIPC(hipEventRecord(c->ev_fork, s));
         HIPC(hipStreamWaitEvent(c->side, c->ev_fork, 0));
+        join.armed = true;
         launch_kalman_a_reg<T>(c->side, st, ws, &c->timer);
         HIPC(hipEventRecord(c->ev_join, c->side));
     }
@@ -376,7 +387,10 @@ int run_update_chain(msckf_ctx* c, int row_cap, bool triangulate) {
     c->timer.begin(s, "compress");
     launch_compress<T>(s, st, fb, ws, c->max_nf, c->max_obs);
     c->timer.end(s);
-    if (early_a) HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
+    if (early_a) {
+        HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
+        join.armed = false;   // the main stream now orders everything after stage A
+    }
     launch_kalman<T>(s, st, prm, ws, &c->timer);
     HIPC(hipGetLastError());
     return 0;
@@ -778,6 +792,16 @@ int msckf_destroy(msckf_ctx_t* c) {
 }
 
 int msckf_scalar_bytes(const msckf_ctx_t* c) { return c ? c->scalar : 0; }
+
+int msckf_device_info(const msckf_ctx_t* c, int* device_out, char* pci_bus_id, int cap) {
+    if (!c) FAIL(-1, "null context");
+    HIPC(hipSetDevice(c->device));
+    int dev = -1;
+    HIPC(hipGetDevice(&dev));
+    if (device_out) *device_out = dev;
+    if (pci_bus_id && cap > 0) HIPC(hipDeviceGetPCIBusId(pci_bus_id, cap, dev));
+    return 0;
+}
 
 int msckf_set_state(msckf_ctx_t* c, int filter, const double* imu, int n_cams, const double* cams, const double* P) {
     if (int r = check_ctx(c, filter)) return r;

@@ -85,8 +85,11 @@ class Hub:
                 if len(ops) != 1:
                     raise RuntimeError("replica hub: ranks disagree on the collective: %s" % sorted(ops))
                 op = ops.pop()
-                vals = [float(m.get("v", 0.0)) for m in msgs]
-                res = {"max": max(vals), "sum": sum(vals)}.get(op, 0.0)
+                if op == "gather":   # every rank's JSON value, in rank order
+                    res = [m.get("v") for m in msgs]
+                else:
+                    vals = [float(m.get("v", 0.0)) for m in msgs]
+                    res = {"max": max(vals), "sum": sum(vals)}.get(op, 0.0)
                 for c, _ in order:
                     _send(c, {"v": res})
                 if op == "close":
@@ -125,6 +128,14 @@ class ReplicaGroup:
     def sum_over_ranks(self, x: float) -> float:
         """SUM over ranks of one float (e.g. frames processed by every rank)."""
         return self._call("sum", x)
+
+    def all_gather(self, obj):
+        """Every rank's JSON-serialisable ``obj``, in rank order (control
+        data only: e.g. the device each replica ran on)."""
+        if self._sock is None:
+            return [obj]
+        _send(self._sock, {"op": "gather", "v": obj})
+        return list(self._lines.read()["v"])
 
     def close(self):
         if self._sock is not None:
@@ -193,7 +204,10 @@ def init() -> ReplicaGroup:
 def spawn(argv: List[str], n: int, env_extra: Optional[dict] = None) -> int:
     """Runs ``python argv...`` as n ranks (one per GPU) from a parent that
     never initialises the GPU; the parent hosts the hub.  Returns the first
-    non-zero exit code of the ranks (0 if all succeed)."""
+    non-zero exit code of the ranks (0 if all succeed).  The children are
+    polled: the first one to fail ends the job -- the others (blocked in a
+    hub read or its accept) are terminated instead of waiting out the hub's
+    timeout."""
     hub = Hub(n)
     procs = []
     for r in range(n):
@@ -203,9 +217,26 @@ def spawn(argv: List[str], n: int, env_extra: Optional[dict] = None) -> int:
                    MASTER_ADDR="127.0.0.1")
         env[HUB_ENV] = hub.address
         procs.append(subprocess.Popen([sys.executable] + list(argv), env=env))
-    codes = [p.wait() for p in procs]
-    hub.thread.join(timeout=30)
-    return next((c for c in codes if c != 0), 0)
+    first_bad = 0
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad and not first_bad:
+            first_bad = bad[0]
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            try:
+                hub.srv.close()
+            except OSError:
+                pass
+        if all(c is not None for c in codes):
+            break
+        time.sleep(0.05)
+    for p in procs:
+        p.wait()
+    hub.thread.join(timeout=5 if first_bad else 30)
+    return first_bad or next((c for c in codes if c != 0), 0)
 
 
 def problem_seeds(rank: int, unique: int) -> List[int]:

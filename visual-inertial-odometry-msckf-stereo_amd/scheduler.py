@@ -40,14 +40,27 @@ _ORDER = {"set_state": 0, "propagate": 1, "augment": 2, "triangulate": 3, "updat
 class MultiMSCKF:
     """``n`` filters (one per sequence) on one device context."""
 
-    def __init__(self, n, config=None, dtype=np.float64, device=0, cam_capacity=None):
+    def __init__(self, n, config=None, dtype=np.float64, device=0, cam_capacity=None, lane_configs=None):
+        """``lane_configs`` (optional, one per lane): per-sequence host-side
+        settings (check_motion's translation threshold, online_reset's
+        position std threshold, window size).  The device context is shared,
+        so every lane must agree on what the device computes with (noise,
+        extrinsics, LM parameters: the C-ABI msckf_config_t)."""
         config = config or FilterConfig()
         if not isinstance(config, FilterConfig):
             config = FilterConfig.from_reference(config)
-        cap = cam_capacity or (config.max_cam_state_size + 2)
-        self.config = config
-        self.ctx = _lib.Context(config, n_filters=n, n_cam_capacity=cap, dtype=dtype, device=device)
-        self.lanes = [MSCKF(config, ctx=self.ctx, slot=i) for i in range(n)]
+        cfgs = [config] * n if lane_configs is None else [
+            c if isinstance(c, FilterConfig) else FilterConfig.from_reference(c) for c in lane_configs]
+        if len(cfgs) != n:
+            raise ValueError("%d lane configs for %d lanes" % (len(cfgs), n))
+        dev0 = bytes(_lib.make_config(cfgs[0]))
+        for i, c in enumerate(cfgs):
+            if bytes(_lib.make_config(c)) != dev0:
+                raise ValueError("lane %d: device-side filter parameters differ from lane 0's" % i)
+        cap = cam_capacity or max(c.max_cam_state_size for c in cfgs) + 2
+        self.config = cfgs[0]
+        self.ctx = _lib.Context(cfgs[0], n_filters=n, n_cam_capacity=cap, dtype=dtype, device=device)
+        self.lanes = [MSCKF(cfgs[i], ctx=self.ctx, slot=i) for i in range(n)]
         self.launches = defaultdict(int)       # batched device calls per request kind
 
     def __len__(self):
