@@ -458,14 +458,16 @@ def _run_sequence(flt, seq):
     return np.array(recs)
 
 
-@pytest.mark.parametrize("name", ["sequence_s1", "sequence_s2", "sequence_s3"])
+@pytest.mark.parametrize("name", ["sequence_s1", "sequence_s2", "sequence_s3", "sequence_s4"])
 def test_sequence_golden(name):
     """The reference filter's runs, reproduced through the drop-in MSCKF
     class: identical gating decisions, stacked-H shapes and online-reset
     frames, state and covariance norm within 1e-6 relative (north star
     tolerance).  s1: EuRoC config, 200 frames; s2: check_motion at translation
     threshold 0.2 (feature.py:124-165); s3: online_reset firing at position
-    std 0.11 m (msckf.py:859-886)."""
+    std 0.11 m (msckf.py:859-886); s4: 180 frames whose covariance the
+    reference's non-Joseph update leaves indefinite at rounding level (stage A
+    factors P_cc with a pivot floor, msckf_kalman.hip pcc_pivot_floor)."""
     g = golden(name)
     seq = synth.make_sequence(int(g["n_frames"]), int(g["seed"]))
     flt = msckf_amd.MSCKF(sequence_config(g))

@@ -144,12 +144,17 @@ def test_check_motion():
     assert 0 < g["ok_4"].sum() < g["ok_2"].sum() < g["ok_m1"].sum()
 
 
-@pytest.mark.parametrize("name", ["sequence_s1", "sequence_s2", "sequence_s3"])
+@pytest.mark.parametrize("name", ["sequence_s1", "sequence_s2", "sequence_s3", "sequence_s4"])
 def test_sequence(name):
     """Synthetic stereo+IMU streams through the whole filter: every gating
     decision and stacked-H shape identical, state to 1e-9.  s1: EuRoC config
     (200 frames); s2: check_motion at translation threshold 0.2; s3:
-    online_reset firing (position std threshold 0.11 m)."""
+    online_reset firing (position std threshold 0.11 m); s4: a stream whose
+    covariance the reference's non-Joseph update (msckf.py:598-604) leaves
+    indefinite at rounding level -- there the reference is ill-conditioned
+    and a mere change of BLAS summation order (numpy here vs the reference's
+    own run) moves the state by ~2e-8 and |P|_F by ~5e-7, so s4 is held to
+    the north-star tolerance (1e-6 relative per frame) instead."""
     from msckf_amd import synth, chi2_threshold
     g = golden(name)
     seq = synth.make_sequence(int(g["n_frames"]), int(g["seed"]))
@@ -166,7 +171,14 @@ def test_sequence(name):
     np.testing.assert_array_equal(np.array(orc.gate_log), g["gates"])
     np.testing.assert_array_equal(np.array(orc.shape_log), g["shapes"])
     assert rec.shape == g["rec"].shape
-    np.testing.assert_allclose(rec, g["rec"], rtol=1e-9, atol=1e-10)
-    assert rel(orc.st.P, g["P_final"]) < 1e-9
+    if name == "sequence_s4":
+        ref = g["rec"]
+        for k in range(len(ref)):
+            assert np.linalg.norm(rec[k, 1:29] - ref[k, 1:29]) <= 1e-7 * np.linalg.norm(ref[k, 1:29]), k
+            assert abs(rec[k, 29] - ref[k, 29]) <= 1e-6 * ref[k, 29], k
+        assert rel(orc.st.P, g["P_final"]) < 1e-6
+    else:
+        np.testing.assert_allclose(rec, g["rec"], rtol=1e-9, atol=1e-10)
+        assert rel(orc.st.P, g["P_final"]) < 1e-9
     if "resets" in g:
         np.testing.assert_array_equal(orc.resets, g["resets"])

@@ -346,6 +346,10 @@ JOBS = {
     "sequence_s2": lambda: gen_sequence("sequence_s2", 120, 2, translation_threshold=0.2),
     # online_reset firing: position std threshold 0.11 m instead of 8 m (config.py:64)
     "sequence_s3": lambda: gen_sequence("sequence_s3", 100, 2, position_std_threshold=0.11),
+    # the reference's non-Joseph update leaves P_cc indefinite at rounding level
+    # (min eigenvalue ~ -2e-12 from frame 2 on); a Cholesky of P_cc without a
+    # pivot floor fails at frame 19 (found by the 11-lane config-4 test)
+    "sequence_s4": lambda: gen_sequence("sequence_s4", 180, 307),
 }
 
 if __name__ == "__main__":

@@ -409,12 +409,12 @@ int read_results(msckf_ctx* c, uint8_t* accepted_out, double* gamma_out, double*
     if (p_w_out && nf) HIPC(download<T>(c, p_w_out, c->p_w.p, (size_t)nf * 3));
     std::vector<int> info(4 * c->B);
     HIPC(hipMemcpy(info.data(), c->info.p, info.size() * sizeof(int), hipMemcpyDeviceToHost));
-    int status = 0;
+    int bad = -1;
     for (int b = 0; b < c->B; ++b) {
         if (rows_out) rows_out[b] = info[4 * b];
-        if (info[4 * b + 3] < 0) status = -3;
+        if (info[4 * b + 3] < 0 && bad < 0) bad = b;
     }
-    if (status) FAIL(-3, "innovation covariance not positive definite");
+    if (bad >= 0) FAIL(-3, "innovation covariance not positive definite (filter slot %d, %d rows)", bad, info[4 * bad]);
     return 0;
 }
 

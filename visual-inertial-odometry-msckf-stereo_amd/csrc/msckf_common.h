@@ -274,5 +274,11 @@ __device__ __forceinline__ T wave_sum(T x) {
     for (int m = 32; m >= 1; m >>= 1) x += __shfl_xor(x, m, 64);
     return x;
 }
+template <typename T>
+__device__ __forceinline__ T wave_max(T x) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) x = fmax(x, __shfl_xor(x, m, 64));
+    return x;
+}
 
 }  // namespace msckf

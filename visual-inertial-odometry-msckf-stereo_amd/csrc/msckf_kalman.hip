@@ -30,6 +30,28 @@ __device__ __forceinline__ int round4(int x) { return (x + 3) & ~3; }
 
 typedef double v4d __attribute__((ext_vector_type(4)));
 
+// Pivot floor of the P_cc factorisations (stage A): KALMAN_PIVOT_FLOOR x the
+// largest cam-block variance.  The reference's (I - KH)P update (msckf.py:598-604,
+// not Joseph form) leaves P_cc indefinite at rounding level after a few frames
+// (smallest eigenvalue ~ -3e-10 x max diag on synthetic EuRoC-shaped streams);
+// the reference never factors P, so a pivot at or below zero must not abort the
+// update here.  Flooring it factors P_cc + E, E diagonal and ~1e-10 relative:
+// the update moves by that much, far inside the 1e-6 parity tolerance.
+constexpr double KALMAN_PIVOT_FLOOR = 1e-10;
+
+// workgroup reduction (all threads call; lds: >= 16 doubles of scratch, reused after)
+template <typename T>
+__device__ double pcc_pivot_floor(const T* P, int ld, int C, double* lds) {
+    double m = 0.0;
+    for (int i = threadIdx.x; i < C; i += blockDim.x) m = fmax(m, (double)P[(size_t)(21 + i) * ld + 21 + i]);
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = m;
+    __syncthreads();
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) m = fmax(m, lds[w]);
+    __syncthreads();
+    return m * KALMAN_PIVOT_FLOOR;
+}
+
 // ---- stage A: [P_cc P_ci; P_ic P_ii] in index space [cams (Cp) | IMU (24)] ----
 template <typename T, int NT, int TPL>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 ? 2 : 1))) k_kal_a(DevState<T> st, UpdWs<T> ws) {
@@ -56,7 +78,9 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 2
         dst[0] = w0; dst[1] = w1; dst[2] = w2; dst[3] = w3;
     };
     auto trail = [&](int i, int j, double v) { Sii[(i - Cp) * KW + (j - Cp)] = v; };
-    const bool ok = rchol_core<NT, TPL>(nrow, nrow, Cp / 4, reinterpret_cast<double*>(smem_raw), load, panel, trail);
+    const double floor = pcc_pivot_floor(P, ld, C, reinterpret_cast<double*>(smem_raw));
+    const bool ok = rchol_core<NT, TPL>(nrow, nrow, Cp / 4, reinterpret_cast<double*>(smem_raw), load, panel, trail,
+                                        floor);
     if (threadIdx.x == 0) ws.afail[b] = ok ? 0 : 1;   // read by k_kal_c1
 }
 
@@ -286,10 +310,18 @@ __global__ void __launch_bounds__(64) k_gchol_diag(DevState<T> st, UpdWs<T> ws, 
         const int i = e / nb, j = e - i * nb;
         d[i][j] = j <= i ? A[(size_t)(k + i) * ld + k + j] : 0.0;
     }
+    // stage A: pivots floored as in k_kal_a (pcc_pivot_floor)
+    double floor = 0.0;
+    if (STAGE == 0) {
+        const T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
+        for (int i = lane; i < nelim; i += 64) floor = fmax(floor, (double)P[(size_t)(21 + i) * st.Dmax + 21 + i]);
+        floor = wave_max(floor) * KALMAN_PIVOT_FLOOR;
+    }
     __syncthreads();
     bool bad = false;
     for (int j = 0; j < nb; ++j) {   // right-looking, lane i owns row i
-        const double piv = d[j][j];
+        double piv = d[j][j];
+        if (floor > 0.0 && !(piv >= floor)) piv = floor;
         if (!(piv > 0.0)) { bad = true; break; }
         const double l = sqrt(piv), inv = 1.0 / l;
         __syncthreads();

@@ -23,6 +23,11 @@ namespace msckf {
 // all 64 banks (a 128-B stride would put it on two).
 // load(i, j) must be symmetric on the square part (diagonal tiles read both
 // triangles).
+// floor > 0: a pivot below floor (or NaN) is replaced by floor instead of
+// failing -- the factorisation is then the exact one of A + E with E >= 0
+// diagonal, non-zero only at those pivots (a covariance that the reference's
+// non-Joseph update, msckf.py:598-604, has left indefinite at rounding level;
+// the reference never factors it, so it does not fail there either).
 // ===========================================================================
 constexpr int RB = 18;   // doubles per 4-row block of the LDS column buffer
 
@@ -30,7 +35,8 @@ constexpr int RB = 18;   // doubles per 4-row block of the LDS column buffer
 // instead of being called per element (lets a loader share operands).
 template <int NT, int TPL, class Load, class Panel, class Trail, bool TILE_LOAD = false>
 __device__ __forceinline__ bool rchol_core(int nrow, int ncol, int nelim, double* lds, Load load, Panel panel,
-                                           Trail trail) {
+                                           Trail trail, double floor = 0.0) {
+    auto fl = [floor](double x) { return (floor > 0.0 && !(x >= floor)) ? floor : x; };
     const int tid = threadIdx.x;
     const int ntiles = ncol * nrow - ncol * (ncol - 1) / 2;
     int crd[TPL], tlmax[TPL];
@@ -77,16 +83,16 @@ __device__ __forceinline__ bool rchol_core(int nrow, int ncol, int nelim, double
 #pragma unroll
                 for (int y = 0; y < 4; ++y) dst[4 * x + y] = a[s][x][y];
             if (RTI(s) == tj) {   // the diagonal tile's owner factors it once for everyone
-                const double l00 = sqrt(a[s][0][0]);
+                const double l00 = sqrt(fl(a[s][0][0]));
                 const double i00 = 1.0 / l00;
                 const double l10 = a[s][1][0] * i00, l20 = a[s][2][0] * i00, l30 = a[s][3][0] * i00;
-                const double l11 = sqrt(a[s][1][1] - l10 * l10);
+                const double l11 = sqrt(fl(a[s][1][1] - l10 * l10));
                 const double i11 = 1.0 / l11;
                 const double l21 = (a[s][2][1] - l20 * l10) * i11, l31 = (a[s][3][1] - l30 * l10) * i11;
-                const double l22 = sqrt(a[s][2][2] - l20 * l20 - l21 * l21);
+                const double l22 = sqrt(fl(a[s][2][2] - l20 * l20 - l21 * l21));
                 const double i22 = 1.0 / l22;
                 const double l32 = (a[s][3][2] - l30 * l20 - l31 * l21) * i22;
-                const double l33 = sqrt(a[s][3][3] - l30 * l30 - l31 * l31 - l32 * l32);
+                const double l33 = sqrt(fl(a[s][3][3] - l30 * l30 - l31 * l31 - l32 * l32));
                 const double i33 = 1.0 / l33;
                 fj[0] = l00; fj[1] = l10; fj[2] = l20; fj[3] = l30;
                 fj[4] = l11; fj[5] = l21; fj[6] = l31; fj[7] = l22;
