@@ -17,7 +17,17 @@ $(SRC)/%.o: $(SRC)/%.hip $(HDRS)
 $(LIB): $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
 
-clean:
-	rm -f $(OBJS) $(LIB)
+# probe build (tools/probes/): same sources with in-kernel phase timers
+PROBE    := tools/probes/libmsckf_probe.so
+POBJS    := $(patsubst $(SRC)/%.o,tools/probes/obj/%.o,$(OBJS))
+probe: $(PROBE)
+tools/probes/obj/%.o: $(SRC)/%.hip $(HDRS)
+	@mkdir -p tools/probes/obj
+	$(HIPCC) $(HIPFLAGS) -DMSCKF_GATE_PROBE -c $< -o $@
+$(PROBE): $(POBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(POBJS)
 
-.PHONY: all clean
+clean:
+	rm -f $(OBJS) $(LIB) $(PROBE)
+
+.PHONY: all clean probe

@@ -334,10 +334,12 @@ def test_batched_fp32_80x1000_vs_oracle():
     check_fp32_batch(problems, 80)
 
 
-@pytest.mark.parametrize("N,F,B", [(40, 150, 2), (82, 50, 1)])
-def test_gate_fp32_gamma_vs_oracle(N, F, B):
+@pytest.mark.parametrize("N,F,B,cap", [(30, 200, 2, 30), (40, 150, 2, None), (82, 50, 1, None)])
+def test_gate_fp32_gamma_vs_oracle(N, F, B, cap):
     """fp32 gating on MFMA tiles against the oracle's fp64 gamma
-    (msckf.py:606-614).  N = 40: every one-wave size class (1..8 16-row blocks,
+    (msckf.py:606-614).  N = 30 (cam capacity 30, the bench's): the
+    filter-resident kernel (P_cc in LDS, one workgroup per filter,
+    k_gate_res); N = 40: every one-wave size class (1..8 16-row blocks,
     single- and multi-pass Y staging); N = 82: also the four-wave workgroup
     kernel for 40 < M <= 82 (up to 16 blocks, Y staged in passes).  Tolerance:
     fp32 with the saddle point's conditioning (~1e3) -- median relative error
@@ -345,7 +347,7 @@ def test_gate_fp32_gamma_vs_oracle(N, F, B):
     differ, and only where the oracle's gamma is within 5 % of the threshold."""
     from msckf_amd import chi2_threshold
     problems = [synth.make_update_problem(N, F, seed=300 + b) for b in range(B)]
-    ctx, ds, feat_off, acc, gam, pw, valid, rows = _batched(problems, np.float32)
+    ctx, ds, feat_off, acc, gam, pw, valid, rows = _batched(problems, np.float32, cap=cap)
     errs = []
     for b, d in enumerate(ds):
         st, acc_o, tri_p, tri_ok, gam_o = oracle_update(d)
@@ -486,3 +488,29 @@ def test_sequence_golden(name):
     print("sequence: worst per-frame state deviation %.3e" % worst)
     assert rel(flt.state_cov(), g["P_final"]) < 1e-6
     np.testing.assert_array_equal(flt.reset_log, g["resets"] if "resets" in g else [])
+
+
+def test_gate_fp32_unordered_tracks():
+    """Tracks whose cam slots do not ascend (the reference always lists a
+    feature's observations in cam order, but the C-ABI takes any order): the
+    batch is routed to the per-feature gating kernels instead of the
+    filter-resident one (which reads P_cc blocks (a, b), a > b).  gamma is
+    invariant to the order of a feature's observations, so the reversed
+    tracks must gate like the ordered ones."""
+    p = synth.make_update_problem(20, 120, seed=411)
+    d = problem_to_dict(p)
+    st, acc_o, tri_p, tri_ok, gam_o = oracle_update(d)
+    sel = [f for f in range(p.F) if tri_ok[f]]
+    res = {}
+    for order in (1, -1):
+        obs = [feature_obs(d, f)[::order] for f in sel]
+        off = np.concatenate([[0], np.cumsum([len(o) for o in obs])])
+        cams = [c for o in obs for c, _ in o]
+        zs = [z for o in obs for _, z in o]
+        ctx = make_ctx(d, dtype=np.float32)
+        acc, gam, rows = ctx.update(0, off, cams, zs, tri_p[sel], chi2_for(np.diff(off)))
+        res[order] = gam
+        ctx.close()
+    e = np.abs(res[-1] - gam_o[sel]) / np.maximum(np.abs(gam_o[sel]), 1e-6)
+    assert np.median(e) < 1e-4 and np.quantile(e, 0.99) < 1e-3, (np.median(e), np.quantile(e, 0.99))
+    np.testing.assert_allclose(res[-1], res[1], rtol=1e-3, atol=1e-6)
