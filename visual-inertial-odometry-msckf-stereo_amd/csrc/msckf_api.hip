@@ -57,6 +57,81 @@ struct DBuf {   // grow-only device buffer
     }
 };
 
+// Pinned host staging for uploads: a ring of page-locked buffers, each
+// reused only after the copy out of it has completed (its event), so an
+// upload returns as soon as its copy is enqueued -- no stream synchronisation
+// (a copy from pageable memory is staged and waited on by the runtime).
+struct PinnedRing {
+    static constexpr int NS = 8;
+    unsigned char* buf[NS] = {};
+    size_t cap[NS] = {};
+    hipEvent_t ev[NS] = {};
+    bool armed[NS] = {};
+    int cur = 0;
+    hipError_t get(size_t n, unsigned char** out) {
+        const int i = cur;
+        if (armed[i]) {
+            hipError_t e = hipEventSynchronize(ev[i]);
+            if (e != hipSuccess) return e;
+            armed[i] = false;
+        }
+        if (!ev[i]) {
+            hipError_t e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
+            if (e != hipSuccess) return e;
+        }
+        if (cap[i] < n) {
+            if (buf[i]) (void)hipHostFree(buf[i]);
+            buf[i] = nullptr;
+            cap[i] = 0;
+            const size_t c = std::max<size_t>(n, 1 << 16);
+            hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&buf[i]), c, hipHostMallocDefault);
+            if (e != hipSuccess) return e;
+            cap[i] = c;
+        }
+        *out = buf[i];
+        return hipSuccess;
+    }
+    hipError_t mark(hipStream_t s) {
+        hipError_t e = hipEventRecord(ev[cur], s);
+        armed[cur] = e == hipSuccess;
+        cur = (cur + 1) % NS;
+        return e;
+    }
+    void release() {
+        for (int i = 0; i < NS; ++i) {
+            if (armed[i]) (void)hipEventSynchronize(ev[i]);
+            if (buf[i]) (void)hipHostFree(buf[i]);
+            if (ev[i]) (void)hipEventDestroy(ev[i]);
+            buf[i] = nullptr;
+            ev[i] = nullptr;
+            cap[i] = 0;
+            armed[i] = false;
+        }
+    }
+};
+
+// Pinned host buffer for downloads (synchronous calls: the stream is
+// synchronised before the buffer is read or reused).
+struct PinnedBuf {
+    unsigned char* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        const size_t c = std::max<size_t>(n, 1 << 16);
+        hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&p), c, hipHostMallocDefault);
+        if (e == hipSuccess) cap = c;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
 }  // namespace
 
 struct msckf_ctx {
@@ -89,6 +164,8 @@ struct msckf_ctx {
     DBuf<int> iscratch;
     KernelTimer timer;
     bool has_snapshot = false;
+    PinnedRing up;      // upload staging
+    PinnedBuf down;     // download staging
 };
 
 namespace {
@@ -178,24 +255,73 @@ std::vector<T> to_T(const double* x, size_t n) {
     return v;
 }
 
-// Copy a double host array to a device buffer of T (synchronous w.r.t. host).
+// Copy a double host array to a device buffer of T: converted into a pinned
+// staging buffer and enqueued on the context stream (asynchronous; the
+// caller's array may be reused as soon as this returns).
 template <typename T>
 hipError_t upload(msckf_ctx* c, void* dst, const double* src, size_t n) {
     if (n == 0) return hipSuccess;
-    std::vector<T> v = to_T<T>(src, n);
-    hipError_t e = hipMemcpyAsync(dst, v.data(), n * sizeof(T), hipMemcpyHostToDevice, c->stream);
+    unsigned char* h = nullptr;
+    hipError_t e = c->up.get(n * sizeof(T), &h);
     if (e != hipSuccess) return e;
-    return hipStreamSynchronize(c->stream);
+    T* v = reinterpret_cast<T*>(h);
+    for (size_t i = 0; i < n; ++i) v[i] = (T)src[i];
+    e = hipMemcpyAsync(dst, h, n * sizeof(T), hipMemcpyHostToDevice, c->stream);
+    if (e != hipSuccess) return e;
+    return c->up.mark(c->stream);
+}
+
+// Raw bytes, same staging (asynchronous).
+hipError_t upload_raw(msckf_ctx* c, void* dst, const void* src, size_t bytes) {
+    if (bytes == 0) return hipSuccess;
+    unsigned char* h = nullptr;
+    hipError_t e = c->up.get(bytes, &h);
+    if (e != hipSuccess) return e;
+    std::memcpy(h, src, bytes);
+    e = hipMemcpyAsync(dst, h, bytes, hipMemcpyHostToDevice, c->stream);
+    if (e != hipSuccess) return e;
+    return c->up.mark(c->stream);
+}
+
+// Several device arrays into one pinned buffer, ONE stream synchronisation.
+struct DownList {
+    struct Item { const void* src; size_t bytes, off; };
+    std::vector<Item> items;
+    size_t total = 0;
+    size_t add(const void* src, size_t bytes) {
+        const size_t off = total;
+        items.push_back({src, bytes, off});
+        total += (bytes + 15) & ~(size_t)15;
+        return off;
+    }
+    hipError_t run(msckf_ctx* c) {
+        hipError_t e = c->down.ensure(total);
+        if (e != hipSuccess) return e;
+        for (auto& it : items)
+            if (it.bytes) {
+                e = hipMemcpyAsync(c->down.p + it.off, it.src, it.bytes, hipMemcpyDeviceToHost, c->stream);
+                if (e != hipSuccess) return e;
+            }
+        e = hipStreamSynchronize(c->stream);
+        if (e == hipSuccess) c->timer.collect();
+        return e;
+    }
+    const unsigned char* at(const msckf_ctx* c, size_t off) const { return c->down.p + off; }
+};
+
+template <typename T>
+void to_double(double* dst, const unsigned char* src, size_t n) {
+    const T* v = reinterpret_cast<const T*>(src);
+    for (size_t i = 0; i < n; ++i) dst[i] = (double)v[i];
 }
 
 template <typename T>
 hipError_t download(msckf_ctx* c, double* dst, const void* src, size_t n) {
     if (n == 0) return hipSuccess;
-    std::vector<T> v(n);
-    hipError_t e = hipMemcpyAsync(v.data(), src, n * sizeof(T), hipMemcpyDeviceToHost, c->stream);
-    if (e != hipSuccess) return e;
-    e = hipStreamSynchronize(c->stream);
-    for (size_t i = 0; i < n; ++i) dst[i] = (double)v[i];
+    DownList d;
+    const size_t o = d.add(src, n * sizeof(T));
+    hipError_t e = d.run(c);
+    if (e == hipSuccess) to_double<T>(dst, d.at(c, o), n);
     return e;
 }
 
@@ -267,11 +393,12 @@ int load_features(msckf_ctx* c, int nf, const int32_t* feat_off, int single_filt
     HIPC(c->accept.ensure(nf + 1));
     HIPC(c->include.ensure(nf + 1));
     hipStream_t s = c->stream;
-    HIPC(hipMemcpyAsync(c->feat_filter.p, h_filt.data(), nf * sizeof(int), hipMemcpyHostToDevice, s));
-    HIPC(hipMemcpyAsync(c->feat_off.p, h_off.data(), (c->B + 1) * sizeof(int), hipMemcpyHostToDevice, s));
-    HIPC(hipMemcpyAsync(c->obs_off.p, obs_off, (nf + 1) * sizeof(int), hipMemcpyHostToDevice, s));
-    if (nobs) HIPC(hipMemcpyAsync(c->obs_cam.p, obs_cam, nobs * sizeof(int), hipMemcpyHostToDevice, s));
-    HIPC(hipMemcpyAsync(c->ysq_off.p, ysq.data(), (nf + 1) * sizeof(long long), hipMemcpyHostToDevice, s));
+    // every host array goes through the pinned upload ring: nothing below waits on the stream
+    HIPC(upload_raw(c, c->feat_filter.p, h_filt.data(), nf * sizeof(int)));
+    HIPC(upload_raw(c, c->feat_off.p, h_off.data(), (c->B + 1) * sizeof(int)));
+    HIPC(upload_raw(c, c->obs_off.p, obs_off, (nf + 1) * sizeof(int)));
+    if (nobs) HIPC(upload_raw(c, c->obs_cam.p, obs_cam, nobs * sizeof(int)));
+    HIPC(upload_raw(c, c->ysq_off.p, ysq.data(), (nf + 1) * sizeof(long long)));
     {   // gating size classes, largest first inside the list (long blocks start early)
         std::vector<std::vector<int>> cls(GateClasses::NC);
         GateClasses gc;
@@ -294,8 +421,7 @@ int load_features(msckf_ctx* c, int nf, const int32_t* feat_off, int single_filt
         }
         gc.off[GateClasses::NC] = pos;
         HIPC(c->gate_list.ensure(flat.size() + 1));
-        if (!flat.empty())
-            HIPC(hipMemcpyAsync(c->gate_list.p, flat.data(), flat.size() * sizeof(int), hipMemcpyHostToDevice, s));
+        if (!flat.empty()) HIPC(upload_raw(c, c->gate_list.p, flat.data(), flat.size() * sizeof(int)));
         gc.list = c->gate_list.p;
         // filter-resident gating: each filter's features by track length, descending
         std::vector<int> res(std::max(nf, 1));
@@ -313,11 +439,10 @@ int load_features(msckf_ctx* c, int nf, const int32_t* feat_off, int single_filt
             for (int i = obs_off[f] + 1; i < obs_off[f + 1]; ++i)
                 if (obs_cam[i] <= obs_cam[i - 1]) { asc = false; break; }
         HIPC(c->res_list.ensure(res.size()));
-        HIPC(hipMemcpyAsync(c->res_list.p, res.data(), res.size() * sizeof(int), hipMemcpyHostToDevice, s));
+        HIPC(upload_raw(c, c->res_list.p, res.data(), res.size() * sizeof(int)));
         gc.res_list = asc ? c->res_list.p : nullptr;
         gc.maxM_all = maxM;
         gc.max_nf = max_nf;
-        HIPC(hipStreamSynchronize(s));
         c->gc = gc;
     }
     {   // segment classes of the per-feature kernels (M <= S)
@@ -332,13 +457,10 @@ int load_features(msckf_ctx* c, int nf, const int32_t* feat_off, int single_filt
         }
         sc.off[SegClasses::NC] = (int)flat.size();
         HIPC(c->seg_list.ensure(flat.size() + 1));
-        if (!flat.empty())
-            HIPC(hipMemcpyAsync(c->seg_list.p, flat.data(), flat.size() * sizeof(int), hipMemcpyHostToDevice, s));
-        HIPC(hipStreamSynchronize(s));
+        if (!flat.empty()) HIPC(upload_raw(c, c->seg_list.p, flat.data(), flat.size() * sizeof(int)));
         sc.list = c->seg_list.p;
         c->sc = sc;
     }
-    HIPC(hipStreamSynchronize(s));
     HIPC(upload<T>(c, c->obs_z.p, obs_z, nobs * 4));
     if (chi2) {
         HIPC(upload<T>(c, c->chi2.p, chi2, nf));
@@ -352,7 +474,6 @@ int load_features(msckf_ctx* c, int nf, const int32_t* feat_off, int single_filt
     } else {
         HIPC(hipMemsetAsync(c->valid.p, 0, nf, s));
     }
-    HIPC(hipStreamSynchronize(s));
     c->nf = nf;
     c->maxM = maxM;
     c->max_nf = c->max_obs = 0;
@@ -419,16 +540,20 @@ int run_update_chain(msckf_ctx* c, int row_cap, bool triangulate) {
 template <typename T>
 int read_results(msckf_ctx* c, uint8_t* accepted_out, double* gamma_out, double* p_w_out, uint8_t* valid_out,
                  int32_t* rows_out) {
-    hipStream_t s = c->stream;
-    HIPC(hipStreamSynchronize(s));
-    c->timer.collect();
+    // every requested array in one pinned D2H batch: a single stream synchronisation
     const int nf = c->nf;
-    if (accepted_out && nf) HIPC(hipMemcpy(accepted_out, c->include.p, nf, hipMemcpyDeviceToHost));
-    if (valid_out && nf) HIPC(hipMemcpy(valid_out, c->valid.p, nf, hipMemcpyDeviceToHost));
-    if (gamma_out && nf) HIPC(download<T>(c, gamma_out, c->gamma.p, nf));
-    if (p_w_out && nf) HIPC(download<T>(c, p_w_out, c->p_w.p, (size_t)nf * 3));
-    std::vector<int> info(4 * c->B);
-    HIPC(hipMemcpy(info.data(), c->info.p, info.size() * sizeof(int), hipMemcpyDeviceToHost));
+    DownList d;
+    const size_t o_acc = accepted_out && nf ? d.add(c->include.p, nf) : 0;
+    const size_t o_val = valid_out && nf ? d.add(c->valid.p, nf) : 0;
+    const size_t o_gam = gamma_out && nf ? d.add(c->gamma.p, (size_t)nf * sizeof(T)) : 0;
+    const size_t o_pw = p_w_out && nf ? d.add(c->p_w.p, (size_t)nf * 3 * sizeof(T)) : 0;
+    const size_t o_info = d.add(c->info.p, (size_t)4 * c->B * sizeof(int));
+    HIPC(d.run(c));
+    if (accepted_out && nf) std::memcpy(accepted_out, d.at(c, o_acc), nf);
+    if (valid_out && nf) std::memcpy(valid_out, d.at(c, o_val), nf);
+    if (gamma_out && nf) to_double<T>(gamma_out, d.at(c, o_gam), nf);
+    if (p_w_out && nf) to_double<T>(p_w_out, d.at(c, o_pw), (size_t)nf * 3);
+    const int* info = reinterpret_cast<const int*>(d.at(c, o_info));
     int bad = -1;
     for (int b = 0; b < c->B; ++b) {
         if (rows_out) rows_out[b] = info[4 * b];
@@ -500,38 +625,40 @@ int do_set_state(msckf_ctx* c, int f, const double* imu, int n_cams, const doubl
         std::vector<T> full((size_t)c->Dmax * c->Dmax, T(0));
         for (int i = 0; i < D; ++i)
             for (int j = 0; j < D; ++j) full[(size_t)i * c->Dmax + j] = (T)P[(size_t)i * D + j];
-        HIPC(hipMemcpyAsync(c->P.p + (size_t)f * c->Dmax * c->Dmax * ts, full.data(), full.size() * ts,
-                            hipMemcpyHostToDevice, s));
-        HIPC(hipStreamSynchronize(s));
+        HIPC(upload_raw(c, c->P.p + (size_t)f * c->Dmax * c->Dmax * ts, full.data(), full.size() * ts));
     }
-    HIPC(hipMemcpy(c->ncams.p + f, &n_cams, sizeof(int), hipMemcpyHostToDevice));
+    HIPC(upload_raw(c, c->ncams.p + f, &n_cams, sizeof(int)));
     c->h_ncams[f] = n_cams;
+    (void)s;
     return 0;
 }
 
 template <typename T>
 int do_get_state(msckf_ctx* c, int f, double* imu, double* cams, double* P, int* n_cams) {
     const size_t ts = sizeof(T);
-    HIPC(hipStreamSynchronize(c->stream));
     const int nc = c->h_ncams[f];
     if (n_cams) *n_cams = nc;
+    DownList d;   // one stream synchronisation for all of it
+    const size_t o_imu = imu ? d.add(c->imu.p + (size_t)f * IMU_STRIDE * ts, IMU_STRIDE * ts) : 0;
+    const size_t o_cam = cams && nc ? d.add(c->cams.p + (size_t)f * c->Nmax * CAM_STRIDE * ts, (size_t)nc * CAM_STRIDE * ts) : 0;
+    const size_t o_P = P ? d.add(c->P.p + (size_t)f * c->Dmax * c->Dmax * ts, (size_t)c->Dmax * c->Dmax * ts) : 0;
+    HIPC(d.run(c));
     if (imu) {
         std::vector<double> rec(IMU_STRIDE);
-        HIPC(download<T>(c, rec.data(), c->imu.p + (size_t)f * IMU_STRIDE * ts, IMU_STRIDE));
+        to_double<T>(rec.data(), d.at(c, o_imu), IMU_STRIDE);
         std::memcpy(imu, rec.data(), MSCKF_IMU_LEN * sizeof(double));
     }
     if (cams && nc) {
         std::vector<double> rec((size_t)nc * CAM_STRIDE);
-        HIPC(download<T>(c, rec.data(), c->cams.p + (size_t)f * c->Nmax * CAM_STRIDE * ts, rec.size()));
+        to_double<T>(rec.data(), d.at(c, o_cam), rec.size());
         for (int i = 0; i < nc; ++i)
             std::memcpy(cams + (size_t)i * MSCKF_CAM_LEN, &rec[(size_t)i * CAM_STRIDE], MSCKF_CAM_LEN * sizeof(double));
     }
     if (P) {
         const int D = 21 + 6 * nc;
-        std::vector<double> full((size_t)c->Dmax * c->Dmax);
-        HIPC(download<T>(c, full.data(), c->P.p + (size_t)f * c->Dmax * c->Dmax * ts, full.size()));
+        const T* full = reinterpret_cast<const T*>(d.at(c, o_P));
         for (int i = 0; i < D; ++i)
-            for (int j = 0; j < D; ++j) P[(size_t)i * D + j] = full[(size_t)i * c->Dmax + j];
+            for (int j = 0; j < D; ++j) P[(size_t)i * D + j] = (double)full[(size_t)i * c->Dmax + j];
     }
     return 0;
 }
@@ -561,7 +688,7 @@ int upload_ints(msckf_ctx* c, std::initializer_list<const std::vector<int>*> lis
         out.push_back(c->iscratch.p + flat.size());
         flat.insert(flat.end(), l->begin(), l->end());
     }
-    if (tot) HIPC(hipMemcpyAsync(c->iscratch.p, flat.data(), tot * sizeof(int), hipMemcpyHostToDevice, c->stream));
+    if (tot) HIPC(upload_raw(c, c->iscratch.p, flat.data(), tot * sizeof(int)));
     return 0;
 }
 
@@ -591,9 +718,7 @@ int do_propagate_batch(msckf_ctx* c, int nfilt, const int32_t* filters, const in
     launch_propagate<T>(c->stream, dev_state<T>(c), make_params<T>(c), nfilt, d[0], d[1],
                         reinterpret_cast<T*>(c->scratch.p));
     c->timer.end(c->stream);
-    HIPC(hipGetLastError());
-    HIPC(hipStreamSynchronize(c->stream));
-    c->timer.collect();
+    HIPC(hipGetLastError());   // asynchronous: the next synchronising call waits for it
     return 0;
 }
 
@@ -609,9 +734,7 @@ int do_augment_batch(msckf_ctx* c, int nfilt, const int32_t* filters) {
     c->timer.begin(c->stream, "augment");
     launch_augment<T>(c->stream, dev_state<T>(c), nfilt, d[0]);
     c->timer.end(c->stream);
-    HIPC(hipGetLastError());
-    HIPC(hipStreamSynchronize(c->stream));
-    c->timer.collect();
+    HIPC(hipGetLastError());   // asynchronous
     for (int i = 0; i < nfilt; ++i) c->h_ncams[filters[i]] += 1;
     return 0;
 }
@@ -647,9 +770,7 @@ int do_prune_batch(msckf_ctx* c, int nfilt, const int32_t* filters, const int32_
     c->timer.begin(c->stream, "prune");
     launch_prune<T>(c->stream, dev_state<T>(c), nfilt, d[0], d[1], d[2], d[3], d[4]);
     c->timer.end(c->stream);
-    HIPC(hipGetLastError());
-    HIPC(hipStreamSynchronize(c->stream));
-    c->timer.collect();
+    HIPC(hipGetLastError());   // asynchronous
     for (int w = 0; w < nfilt; ++w) c->h_ncams[filters[w]] = new_n[w];
     return 0;
 }
@@ -674,15 +795,17 @@ template <typename T>
 int do_get_states_batch(msckf_ctx* c, int nfilt, const int32_t* filters, double* imu_out, double* cams_out,
                         int32_t* ncams_out) {
     const size_t ts = sizeof(T);
+    DownList d;   // one stream synchronisation
+    const size_t o_imu = d.add(c->imu.p, (size_t)c->B * IMU_STRIDE * ts);
+    const size_t o_cam = cams_out ? d.add(c->cams.p, (size_t)c->B * c->Nmax * CAM_STRIDE * ts) : 0;
+    HIPC(d.run(c));
     std::vector<double> imu_all((size_t)c->B * IMU_STRIDE);
-    HIPC(hipStreamSynchronize(c->stream));
-    HIPC(download<T>(c, imu_all.data(), c->imu.p, imu_all.size()));
+    to_double<T>(imu_all.data(), d.at(c, o_imu), imu_all.size());
     std::vector<double> cams_all;
     if (cams_out) {
         cams_all.resize((size_t)c->B * c->Nmax * CAM_STRIDE);
-        HIPC(download<T>(c, cams_all.data(), c->cams.p, cams_all.size()));
+        to_double<T>(cams_all.data(), d.at(c, o_cam), cams_all.size());
     }
-    (void)ts;
     for (int w = 0; w < nfilt; ++w) {
         const int f = filters[w];
         if (imu_out)
@@ -716,10 +839,12 @@ int do_triangulate(msckf_ctx* c, int f, int nf, const int32_t* obs_off, const in
     launch_triangulate<T>(c->stream, dev_state<T>(c), make_params<T>(c), feat_batch<T>(c), c->sc);
     c->timer.end(c->stream);
     HIPC(hipGetLastError());
-    HIPC(hipStreamSynchronize(c->stream));
-    c->timer.collect();
-    HIPC(download<T>(c, p_w_out, c->p_w.p, (size_t)nf * 3));
-    HIPC(hipMemcpy(valid_out, c->valid.p, nf, hipMemcpyDeviceToHost));
+    DownList d;   // one stream synchronisation
+    const size_t o_pw = d.add(c->p_w.p, (size_t)nf * 3 * sizeof(T));
+    const size_t o_v = d.add(c->valid.p, nf);
+    HIPC(d.run(c));
+    to_double<T>(p_w_out, d.at(c, o_pw), (size_t)nf * 3);
+    std::memcpy(valid_out, d.at(c, o_v), nf);
     return 0;
 }
 
@@ -799,6 +924,8 @@ int msckf_destroy(msckf_ctx_t* c) {
     for (auto* b : {&c->ncams, &c->ncams_snap, &c->info, &c->afail, &c->feat_filter, &c->feat_off, &c->obs_off, &c->obs_cam,
                     &c->row_off, &c->iscratch, &c->gate_list, &c->res_list, &c->seg_list})
         b->release();
+    c->up.release();
+    c->down.release();
     c->ysq_off.release();
     c->valid.release();
     c->accept.release();
