@@ -29,19 +29,23 @@ def main():
     dtype = np.float32 if args.dtype == "fp32" else np.float64
     probs = bench.make_problems(args, 0, min(args.unique, args.batch))
     ctx, _ = bench.build_batch(args, probs, dtype, 0)
-    buf = (C.c_ulonglong * (2 * 9 * 8))()
+    buf = (C.c_ulonglong * (3 * 9 * 8))()
     ctx.restore(); ctx.batch_update(row_cap=0, triangulate=True); ctx.sync()
     read(buf)   # reset after the warm-up
     ctx.restore(); ctx.batch_update(row_cap=0, triangulate=True); ctx.sync()
     read(buf)
-    a = np.frombuffer(buf, dtype=np.uint64).reshape(2, 9, 8).astype(float)
-    t = 1 if args.dtype == "fp64" else 0
+    a = np.frombuffer(buf, dtype=np.uint64).reshape(3, 9, 8).astype(float)
     out = {}
-    for nb in range(1, 9):
-        w = a[t, nb, 6]
-        if w == 0:
-            continue
-        out["NB%d" % nb] = dict({"waves": int(w)}, **{p: round(a[t, nb, i] / w) for i, p in enumerate(PH)})
+    for t, kind in ((0, "per_feature_f32"), (1, "per_feature_f64"), (2, "resident_f32")):
+        for nb in range(1, 9):
+            w = a[t, nb, 6]
+            if w == 0:
+                continue
+            ph = PH if t < 2 else ["scatter_prefetch", "y_pairs", "assemble", "eliminate", "finish", "total"]
+            out["%s NB%d" % (kind, nb)] = dict({"features": int(w)}, **{p: round(a[t, nb, i] / w) for i, p in enumerate(ph)})
+    if a[2, 0, 6] > 0:
+        out["resident_f32 kernel"] = {"prologue_per_wave": round(a[2, 0, 7] / (8 * 2048)),
+                                      "wave_total": round(a[2, 0, 6] / (8 * 2048))}
     print(json.dumps({"dtype": args.dtype, "cycles_per_wave": out}, indent=1))
     ctx.close()
 

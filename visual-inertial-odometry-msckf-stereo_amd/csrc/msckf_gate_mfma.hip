@@ -33,12 +33,14 @@ namespace msckf {
 // scalar type, wave-cycle sums (s_memtime) of record fetch, Y pair blocks,
 // assembly, elimination, finish, and the wave count.
 #ifdef MSCKF_GATE_PROBE
-__device__ unsigned long long g_gate_probe[2][9][8];
+__device__ unsigned long long g_gate_probe[3][9][8];   // [f32, f64, f32 resident][NB][phase]
 #define GPROBE_T(v) const unsigned long long v = __builtin_readcyclecounter()
-#define GPROBE_ADD(ts, NB, ph, dt) \
-    do { if ((threadIdx.x & 63) == 0) atomicAdd(&g_gate_probe[(ts) == 8][NB][ph], (unsigned long long)(dt)); } while (0)
+#define GPROBE_ADDK(kind, NB, ph, dt) \
+    do { if ((threadIdx.x & 63) == 0) atomicAdd(&g_gate_probe[kind][NB][ph], (unsigned long long)(dt)); } while (0)
+#define GPROBE_ADD(ts, NB, ph, dt) GPROBE_ADDK((ts) == 8, NB, ph, dt)
 #else
 #define GPROBE_T(v) (void)0
+#define GPROBE_ADDK(kind, NB, ph, dt) (void)0
 #define GPROBE_ADD(ts, NB, ph, dt) (void)0
 #endif
 
@@ -877,6 +879,9 @@ __device__ __forceinline__ float gr_feature(const float* __restrict__ pcc, const
     F4 acc[NBLK];
     const int M3 = 3 * M, capb = gr_capb(Mmax);
     float* stage = area;
+#ifdef MSCKF_GATE_PROBE
+    unsigned long long t_y = 0, t_asm = 0;
+#endif
     auto npairs = [&](int lo, int hi) { return hi < lo ? 0 : (hi + 1) * (hi + 2) / 2 - lo * (lo + 1) / 2; };
     for (int R0 = 0; R0 < NB;) {
         const int alo = (16 * R0) / 3;
@@ -888,6 +893,7 @@ __device__ __forceinline__ float gr_feature(const float* __restrict__ pcc, const
             ahi = ah2;
         }
         const int kbase = alo * (alo + 1) / 2, nbp = npairs(alo, ahi);
+        GPROBE_T(t_p0);
         for (int kk = lane; kk < nbp; kk += 64) {
             const int k = kbase + kk;
             int a = (int)((__builtin_amdgcn_sqrtf(8.0f * (float)k + 1.0f) - 1.0f) * 0.5f);
@@ -936,12 +942,23 @@ __device__ __forceinline__ float gr_feature(const float* __restrict__ pcc, const
             }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // one wave: its stores are visible to all lanes
+        GPROBE_T(t_p1);
         gm_assemble<float, NB>(acc, R0, R1, kbase, M3, s2, stage, ht, rt, Mmax, lane);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads done before the next pass / the panel reuse
+#ifdef MSCKF_GATE_PROBE
+        GPROBE_T(t_p2);
+        t_y += t_p1 - t_p0;
+        t_asm += t_p2 - t_p1;
+#endif
         R0 = R1;
     }
+    GPROBE_ADDK(2, NB, 1, t_y);
+    GPROBE_ADDK(2, NB, 2, t_asm);
+    GPROBE_T(t_e0);
     float* pan = area;
     const bool fail = gm_eliminate<float, NB, (NB >= GR_STREAM_NB)>(acc, pan, lane);
+    GPROBE_T(t_e1);
+    GPROBE_ADDK(2, NB, 3, t_e1 - t_e0);
     // gamma from the B rows' 4x4 Schur block (as gm_finish; the caller stores it)
     const int col_l = lane & 15, rg = lane >> 4;
     if (col_l >= 12 && rg == 3) {
@@ -965,6 +982,9 @@ __device__ __forceinline__ float gr_feature(const float* __restrict__ pcc, const
         if (fail || !(d0 < 0.f) || !(d1 < 0.f) || !(d2 < 0.f) || !(gam == gam)) gam = INFINITY;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // pan reads done before it is reused
+    GPROBE_T(t_f1);
+    GPROBE_ADDK(2, NB, 4, t_f1 - t_e1);
+    GPROBE_ADDK(2, NB, 6, 1);
     return gam;
 }
 
@@ -976,6 +996,7 @@ __global__ void __launch_bounds__(64 * GR_NW) k_gate_res(DevState<float> st, Par
     const int b = xcd_remap(blockIdx.x, gridDim.x);
     const int f0 = fb.feat_off[b], nfeat = fb.feat_off[b + 1] - f0;
     if (nfeat == 0) return;
+    GPROBE_T(t_kstart);
     const int N = st.ncams[b], ld = st.Dmax;
     float* pcc = reinterpret_cast<float*>(smem_raw);
     int* meta = reinterpret_cast<int*>(pcc + gr_pcc_floats(st.Nmax));   // [fcap][4]: f, o0, M (0: invalid), chi2
@@ -1017,6 +1038,8 @@ __global__ void __launch_bounds__(64 * GR_NW) k_gate_res(DevState<float> st, Par
         }
     }
     __syncthreads();
+    GPROBE_T(t_pro);
+    GPROBE_ADDK(2, 0, 7, t_pro - t_kstart);
     float* ht = wbase;
     float* rt = ht + 18 * Mmax;
     float* area = ht + gm_head(Mmax);
@@ -1039,6 +1062,7 @@ __global__ void __launch_bounds__(64 * GR_NW) k_gate_res(DevState<float> st, Par
     int pf = -1, pa = 0;
     float pg = 0.f;
     for (; pos < nfeat; pos += GR_NW) {
+        GPROBE_T(t_i0);
         const int f = __builtin_amdgcn_readfirstlane(meta[4 * pos]);
         const int M = __builtin_amdgcn_readfirstlane(meta[4 * pos + 2]);
         const float chi2 = __int_as_float(meta[4 * pos + 3]);
@@ -1067,6 +1091,10 @@ __global__ void __launch_bounds__(64 * GR_NW) k_gate_res(DevState<float> st, Par
         // feature instead of being hoisted out of this loop (and spilled)
         int lane = lane0;
         asm volatile("" : "+v"(lane));
+#ifdef MSCKF_GATE_PROBE
+        GPROBE_T(t_i1);
+        if (M > 0) GPROBE_ADDK(2, gm_nb(M), 0, t_i1 - t_i0);
+#endif
         if (M > 0) {
             switch (gm_nb(M)) {
                 case 1: gam = gr_feature<1>(pcc, ht, rt, area, slot, M, Mmax, rn2, s2, lane); break;
@@ -1080,7 +1108,13 @@ __global__ void __launch_bounds__(64 * GR_NW) k_gate_res(DevState<float> st, Par
         pf = f;
         pg = gam;
         pa = (gam < chi2) ? 1 : 0;
+#ifdef MSCKF_GATE_PROBE
+        GPROBE_T(t_i2);
+        if (M > 0) GPROBE_ADDK(2, gm_nb(M), 5, t_i2 - t_i0);
+#endif
     }
+    GPROBE_T(t_kend);
+    GPROBE_ADDK(2, 0, 6, t_kend - t_kstart);
     if (lane == 0 && pf >= 0) {
         fb.gamma[pf] = pg;
         fb.accept[pf] = pa;
@@ -1188,9 +1222,9 @@ void launch_gate_mfma(hipStream_t s, const DevState<T>& st, const Params<T>& prm
     }
 }
 #ifdef MSCKF_GATE_PROBE
-extern "C" int msckf_gate_probe_read(unsigned long long* out) {   // [2][9][8], then reset
+extern "C" int msckf_gate_probe_read(unsigned long long* out) {   // [3][9][8], then reset
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_gate_probe), sizeof(g_gate_probe)) != hipSuccess) return -1;
-    static unsigned long long zero[2][9][8] = {};
+    static unsigned long long zero[3][9][8] = {};
     return hipMemcpyToSymbol(HIP_SYMBOL(g_gate_probe), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
 }
 #endif
