@@ -337,9 +337,8 @@ def test_batched_fp32_80x1000_vs_oracle():
 @pytest.mark.parametrize("N,F,B,cap", [(30, 200, 2, 30), (40, 150, 2, None), (82, 50, 1, None)])
 def test_gate_fp32_gamma_vs_oracle(N, F, B, cap):
     """fp32 gating on MFMA tiles against the oracle's fp64 gamma
-    (msckf.py:606-614).  N = 30 (cam capacity 30, the bench's): the
-    filter-resident kernel (P_cc in LDS, one workgroup per filter,
-    k_gate_res); N = 40: every one-wave size class (1..8 16-row blocks,
+    (msckf.py:606-614).  N = 30 (cam capacity 30, the bench's workload);
+    N = 40: every one-wave size class (1..8 16-row blocks,
     single- and multi-pass Y staging); N = 82: also the four-wave workgroup
     kernel for 40 < M <= 82 (up to 16 blocks, Y staged in passes).  Tolerance:
     fp32 with the saddle point's conditioning (~1e3) -- median relative error
@@ -490,11 +489,9 @@ def test_sequence_golden(name):
 
 def test_gate_fp32_unordered_tracks():
     """Tracks whose cam slots do not ascend (the reference always lists a
-    feature's observations in cam order, but the C-ABI takes any order): the
-    batch is routed to the per-feature gating kernels instead of the
-    filter-resident one (which reads P_cc blocks (a, b), a > b).  gamma is
-    invariant to the order of a feature's observations, so the reversed
-    tracks must gate like the ordered ones."""
+    feature's observations in cam order, but the C-ABI takes any order):
+    gamma is invariant to the order of a feature's observations, so the
+    reversed tracks must gate like the ordered ones."""
     p = synth.make_update_problem(20, 120, seed=411)
     d = problem_to_dict(p)
     st, acc_o, tri_p, tri_ok, gam_o = oracle_update(d)

@@ -152,7 +152,7 @@ struct msckf_ctx {
     // feature batch
     int nf = 0, maxM = 0, max_nf = 0, max_obs = 0;   // per filter, of the loaded batch
     std::vector<int> h_feat_off;
-    DBuf<int> feat_filter, feat_off, obs_off, obs_cam, row_off, gate_list, res_list;
+    DBuf<int> feat_filter, feat_off, obs_off, obs_cam, row_off, gate_list;
     GateClasses gc;
     SegClasses sc;
     DBuf<int> seg_list;
@@ -423,26 +423,6 @@ int load_features(msckf_ctx* c, int nf, const int32_t* feat_off, int single_filt
         HIPC(c->gate_list.ensure(flat.size() + 1));
         if (!flat.empty()) HIPC(upload_raw(c, c->gate_list.p, flat.data(), flat.size() * sizeof(int)));
         gc.list = c->gate_list.p;
-        // filter-resident gating: each filter's features by track length, descending
-        std::vector<int> res(std::max(nf, 1));
-        int max_nf = 0;
-        for (int b = 0; b < c->B; ++b) {
-            const int a = h_off[b], e = h_off[b + 1];
-            max_nf = std::max(max_nf, e - a);
-            for (int f = a; f < e; ++f) res[f] = f;
-            std::stable_sort(res.begin() + a, res.begin() + e, [&](int x, int y) {
-                return obs_off[x + 1] - obs_off[x] > obs_off[y + 1] - obs_off[y];
-            });
-        }
-        bool asc = true;   // every track's cam slots ascend (k_gate_res reads P_cc blocks (a, b), a > b)
-        for (int f = 0; f < nf && asc; ++f)
-            for (int i = obs_off[f] + 1; i < obs_off[f + 1]; ++i)
-                if (obs_cam[i] <= obs_cam[i - 1]) { asc = false; break; }
-        HIPC(c->res_list.ensure(res.size()));
-        HIPC(upload_raw(c, c->res_list.p, res.data(), res.size() * sizeof(int)));
-        gc.res_list = asc ? c->res_list.p : nullptr;
-        gc.maxM_all = maxM;
-        gc.max_nf = max_nf;
         c->gc = gc;
     }
     {   // segment classes of the per-feature kernels (M <= S)
@@ -922,7 +902,7 @@ int msckf_destroy(msckf_ctx_t* c) {
                     &c->dx, &c->obs_z, &c->chi2, &c->p_w, &c->obs_ws, &c->obs_ht, &c->obs_g, &c->tau, &c->ysq, &c->gamma, &c->scratch})
         b->release();
     for (auto* b : {&c->ncams, &c->ncams_snap, &c->info, &c->afail, &c->feat_filter, &c->feat_off, &c->obs_off, &c->obs_cam,
-                    &c->row_off, &c->iscratch, &c->gate_list, &c->res_list, &c->seg_list})
+                    &c->row_off, &c->iscratch, &c->gate_list, &c->seg_list})
         b->release();
     c->up.release();
     c->down.release();

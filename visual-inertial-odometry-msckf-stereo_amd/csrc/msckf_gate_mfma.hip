@@ -33,7 +33,7 @@ namespace msckf {
 // scalar type, wave-cycle sums (s_memtime) of record fetch, Y pair blocks,
 // assembly, elimination, finish, and the wave count.
 #ifdef MSCKF_GATE_PROBE
-__device__ unsigned long long g_gate_probe[3][9][8];   // [f32, f64, f32 resident][NB][phase]
+__device__ unsigned long long g_gate_probe[2][9][8];   // [f32, f64][NB][phase]
 #define GPROBE_T(v) const unsigned long long v = __builtin_readcyclecounter()
 #define GPROBE_ADDK(kind, NB, ph, dt) \
     do { if ((threadIdx.x & 63) == 0) atomicAdd(&g_gate_probe[kind][NB][ph], (unsigned long long)(dt)); } while (0)
@@ -839,288 +839,6 @@ __global__ void __launch_bounds__(256) k_gate_mfma_wg(DevState<float> st, Params
     }
 }
 
-// ---------------------------------------------------------------------------
-// Filter-resident gating (fp32 contexts whose P_cc fits in LDS): one
-// 512-thread workgroup per filter.  The per-feature kernel above spends most
-// of a wave's life waiting on its memory traffic (tools/probes/gate_phases.py:
-// the Y phase's scattered 24-byte P-row loads ~65 % of an NB = 6 wave, record
-// fetch and Y ~70 % in the small classes) although every feature of a filter
-// re-reads blocks of the same P_cc.  Here:
-//   * the filter's P_cc lower 6x6 blocks are staged in LDS once -- block
-//     (a, b), a >= b, at 36 (a (a + 1) / 2 + b), row-major, so a lane reads
-//     one block with nine ds_read_b128 (consecutive blocks 144 B apart: the 16
-//     lanes of a ds_read_b128 group cover all 64 banks once);
-//   * so is the filter's feature metadata (host list sorted by track length,
-//     descending), in the same memory round trip;
-//   * wave w walks list positions w, w + 8, ... -- the next feature's gating
-//     records are loaded into registers while the current one is eliminated,
-//     and its (gamma, accept) store is deferred past that load, so the steady
-//     state has no exposed global memory round trip;
-//   * per feature, the pair stage / assembly / MFMA LDL^T of k_gate_mfma in
-//     the size class of its own M (a switch over NB = 1..GR_NBMAX).
-// ---------------------------------------------------------------------------
-constexpr int GR_NW = 8;       // waves per workgroup
-constexpr int GR_NBMAX = 6;    // M <= 30
-constexpr int GR_NCH = 6;      // record pairs per lane: 12 M <= 64 GR_NCH
-#ifndef GR_STREAM_NB
-#define GR_STREAM_NB 5         // classes from this NB on eliminate streaming block rows (register budget)
-#endif
-__host__ __device__ constexpr int gr_capb(int Mmax) { return 6 * Mmax; }   // one block row per pass
-__host__ __device__ constexpr int gr_wave_floats(int Mmax) {
-    return gm_head(Mmax) + gm_area(Mmax, gr_capb(Mmax)) + ((Mmax + 3) & ~3);
-}
-__host__ __device__ constexpr int gr_pcc_floats(int Nmax) { return 18 * Nmax * (Nmax + 1); }
-
-template <int NB>
-__device__ __forceinline__ float gr_feature(const float* __restrict__ pcc, const float* ht, const float* rt,
-                                            float* area, const int* slot, int M, int Mmax, float rn2, float s2,
-                                            int lane) {
-    constexpr int NBLK = NB * (NB + 1) / 2;
-    F4 acc[NBLK];
-    const int M3 = 3 * M, capb = gr_capb(Mmax);
-    float* stage = area;
-#ifdef MSCKF_GATE_PROBE
-    unsigned long long t_y = 0, t_asm = 0;
-#endif
-    auto npairs = [&](int lo, int hi) { return hi < lo ? 0 : (hi + 1) * (hi + 2) / 2 - lo * (lo + 1) / 2; };
-    for (int R0 = 0; R0 < NB;) {
-        const int alo = (16 * R0) / 3;
-        int R1 = R0 + 1, ahi = min(M - 1, (16 * R1 - 1) / 3);
-        while (R1 < NB) {
-            const int ah2 = min(M - 1, (16 * (R1 + 1) - 1) / 3);
-            if (npairs(alo, ah2) > capb) break;
-            ++R1;
-            ahi = ah2;
-        }
-        const int kbase = alo * (alo + 1) / 2, nbp = npairs(alo, ahi);
-        GPROBE_T(t_p0);
-        for (int kk = lane; kk < nbp; kk += 64) {
-            const int k = kbase + kk;
-            int a = (int)((__builtin_amdgcn_sqrtf(8.0f * (float)k + 1.0f) - 1.0f) * 0.5f);
-            if (a * (a + 1) / 2 > k) --a;
-            if ((a + 1) * (a + 2) / 2 <= k) ++a;
-            const int bo = k - a * (a + 1) / 2;
-            const int sa = slot[a], sb = slot[bo];
-            // block (sa, sb), sa > sb: the host routes a batch here only when every
-            // track's cam slots ascend (the reference's observation order)
-            float Pl[36];
-            {
-                const F4* src = reinterpret_cast<const F4*>(pcc + 36 * (sa * (sa + 1) / 2 + sb));
-#pragma unroll
-                for (int j = 0; j < 9; ++j) {
-                    const F4 v = src[j];
-                    Pl[4 * j] = v.x; Pl[4 * j + 1] = v.y; Pl[4 * j + 2] = v.z; Pl[4 * j + 3] = v.w;
-                }
-            }
-            const float* Ha = ht + 18 * a;
-            const float* Hb = ht + 18 * bo;
-            float* dst = stage + 9 * kk;
-            F2 hb01[6];   // (Hb[0][u], Hb[1][u])
-#pragma unroll
-            for (int u = 0; u < 6; ++u) hb01[u] = F2{Hb[u], Hb[6 + u]};
-#pragma unroll
-            for (int x = 0; x < 3; ++x) {
-                F2 t2[3] = {F2{0, 0}, F2{0, 0}, F2{0, 0}};   // Ha[x] P as three column pairs
-#pragma unroll
-                for (int u = 0; u < 6; ++u) {
-                    const float h = Ha[6 * x + u];
-#pragma unroll
-                    for (int c = 0; c < 3; ++c)
-                        t2[c] = __builtin_elementwise_fma(F2{h, h}, F2{Pl[6 * u + 2 * c], Pl[6 * u + 2 * c + 1]}, t2[c]);
-                }
-                const float t1[6] = {t2[0].x, t2[0].y, t2[1].x, t2[1].y, t2[2].x, t2[2].y};
-                F2 y01 = {0, 0};
-                float y2 = 0;
-#pragma unroll
-                for (int u = 0; u < 6; ++u) {
-                    y01 = __builtin_elementwise_fma(F2{t1[u], t1[u]}, hb01[u], y01);
-                    y2 = fmaf(t1[u], Hb[12 + u], y2);
-                }
-                dst[3 * x] = y01.x;
-                dst[3 * x + 1] = y01.y;
-                dst[3 * x + 2] = y2;
-            }
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // one wave: its stores are visible to all lanes
-        GPROBE_T(t_p1);
-        gm_assemble<float, NB>(acc, R0, R1, kbase, M3, s2, stage, ht, rt, Mmax, lane);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads done before the next pass / the panel reuse
-#ifdef MSCKF_GATE_PROBE
-        GPROBE_T(t_p2);
-        t_y += t_p1 - t_p0;
-        t_asm += t_p2 - t_p1;
-#endif
-        R0 = R1;
-    }
-    GPROBE_ADDK(2, NB, 1, t_y);
-    GPROBE_ADDK(2, NB, 2, t_asm);
-    GPROBE_T(t_e0);
-    float* pan = area;
-    const bool fail = gm_eliminate<float, NB, (NB >= GR_STREAM_NB)>(acc, pan, lane);
-    GPROBE_T(t_e1);
-    GPROBE_ADDK(2, NB, 3, t_e1 - t_e0);
-    // gamma from the B rows' 4x4 Schur block (as gm_finish; the caller stores it)
-    const int col_l = lane & 15, rg = lane >> 4;
-    if (col_l >= 12 && rg == 3) {
-        const F4 v = acc[bidx(NB - 1, NB - 1)];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) pan[4 * i + (col_l - 12)] = v[i];
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    float gam = 0.f;
-    if (lane == 0) {
-        const float* a = pan;
-        const float d0 = a[0];
-        const float l10 = a[4] / d0, l20 = a[8] / d0, l30 = a[12] / d0;
-        const float d1 = a[5] - l10 * l10 * d0;
-        const float l21 = (a[9] - l20 * l10 * d0) / d1;
-        const float l31 = (a[13] - l30 * l10 * d0) / d1;
-        const float d2 = a[10] - l20 * l20 * d0 - l21 * l21 * d1;
-        const float l32 = (a[14] - l30 * l20 * d0 - l31 * l21 * d1) / d2;
-        const float d3 = a[15] - l30 * l30 * d0 - l31 * l31 * d1 - l32 * l32 * d2;
-        gam = -d3 + rn2 / s2;
-        if (fail || !(d0 < 0.f) || !(d1 < 0.f) || !(d2 < 0.f) || !(gam == gam)) gam = INFINITY;
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // pan reads done before it is reused
-    GPROBE_T(t_f1);
-    GPROBE_ADDK(2, NB, 4, t_f1 - t_e1);
-    GPROBE_ADDK(2, NB, 6, 1);
-    return gam;
-}
-
-__global__ void __launch_bounds__(64 * GR_NW) k_gate_res(DevState<float> st, Params<float> prm, FeatBatch<float> fb,
-                                                       const int* __restrict__ rlist, int Mmax, int fcap) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    const int tid = threadIdx.x, lane0 = tid & 63, lane = lane0;
-    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int b = xcd_remap(blockIdx.x, gridDim.x);
-    const int f0 = fb.feat_off[b], nfeat = fb.feat_off[b + 1] - f0;
-    if (nfeat == 0) return;
-    GPROBE_T(t_kstart);
-    const int N = st.ncams[b], ld = st.Dmax;
-    float* pcc = reinterpret_cast<float*>(smem_raw);
-    int* meta = reinterpret_cast<int*>(pcc + gr_pcc_floats(st.Nmax));   // [fcap][4]: f, o0, M (0: invalid), chi2
-    float* wbase = reinterpret_cast<float*>(meta + 4 * fcap) + (size_t)wv * gr_wave_floats(Mmax);
-    // ---- P_cc lower blocks and the feature list: one memory round trip ----
-    {
-        const float* P = st.P + (size_t)b * ld * ld + (size_t)21 * ld + 21;
-        const int nblk = N * (N + 1) / 2;
-        constexpr int BPR = (64 * GR_NW) / 36;   // blocks per round: thread t -> block t / 36, element t % 36
-        constexpr int NCK = 17;                   // rounds in flight per chunk (two chunks at N = 30)
-        const int kk = tid / 36, w = tid - 36 * kk, u = w / 6, v = w - 6 * u;
-        int fl = 0;
-        if (tid < nfeat) fl = rlist[f0 + tid];   // nfeat <= fcap <= 512 (host check)
-        for (int j0 = 0; BPR * j0 < nblk; j0 += NCK) {
-            float pv[NCK];
-            int dst[NCK];
-#pragma unroll
-            for (int j = 0; j < NCK; ++j) {
-                const int k = BPR * (j0 + j) + kk;
-                const bool ok = kk < BPR && k < nblk;
-                const int kc = ok ? k : 0;
-                int a = (int)((__builtin_amdgcn_sqrtf(8.0f * (float)kc + 1.0f) - 1.0f) * 0.5f);
-                if (a * (a + 1) / 2 > kc) --a;
-                if ((a + 1) * (a + 2) / 2 <= kc) ++a;
-                const int c = kc - a * (a + 1) / 2;
-                pv[j] = ok ? P[(size_t)(6 * a + u) * ld + 6 * c + v] : 0.f;
-                dst[j] = ok ? 36 * k + w : -1;
-            }
-#pragma unroll
-            for (int j = 0; j < NCK; ++j)
-                if (dst[j] >= 0) pcc[dst[j]] = pv[j];
-        }
-        if (tid < nfeat) {
-            const int o0 = fb.obs_off[fl], M = fb.obs_off[fl + 1] - o0;
-            meta[4 * tid] = fl;
-            meta[4 * tid + 1] = o0;
-            meta[4 * tid + 2] = fb.valid[fl] ? M : 0;
-            meta[4 * tid + 3] = __float_as_int(fb.chi2[fl]);
-        }
-    }
-    __syncthreads();
-    GPROBE_T(t_pro);
-    GPROBE_ADDK(2, 0, 7, t_pro - t_kstart);
-    float* ht = wbase;
-    float* rt = ht + 18 * Mmax;
-    float* area = ht + gm_head(Mmax);
-    int* slot = reinterpret_cast<int*>(area + gm_area(Mmax, gr_capb(Mmax)));
-    const float s2 = prm.sigma2;
-    auto fetch = [&](int pos, F2 (&cv)[GR_NCH], int& sl) {
-        const int o0 = meta[4 * pos + 1], M = meta[4 * pos + 2];
-        const F2* src = reinterpret_cast<const F2*>(fb.obs_ht + (size_t)o0 * OBS_HTS);
-#pragma unroll
-        for (int j = 0; j < GR_NCH; ++j) {
-            const int k = lane + 64 * j;
-            cv[j] = k < 12 * M ? src[k] : F2{0, 0};
-        }
-        sl = lane < M ? fb.obs_cam[o0 + lane] : 0;
-    };
-    F2 cv[GR_NCH];
-    int sl = 0;
-    int pos = wv;
-    if (pos < nfeat) fetch(pos, cv, sl);
-    int pf = -1, pa = 0;
-    float pg = 0.f;
-    for (; pos < nfeat; pos += GR_NW) {
-        GPROBE_T(t_i0);
-        const int f = __builtin_amdgcn_readfirstlane(meta[4 * pos]);
-        const int M = __builtin_amdgcn_readfirstlane(meta[4 * pos + 2]);
-        const float chi2 = __int_as_float(meta[4 * pos + 3]);
-        // this feature's records into the wave's LDS rows (the loads were issued a feature ago)
-        float rn2 = 0.f;
-#pragma unroll
-        for (int j = 0; j < GR_NCH; ++j) {
-            const int k = lane + 64 * j, o = k / 12, e = 2 * (k - 12 * o);
-            if (k < 12 * M) {
-                if (e < OBS_RT) *reinterpret_cast<F2*>(ht + 18 * o + e) = cv[j];
-                else if (e < OBS_RT + 4) *reinterpret_cast<F2*>(rt + 4 * o + (e - OBS_RT)) = cv[j];
-                if (e == OBS_RT + 2) rn2 += cv[j].y * cv[j].y;   // r_n
-            }
-        }
-        if (lane < M) slot[lane] = sl;
-        // the next feature's records, then the previous feature's result
-        if (pos + GR_NW < nfeat) fetch(pos + GR_NW, cv, sl);
-        if (lane == 0 && pf >= 0) {
-            fb.gamma[pf] = pg;
-            fb.accept[pf] = pa;
-        }
-        rn2 = wave_sum(rn2);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        float gam = NAN;
-        // an opaque copy of the lane id: its index arithmetic is redone per
-        // feature instead of being hoisted out of this loop (and spilled)
-        int lane = lane0;
-        asm volatile("" : "+v"(lane));
-#ifdef MSCKF_GATE_PROBE
-        GPROBE_T(t_i1);
-        if (M > 0) GPROBE_ADDK(2, gm_nb(M), 0, t_i1 - t_i0);
-#endif
-        if (M > 0) {
-            switch (gm_nb(M)) {
-                case 1: gam = gr_feature<1>(pcc, ht, rt, area, slot, M, Mmax, rn2, s2, lane); break;
-                case 2: gam = gr_feature<2>(pcc, ht, rt, area, slot, M, Mmax, rn2, s2, lane); break;
-                case 3: gam = gr_feature<3>(pcc, ht, rt, area, slot, M, Mmax, rn2, s2, lane); break;
-                case 4: gam = gr_feature<4>(pcc, ht, rt, area, slot, M, Mmax, rn2, s2, lane); break;
-                case 5: gam = gr_feature<5>(pcc, ht, rt, area, slot, M, Mmax, rn2, s2, lane); break;
-                default: gam = gr_feature<6>(pcc, ht, rt, area, slot, M, Mmax, rn2, s2, lane); break;
-            }
-        }
-        pf = f;
-        pg = gam;
-        pa = (gam < chi2) ? 1 : 0;
-#ifdef MSCKF_GATE_PROBE
-        GPROBE_T(t_i2);
-        if (M > 0) GPROBE_ADDK(2, gm_nb(M), 5, t_i2 - t_i0);
-#endif
-    }
-    GPROBE_T(t_kend);
-    GPROBE_ADDK(2, 0, 6, t_kend - t_kstart);
-    if (lane == 0 && pf >= 0) {
-        fb.gamma[pf] = pg;
-        fb.accept[pf] = pa;
-    }
-}
-
 template <typename T, int NB, bool MP>
 void launch_cfg(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const FeatBatch<T>& fb,
                 const int* list, int cnt, int Mmax, int capb, int wpb, size_t lds) {
@@ -1161,24 +879,6 @@ void launch_nb(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const
 
 
 }  // namespace
-
-size_t gate_res_lds_bytes(int Nmax, int Mmax, int fcap) {
-    return ((size_t)gr_pcc_floats(Nmax) + 4 * (size_t)fcap + (size_t)GR_NW * gr_wave_floats(Mmax)) * sizeof(float);
-}
-bool gate_res_fits(int Nmax, int maxM, int max_nf) {
-    return Nmax <= 32 && maxM >= 1 && gm_nb(maxM) <= GR_NBMAX && max_nf <= 64 * GR_NW &&
-           gate_res_lds_bytes(Nmax, maxM, max_nf) <= 160 * 1024;
-}
-void launch_gate_res(hipStream_t s, const DevState<float>& st, const Params<float>& prm, const FeatBatch<float>& fb,
-                     const int* rlist, int maxM, int max_nf) {
-    const size_t lds = gate_res_lds_bytes(st.Nmax, maxM, max_nf);
-    static size_t attr = 64 * 1024;
-    if (lds > attr) {
-        (void)hipFuncSetAttribute((const void*)k_gate_res, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        attr = lds;
-    }
-    hipLaunchKernelGGL(k_gate_res, dim3(st.B), dim3(64 * GR_NW), lds, s, st, prm, fb, rlist, maxM, max_nf);
-}
 
 // fp64 up to NB = 6 (M <= 30): beyond it the accumulators spill (k_gate_wave then)
 bool gate_mfma_fits(int maxM, int ts) { return maxM >= 1 && gm_nb(maxM) <= (ts == 8 ? 6 : 8); }
@@ -1222,9 +922,9 @@ void launch_gate_mfma(hipStream_t s, const DevState<T>& st, const Params<T>& prm
     }
 }
 #ifdef MSCKF_GATE_PROBE
-extern "C" int msckf_gate_probe_read(unsigned long long* out) {   // [3][9][8], then reset
+extern "C" int msckf_gate_probe_read(unsigned long long* out) {   // [2][9][8], then reset
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_gate_probe), sizeof(g_gate_probe)) != hipSuccess) return -1;
-    static unsigned long long zero[3][9][8] = {};
+    static unsigned long long zero[2][9][8] = {};
     return hipMemcpyToSymbol(HIP_SYMBOL(g_gate_probe), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
 }
 #endif

@@ -2599,12 +2599,6 @@ template <typename T>
 void launch_gate(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const FeatBatch<T>& fb,
                  const GateClasses& gc) {
     if (fb.nf == 0) return;
-    if constexpr (sizeof(T) == 4) {
-        if (gc.res_list && gate_res_fits(st.Nmax, gc.maxM_all, gc.max_nf)) {
-            launch_gate_res(s, st, prm, fb, gc.res_list, gc.maxM_all, gc.max_nf);
-            return;
-        }
-    }
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void*)k_gate_lds<T>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);

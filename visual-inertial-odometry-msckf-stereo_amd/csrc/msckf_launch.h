@@ -100,10 +100,6 @@ struct GateClasses {
     const int* list = nullptr;
     int off[NC + 1] = {};
     int maxM[NC] = {};
-    // filter-resident gating (fp32): every filter's features sorted by M,
-    // descending, in its feat_off range; batch maximum of M and of features per filter
-    const int* res_list = nullptr;
-    int maxM_all = 0, max_nf = 0;
 };
 template <typename T>
 void launch_gate(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&, const GateClasses&);
@@ -113,11 +109,6 @@ bool gate_mfma_fits(int maxM, int scalar_bytes);
 template <typename T>
 void launch_gate_mfma(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&, const int* list, int cnt,
                       int maxM);
-// fp32 gating with the filter's P_cc resident in LDS, one workgroup per filter
-// (windows of <= 32 cams whose P_cc blocks, feature list and wave areas fit in LDS)
-bool gate_res_fits(int Nmax, int maxM, int max_nf);
-void launch_gate_res(hipStream_t, const DevState<float>&, const Params<float>&, const FeatBatch<float>&,
-                     const int* res_list, int maxM, int max_nf);
 // fp32 gating of large tracks (40 < M <= 82) on MFMA tiles, one 4-wave workgroup per feature
 bool gate_mfma_wg_fits(int maxM);
 void launch_gate_mfma_wg(hipStream_t, const DevState<float>&, const Params<float>&, const FeatBatch<float>&,
