@@ -46,7 +46,7 @@ __device__ __forceinline__ bool mchol_core(int nrow, int ncol, int nelim, double
         const int c = colmajor_col(tc, nrow);
         const int r = c + (tc - (c * nrow - c * (c - 1) / 2));
         ti[s] = __builtin_amdgcn_readfirstlane(t < ntiles ? r : -1);
-        tj[s] = __builtin_amdgcn_readfirstlane(c);
+        tj[s] = __builtin_amdgcn_readfirstlane(t < ntiles ? c : -1);   // an empty slot matches no column
     }
     v4d acc[TPW];
 #pragma unroll
@@ -156,7 +156,7 @@ __device__ __forceinline__ bool mchol_core(int nrow, int ncol, int nelim, double
         // 4. trailing update of the tiles right of column k
 #pragma unroll
         for (int s = 0; s < TPW; ++s) {
-            if (ti[s] < 0 || tj[s] <= k) continue;
+            if (ti[s] < 0 || tj[s] <= k) continue;   // (empty slots: ti = tj = -1)
             const double* ri = pan + 16 * ti[s] * MC_PS + op;
             const double* rj = pan + 16 * tj[s] * MC_PS + op;
 #pragma unroll
