@@ -1106,4 +1106,16 @@ int msckf_kernel_times(msckf_ctx_t* c, int max_k, double* ms_total, int32_t* lau
     return k;
 }
 
+// Debug (not in include/msckf_hip.h): copy the first `count` doubles of a
+// Kalman workspace buffer (0 Lc, 1 Vi, 2 Sii, 3 G, 4 Tm, 5 W) to the host.
+int msckf_debug_workspace(msckf_ctx_t* c, int which, double* out, size_t count) {
+    if (!c || !out) FAIL(-1, "null argument");
+    const void* src = which == 0 ? c->Lc.p : which == 1 ? c->Vi.p : which == 2 ? c->Sii.p
+                    : which == 3 ? c->G.p : which == 4 ? c->Tm.p : which == 5 ? c->W.p : nullptr;
+    if (!src) FAIL(-1, "unknown workspace %d", which);
+    HIPC(hipStreamSynchronize(c->stream));
+    HIPC(hipMemcpy(out, src, count * sizeof(double), hipMemcpyDeviceToHost));
+    return 0;
+}
+
 }  // extern "C"

@@ -955,11 +955,13 @@ static void launch_b(hipStream_t s, const DevState<T>& st, const Params<T>& prm,
 
 // MFMA partial Cholesky (msckf_mchol.h): NW waves, TPW tiles per wave
 constexpr int MC_NW = 16;
-template <typename K>
-static void set_lds_attr(K* k) {
+// one flag per kernel instantiation (a template over the kernel itself: kernels
+// of one signature must not share it)
+template <auto K>
+static void set_lds_attr() {
     static bool done = false;
     if (!done) {
-        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)K, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         done = true;
     }
 }
@@ -971,10 +973,10 @@ void launch_kalman_a_reg(hipStream_t s, const DevState<T>& st, const UpdWs<T>& w
     const size_t lds = mchol_lds_doubles(nrow) * sizeof(double);
     kt->begin(s, "kalman_a");
     if (nrow * (nrow + 1) / 2 <= MC_NW * 4) {
-        set_lds_attr(k_kal_am<T, MC_NW, 4>);
+        set_lds_attr<k_kal_am<T, MC_NW, 4>>();
         hipLaunchKernelGGL((k_kal_am<T, MC_NW, 4>), dim3(st.B), dim3(64 * MC_NW), lds, s, st, ws);
     } else {   // nrow <= 14 (C <= 192): 105 tiles
-        set_lds_attr(k_kal_am<T, MC_NW, 7>);
+        set_lds_attr<k_kal_am<T, MC_NW, 7>>();
         hipLaunchKernelGGL((k_kal_am<T, MC_NW, 7>), dim3(st.B), dim3(64 * MC_NW), lds, s, st, ws);
     }
     kt->end(s);
@@ -1007,10 +1009,10 @@ void launch_kalman_chol(hipStream_t s, const DevState<T>& st, const Params<T>& p
         const int nT1 = Cq / 16;
         const size_t lds = mchol_lds_doubles(nT1) * sizeof(double);
         if (nT1 * (nT1 + 1) / 2 <= MC_NW * 3) {
-            set_lds_attr(k_kal_c1m<T, MC_NW, 3>);
+            set_lds_attr<k_kal_c1m<T, MC_NW, 3>>();
             hipLaunchKernelGGL((k_kal_c1m<T, MC_NW, 3>), dim3(st.B), dim3(64 * MC_NW), lds, s, st, ws);
         } else {   // nT1 <= 12: 78 tiles
-            set_lds_attr(k_kal_c1m<T, MC_NW, 5>);
+            set_lds_attr<k_kal_c1m<T, MC_NW, 5>>();
             hipLaunchKernelGGL((k_kal_c1m<T, MC_NW, 5>), dim3(st.B), dim3(64 * MC_NW), lds, s, st, ws);
         }
         if (Cq <= 16 * 8) launch_c2<T, 7, 2, 8>(s, st, ws);
