@@ -5,7 +5,7 @@
 #include <cmath>
 #include <cstdio>
 #include <vector>
-#include "../../visual-inertial-odometry-msckf-stereo_amd/csrc/msckf_mchol.h"
+#include "msckf_mchol.h"
 using namespace msckf;
 
 template <int NW, int TPW>
@@ -17,7 +17,7 @@ __global__ void __launch_bounds__(64 * NW) k_test(const double* A, int n, int nr
     mchol_core<NW, TPW>(nrow, nrow, nelim, lds, load, out, trail, 0.0);
 }
 
-template <int TPW>
+template <int NW, int TPW>
 static int run(int nrow, int nelim) {
     const int n = 16 * nrow, m = 16 * nelim;
     std::vector<double> A(n * n), X(n * n);
@@ -43,8 +43,8 @@ static int run(int nrow, int nelim) {
     hipMemcpy(dA, A.data(), n * n * 8, hipMemcpyHostToDevice);
     hipMemset(dL, 0, n * n * 8); hipMemset(dS, 0, n * n * 8);
     const size_t lds = mchol_lds_doubles(nrow) * 8;
-    (void)hipFuncSetAttribute((const void*)k_test<16, TPW>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    hipLaunchKernelGGL((k_test<16, TPW>), dim3(1), dim3(1024), lds, 0, dA, n, nrow, nelim, dL, dS);
+    (void)hipFuncSetAttribute((const void*)k_test<NW, TPW>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipLaunchKernelGGL((k_test<NW, TPW>), dim3(1), dim3(64 * NW), lds, 0, dA, n, nrow, nelim, dL, dS);
     hipError_t e = hipDeviceSynchronize();
     std::vector<double> L(n * n), S(n * n);
     hipMemcpy(L.data(), dL, n * n * 8, hipMemcpyDeviceToHost);
@@ -56,7 +56,7 @@ static int run(int nrow, int nelim) {
             else if (j < m) eP = std::fmax(eP, std::fabs(L[i * n + j] - H[i * n + j]));
             else eS = std::fmax(eS, std::fabs(S[i * n + j] - H[i * n + j]));
         }
-    printf("mchol probe nrow %d nelim %d TPW %d (%s): max |dL| %.3e  panel %.3e  schur %.3e\n", nrow, nelim, TPW,
+    printf("mchol probe NW %d nrow %d nelim %d TPW %d (%s): max |dL| %.3e  panel %.3e  schur %.3e\n", NW, nrow, nelim, TPW,
            hipGetErrorString(e), eL, eP, eS);
     // first bad entries
     int shown = 0;
@@ -65,16 +65,30 @@ static int run(int nrow, int nelim) {
             const double ref = H[i * n + j], got = j < m ? L[i * n + j] : S[i * n + j];
             if (std::fabs(got - ref) > 1e-9 * (1 + std::fabs(ref))) { printf("  (%d,%d) got %.6g ref %.6g\n", i, j, got, ref); ++shown; }
         }
+    // throughput: 2048 workgroups on the same matrix (identical writes)
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0); hipEventCreate(&e1);
+    for (int rep = 0; rep < 2; ++rep) {
+        hipEventRecord(e0, 0);
+        hipLaunchKernelGGL((k_test<NW, TPW>), dim3(2048), dim3(64 * NW), lds, 0, dA, n, nrow, nelim, dL, dS);
+        hipEventRecord(e1, 0);
+        hipEventSynchronize(e1);
+    }
+    float ms = 0;
+    hipEventElapsedTime(&ms, e0, e1);
+    printf("   2048 workgroups: %.3f ms (lds %zu B)\n", ms, lds);
     hipFree(dA); hipFree(dL); hipFree(dS);
     return 0;
 }
 
 int main() {
-    run<4>(6, 4);
-    run<4>(10, 8);
-    run<7>(10, 8);
-    run<7>(14, 12);
-    run<5>(12, 12);
-    run<4>(5, 5);
+    run<16, 4>(6, 4);
+    run<16, 7>(14, 12);
+    run<16, 5>(12, 12);
+    run<8, 3>(6, 4);
+    run<8, 14>(14, 12);
+    run<8, 10>(12, 12);
+    run<4, 27>(14, 12);
+    run<4, 20>(12, 12);
     return 0;
 }

@@ -14,14 +14,12 @@
 //   C  k_kal_c1  Cholesky of T; k_kal_c2: W^T = L_T^-1 [Vc_i ; Lc]^T and
 //                y = L_T^-1 c (MFMA blocked forward substitution)
 //   E  k_kal_e1  P+ = blockdiag(S_ii, 0) + s2 W W^T and dx = W y
-// Up to 32 cams A and C1 keep the matrix in VGPRs as 16 x 16 fp64 MFMA
-// accumulator tiles (one workgroup per filter, msckf_mchol.h); larger windows
-// run A and C as blocked global-memory Choleskys (k_gchol_*) and B / E as
-// 64 x 64-tiled GEMMs (k_kal_b1/b2, k_kal_e).
+// Up to 32 cams A and C1 keep the matrix in registers as 4x4 tiles (one
+// workgroup per filter); larger windows run A and C as blocked global-memory
+// Choleskys (k_gchol_*) and B / E as 64 x 64-tiled GEMMs (k_kal_b1/b2, k_kal_e).
 #include "msckf_common.h"
 #include "msckf_launch.h"
 #include "msckf_rchol.h"
-#include "msckf_mchol.h"
 
 namespace msckf {
 
@@ -54,69 +52,41 @@ __device__ double pcc_pivot_floor(const T* P, int ld, int C, double* lds) {
     return m * KALMAN_PIVOT_FLOOR;
 }
 
-// ---- stage A on the matrix cores (register-tile windows, C <= 192): the
-// same partial Cholesky as k_kal_a in index space [cams (Cq) | IMU (32)],
-// 16-pivot MFMA steps (msckf_mchol.h) ----
-template <typename T, int NW, int TPW>
-__global__ void __launch_bounds__(64 * NW) k_kal_am(DevState<T> st, UpdWs<T> ws) {
+// ---- stage A: [P_cc P_ci; P_ic P_ii] in index space [cams (Cp) | IMU (24)] ----
+template <typename T, int NT, int TPL>
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 ? 2 : 1))) k_kal_a(DevState<T> st, UpdWs<T> ws) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    double* lds = reinterpret_cast<double*>(smem_raw);
+    // launched before k_select (side stream): every filter is factored, the
+    // status goes to afail only, and k_kal_c1 turns it into info[3] for the
+    // filters that do update
     const int b = blockIdx.x;
-    const int C = 6 * st.ncams[b], Cq = (C + 15) & ~15;
-    const int nrow = Cq / 16 + 2;   // the cam pivots, then the 21 IMU rows padded to 32
+    const int C = 6 * st.ncams[b], Cp = round4(C);
+    const int nrow = (Cp + KW) / 4;
     const T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
     const int ld = st.Dmax, Cpw = ws.Cp;
     KT* Lc = ws.Lc + (size_t)b * Cpw * Cpw;
     KT* Vi = ws.Vi + (size_t)b * KW * Cpw;
     KT* Sii = ws.Sii + (size_t)b * KW * KW;
-    auto map = [&](int i) { return i < C ? 21 + i : (i < Cq ? -1 : (i - Cq < 21 ? i - Cq : -1)); };
+    auto map = [&](int i) { return i < C ? 21 + i : (i < Cp ? -1 : (i < Cp + 21 ? i - Cp : -1)); };
     auto load = [&](int i, int j) -> double {
         const int mi = map(i), mj = map(j);
         if (mi < 0 || mj < 0) return i == j ? 1.0 : 0.0;
         return (double)P[(size_t)mi * ld + mj];
     };
-    auto out = [&](int i, int j, double v) {
-        if (i < Cq) Lc[(size_t)i * Cpw + j] = v;
-        else if (i - Cq < KW) Vi[(size_t)(i - Cq) * Cpw + j] = v;
+    auto panel = [&](int r, int c0, double w0, double w1, double w2, double w3) {
+        KT* dst = r < Cp ? Lc + (size_t)r * Cpw + c0 : Vi + (size_t)(r - Cp) * Cpw + c0;
+        dst[0] = w0; dst[1] = w1; dst[2] = w2; dst[3] = w3;
     };
-    auto trail = [&](int i, int j, double v) {
-        if (i - Cq < KW && j - Cq < KW) Sii[(i - Cq) * KW + (j - Cq)] = v;
-    };
-    const double floor = pcc_pivot_floor(P, ld, C, lds);
-    const bool ok = mchol_core<NW, TPW>(nrow, nrow, Cq / 16, lds, load, out, trail, floor);
-    if (threadIdx.x == 0) ws.afail[b] = ok ? 0 : 1;   // read by k_kal_c1m
-}
-
-// ---- stage C1 on the matrix cores: Cholesky of T (C x C, identity-padded to Cq) ----
-template <typename T, int NW, int TPW>
-__global__ void __launch_bounds__(64 * NW) k_kal_c1m(DevState<T> st, UpdWs<T> ws) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    const int b = blockIdx.x;
-    if (ws.info[4 * b] == 0) return;
-    if (ws.afail[b]) {   // stage A failed (P_cc not PD): no update for this filter
-        if (threadIdx.x == 0) ws.info[4 * b + 3] = -1;
-        return;
-    }
-    const int C = 6 * st.ncams[b], Cq = (C + 15) & ~15;
-    const int ldt = ws.Cmax + 1;
-    const KT* Tm = ws.Tm + (size_t)b * ws.Cmax * ldt;
-    KT* L = ws.G + (size_t)b * ws.Cmax * ldt;
-    auto load = [&](int i, int j) -> double {
-        if (i >= C || j >= C) return i == j ? 1.0 : 0.0;
-        return i >= j ? Tm[(size_t)i * ldt + j] : Tm[(size_t)j * ldt + i];
-    };
-    auto out = [&](int i, int j, double v) {
-        if (i < C && j < C) L[(size_t)i * ldt + j] = v;
-    };
-    auto trail = [](int, int, double) {};
-    const bool ok = mchol_core<NW, TPW>(Cq / 16, Cq / 16, Cq / 16, reinterpret_cast<double*>(smem_raw), load, out,
-                                        trail, 0.0);
-    if (!ok && threadIdx.x == 0) ws.info[4 * b + 3] = -1;
+    auto trail = [&](int i, int j, double v) { Sii[(i - Cp) * KW + (j - Cp)] = v; };
+    const double floor = pcc_pivot_floor(P, ld, C, reinterpret_cast<double*>(smem_raw));
+    const bool ok = rchol_core<NT, TPL>(nrow, nrow, Cp / 4, reinterpret_cast<double*>(smem_raw), load, panel, trail,
+                                        floor);
+    if (threadIdx.x == 0) ws.afail[b] = ok ? 0 : 1;   // read by k_kal_c1
 }
 
 // ---- stage C (register-tile windows, C <= 192) ----
-// C1: Cholesky of T alone (k_kal_c1m above, MFMA), L_T written over the G
-//     workspace (free after stage B).
+// C1: Cholesky of T alone (4x4 register tiles, one workgroup per filter), L_T
+//     written over the G workspace (free after stage B).
 // C2: W^T = L_T^-1 X^T with X = [Vc_i ; Lc ; c^T] (E = 22 + C rows) as a
 //     blocked forward substitution on MFMA: wave w owns the 16-row tiles
 //     ct = w + NW t of X and keeps the solved blocks Y'[K] (16 x 16, K < nT) in
@@ -127,6 +97,36 @@ __global__ void __launch_bounds__(64 * NW) k_kal_c1m(DevState<T> st, UpdWs<T> ws
 //     with -L_T[J, 0:16J] staged in LDS ([col][row], 17-double rows) and the
 //     16 x 16 inverses of the diagonal blocks formed once up front.  W^T is
 //     stored row-major over k (coalesced), the layout k_kal_e1 reads.
+template <typename T, int NT, int TPL>
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 ? 2 : 1))) k_kal_c1(DevState<T> st, UpdWs<T> ws) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    const int b = blockIdx.x;
+    if (ws.info[4 * b] == 0) return;
+    if (ws.afail[b]) {   // stage A failed (P_cc not PD): no update for this filter
+        if (threadIdx.x == 0) ws.info[4 * b + 3] = -1;
+        return;
+    }
+    const int C = 6 * st.ncams[b], Cp = round4(C), nTc = Cp / 4;
+    const int ldt = ws.Cmax + 1;
+    const KT* Tm = ws.Tm + (size_t)b * ws.Cmax * ldt;
+    KT* L = ws.G + (size_t)b * ws.Cmax * ldt;
+    auto load = [&](int i, int j) -> double {
+        if (i >= C || j >= C) return i == j ? 1.0 : 0.0;
+        return i >= j ? Tm[(size_t)i * ldt + j] : Tm[(size_t)j * ldt + i];
+    };
+    auto panel = [&](int r, int c0, double w0, double w1, double w2, double w3) {
+        if (r >= C) return;
+        KT* dst = L + (size_t)r * ldt;
+        const double w[4] = {w0, w1, w2, w3};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (c0 + q < C && c0 + q <= r) dst[c0 + q] = w[q];
+    };
+    auto trail = [](int, int, double) {};
+    const bool ok = rchol_core<NT, TPL>(nTc, nTc, nTc, reinterpret_cast<double*>(smem_raw), load, panel, trail);
+    if (!ok && threadIdx.x == 0) ws.info[4 * b + 3] = -1;
+}
+
 constexpr int C2S = 17;   // LDS row stride (doubles) of the staged L_T block row
 
 template <typename T, int NW, int CT, int NTM>
@@ -890,6 +890,20 @@ __global__ void __launch_bounds__(64 * NW) k_kal_e1(DevState<T> st, Params<T> pr
 // ===========================================================================
 // Host side
 // ===========================================================================
+struct RcholCfg { int nt, tpl; };
+
+static bool pick_rchol(int tiles, RcholCfg& c) {
+    if (tiles <= 256 * 4) { c = {256, 4}; return true; }
+    if (tiles <= 256 * 6) { c = {256, 6}; return true; }
+    if (tiles <= 512 * 4) { c = {512, 4}; return true; }
+    return false;
+}
+
+template <typename T, int NT, int TPL>
+static void launch_a_cfg(hipStream_t s, const DevState<T>& st, const UpdWs<T>& ws, size_t lds) {
+    hipLaunchKernelGGL((k_kal_a<T, NT, TPL>), dim3(st.B), dim3(NT), lds, s, st, ws);
+}
+
 // Host side of the blocked global-memory factorisation (large windows).
 template <int STAGE, typename T>
 static void launch_gchol(hipStream_t s, const DevState<T>& st, const UpdWs<T>& ws) {
@@ -929,6 +943,10 @@ static void launch_e1(hipStream_t s, const DevState<T>& st, const Params<T>& prm
     hipLaunchKernelGGL((k_kal_e1<T, NW, TPW>), dim3(st.B), dim3(64 * NW), lds, s, st, prm, ws);
 }
 
+template <typename T, int NT, int TPL>
+static void launch_c1(hipStream_t s, const DevState<T>& st, const UpdWs<T>& ws, size_t lds) {
+    hipLaunchKernelGGL((k_kal_c1<T, NT, TPL>), dim3(st.B), dim3(NT), lds, s, st, ws);
+}
 template <typename T, int NW, int CT, int NTM>
 static void launch_c2(hipStream_t s, const DevState<T>& st, const UpdWs<T>& ws) {
     constexpr int IMG = 16 * NTM * C2S > NW * 272 ? 16 * NTM * C2S : NW * 272;
@@ -953,39 +971,24 @@ static void launch_b(hipStream_t s, const DevState<T>& st, const Params<T>& prm,
     hipLaunchKernelGGL((k_kal_b<T, NW, WR, WC, NTM>), dim3(st.B), dim3(64 * NW), lds, s, st, prm, ws);
 }
 
-// MFMA partial Cholesky (msckf_mchol.h): NW waves, TPW tiles per wave
-constexpr int MC_NW = 16;
-// one flag per kernel instantiation (a template over the kernel itself: kernels
-// of one signature must not share it)
-template <auto K>
-static void set_lds_attr() {
-    static bool done = false;
-    if (!done) {
-        (void)hipFuncSetAttribute((const void*)K, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        done = true;
-    }
-}
-
 template <typename T>
 void launch_kalman_a_reg(hipStream_t s, const DevState<T>& st, const UpdWs<T>& ws, KernelTimer* kt) {
-    const int Cq = (ws.Cmax + 15) & ~15;
-    const int nrow = Cq / 16 + 2;   // stage A: cam tiles + the IMU rows
-    const size_t lds = mchol_lds_doubles(nrow) * sizeof(double);
+    const int Cp = (ws.Cmax + 3) & ~3;
+    const int nrow = (Cp + KW) / 4;   // stage A, 4x4 register tiles
+    RcholCfg c;
+    pick_rchol(nrow * (nrow + 1) / 2, c);
+    const size_t lds = rchol_lds_doubles(nrow) * sizeof(double);
     kt->begin(s, "kalman_a");
-    if (nrow * (nrow + 1) / 2 <= MC_NW * 4) {
-        set_lds_attr<k_kal_am<T, MC_NW, 4>>();
-        hipLaunchKernelGGL((k_kal_am<T, MC_NW, 4>), dim3(st.B), dim3(64 * MC_NW), lds, s, st, ws);
-    } else {   // nrow <= 14 (C <= 192): 105 tiles
-        set_lds_attr<k_kal_am<T, MC_NW, 7>>();
-        hipLaunchKernelGGL((k_kal_am<T, MC_NW, 7>), dim3(st.B), dim3(64 * MC_NW), lds, s, st, ws);
-    }
+    if (c.nt == 256 && c.tpl == 4) launch_a_cfg<T, 256, 4>(s, st, ws, lds);
+    else if (c.nt == 256) launch_a_cfg<T, 256, 6>(s, st, ws, lds);
+    else launch_a_cfg<T, 512, 4>(s, st, ws, lds);
     kt->end(s);
 }
 
 template <typename T>
 void launch_kalman_chol(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const UpdWs<T>& ws,
                         KernelTimer* kt) {
-    const int Cmax = ws.Cmax;
+    const int Cp = (ws.Cmax + 3) & ~3, Cmax = ws.Cmax;
     const bool reg = kalman_chol_supported(Cmax);   // else large window: global-memory stages A and C
     const int Cq = (Cmax + 15) & ~15;
     if (!reg) {   // (register-tile stage A: launch_kalman_a_reg, on the side stream)
@@ -1005,16 +1008,14 @@ void launch_kalman_chol(hipStream_t s, const DevState<T>& st, const Params<T>& p
     }
     kt->end(s);
     kt->begin(s, "kalman_c");
-    if (reg) {   // C1: Cholesky of T (MFMA, msckf_mchol.h); C2: MFMA forward substitution of the extra rows
-        const int nT1 = Cq / 16;
-        const size_t lds = mchol_lds_doubles(nT1) * sizeof(double);
-        if (nT1 * (nT1 + 1) / 2 <= MC_NW * 3) {
-            set_lds_attr<k_kal_c1m<T, MC_NW, 3>>();
-            hipLaunchKernelGGL((k_kal_c1m<T, MC_NW, 3>), dim3(st.B), dim3(64 * MC_NW), lds, s, st, ws);
-        } else {   // nT1 <= 12: 78 tiles
-            set_lds_attr<k_kal_c1m<T, MC_NW, 5>>();
-            hipLaunchKernelGGL((k_kal_c1m<T, MC_NW, 5>), dim3(st.B), dim3(64 * MC_NW), lds, s, st, ws);
-        }
+    if (reg) {   // C1: Cholesky of T (register tiles); C2: MFMA forward substitution of the extra rows
+        const int nTc = Cp / 4;
+        RcholCfg c;
+        pick_rchol(nTc * (nTc + 1) / 2, c);
+        const size_t lds = rchol_lds_doubles(nTc) * sizeof(double);
+        if (c.nt == 256 && c.tpl == 4) launch_c1<T, 256, 4>(s, st, ws, lds);
+        else if (c.nt == 256) launch_c1<T, 256, 6>(s, st, ws, lds);
+        else launch_c1<T, 512, 4>(s, st, ws, lds);
         if (Cq <= 16 * 8) launch_c2<T, 7, 2, 8>(s, st, ws);
         else launch_c2<T, 13, 1, 12>(s, st, ws);
     } else {
