@@ -371,9 +371,7 @@ def test_gate_fp64_gamma_vs_oracle(N, F, B):
     """fp64 gating against the oracle's gamma (msckf.py:606-614), relative
     1e-9: the one-wave fp64 MFMA kernel (v_mfma_f64_16x16x4_f64, its own
     accumulator row layout) for every class up to 6 blocks (M <= 30, single- and
-    multi-pass Y staging), the eight-wave fp64 MFMA workgroup kernel for
-    30 < M <= 82 (7..16 blocks, two block rows per wave, Y staged in passes);
-    decisions identical."""
+    multi-pass Y staging), k_gate_wave for 31 <= M <= 40; decisions identical."""
     problems = [synth.make_update_problem(N, F, seed=700 + b) for b in range(B)]
     ctx, ds, feat_off, acc, gam, pw, valid, rows = _batched(problems, np.float64)
     n = 0

@@ -839,297 +839,6 @@ __global__ void __launch_bounds__(256) k_gate_mfma_wg(DevState<float> st, Params
     }
 }
 
-// ---------------------------------------------------------------------------
-// fp64 large tracks (30 < M <= 82, nb <= 16 blocks): the same elimination on
-// v_mfma_f64_16x16x4_f64 with eight waves per feature.  An fp64 16x16 block is
-// eight registers per lane, so the lower block triangle (up to 136 blocks)
-// is spread as evenly as whole block rows allow: wave w owns block rows
-// RB0 = w (blocks c = 0..w, in slots 16 - c) and RB1 = 15 - w (blocks c =
-// 0..15 - w, in slots c) -- 17 accumulator slots per wave, every slot a
-// compile-time register array index with a compile-time block column.
-// Result layout (f64): lane l holds column l & 15, rows (l >> 4) + 4 i.
-// Per 4-pivot step: the owners of the pivot columns dump them into a
-// double-buffered LDS panel, one barrier, then every wave factors the 4x4
-// diagonal, forms the B operands of every block column and the A operands of
-// its two rows, and updates its blocks.  Y pairs are staged in passes over
-// observation rows by all 512 threads (one P row in flight per thread), each
-// pass followed by the owners' assembly.  (Replaces k_gate_wave / k_gate_big's
-// VALU register tiles in the fp64 contexts.)
-constexpr int G8_NB = 16, G8_SLOTS = 17;
-__host__ __device__ constexpr int g8_pan() { return 2 * 16 * G8_NB * 4; }   // doubles, double-buffered
-__host__ __device__ constexpr int g8_doubles(int Mmax, int capb) {
-    return gm_head(Mmax) + g8_pan() + ((9 * capb + 3) & ~3) + 2 * ((Mmax + 3) & ~3) + 16;
-}
-
-__global__ void __launch_bounds__(512) k_gate_mfma_wg64(DevState<double> st, Params<double> prm,
-                                                        FeatBatch<double> fb, const int* __restrict__ flist,
-                                                        int Mmax, int capb) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int f = __builtin_amdgcn_readfirstlane(flist[blockIdx.x]);
-    if (!fb.valid[f]) {
-        if (tid == 0) { fb.gamma[f] = NAN; fb.accept[f] = 0; }
-        return;
-    }
-    const double chi2 = fb.chi2[f];
-    const int b = __builtin_amdgcn_readfirstlane(fb.feat_filter[f]);
-    const int o0 = __builtin_amdgcn_readfirstlane(fb.obs_off[f]);
-    const int M = __builtin_amdgcn_readfirstlane(fb.obs_off[f + 1]) - o0, M3 = 3 * M;
-    const int nY = (M3 + 3) >> 2;
-    const int nb = gm_nb(M);
-    const int nB = 16 * nb - 4;
-    double* ht = reinterpret_cast<double*>(smem_raw);
-    double* rt = ht + 18 * Mmax;
-    double* pan = ht + gm_head(Mmax);                 // [2][16 G8_NB][4]
-    double* stage = pan + g8_pan();                   // [capb][9]
-    double* fin = stage + ((9 * capb + 3) & ~3);      // [16] the B rows' Schur block
-    int* slot = reinterpret_cast<int*>(fin + 16);     // [Mmax] P row offsets, then [Mmax] column offsets
-    int* coff = slot + ((Mmax + 3) & ~3);
-    {   // records as element pairs, cam offsets (all loads issued before the first wait)
-        constexpr int NCH = (12 * 84 + 511) / 512;
-        const D2* src = reinterpret_cast<const D2*>(fb.obs_ht + (size_t)o0 * OBS_HTS);
-        D2 cv[NCH];
-#pragma unroll
-        for (int j = 0; j < NCH; ++j) {
-            const int k = tid + 512 * j;
-            cv[j] = k < 12 * M ? src[k] : D2{0, 0};
-        }
-        const int sl = tid < M ? fb.obs_cam[o0 + tid] : 0;
-#pragma unroll
-        for (int j = 0; j < NCH; ++j) {
-            const int k = tid + 512 * j, o = k / 12, e = 2 * (k - 12 * o);
-            if (k < 12 * M) {
-                if (e < OBS_RT) *reinterpret_cast<D2*>(ht + 18 * o + e) = cv[j];
-                else if (e < OBS_RT + 4) *reinterpret_cast<D2*>(rt + 4 * o + (e - OBS_RT)) = cv[j];
-            }
-        }
-        if (tid < M) {
-            slot[tid] = (21 + 6 * sl) * st.Dmax + 21;
-            coff[tid] = 6 * sl;
-        }
-    }
-    __syncthreads();
-
-    const int col_l = lane & 15, rg = lane >> 4;
-    const int RB0 = w, RB1 = 15 - w;   // this wave's block rows
-    D4 acc[G8_SLOTS];
-    const double s2 = prm.sigma2;
-    // slot s holds block (RB1, s) when s <= RB1, else (RB0, 16 - s)
-    // Assembly of this wave's blocks whose block row lies in [R0, R1): every
-    // element written once (Y entries from the pass's pair stage, kbase = its
-    // first pair; B rows; unit padding pivots; zeros) -- no accumulator read back.
-    auto assemble = [&](int R0, int R1, int kbase) {
-        int cl = lane & 15, rr = lane >> 4;   // opaque copies: index math stays in the pass loop
-        asm volatile("" : "+v"(cl), "+v"(rr));
-#pragma unroll
-        for (int s = 0; s < G8_SLOTS; ++s) {
-            const bool hi = s <= RB1;
-            const int RB = hi ? RB1 : RB0, c = hi ? s : 16 - s;
-            if (RB >= nb || RB < R0 || RB >= R1 || c > RB) continue;   // uniform
-            const int p = 16 * c + cl, ob = p / 3, cp = p - 3 * ob;
-            double bval3 = 0.0;   // element 3 of block nb - 1: B row rr (rows 12..15)
-            if (RB == nb - 1) {
-                const bool pv = p < M3;
-                const int o = pv ? ob : 0;
-                const double hv = rr < 3 ? ht[18 * o + 6 * cp + 3 + rr] : rt[4 * o + cp];
-                bval3 = pv ? (rr < 3 ? -hv : hv) : 0.0;
-            }
-            D4 a;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int q = 16 * RB + rr + 4 * i, oa = q / 3;
-                const bool take = q < M3 && (RB > c || q >= p);
-                const int ofs = 9 * (oa * (oa + 1) / 2 - kbase) + 3 * (q - 3 * oa) + 9 * ob + cp;
-                const double y = stage[take ? ofs : 0];
-                double v = i == 3 ? bval3 : 0.0;
-                if (q == p && q >= M3 && q < nB) v = 1.0;
-                a[i] = take ? y + (q == p ? s2 : 0.0) : v;
-            }
-            acc[s] = a;
-        }
-    };
-
-    const double* P = st.P + (size_t)b * st.Dmax * st.Dmax;
-    const int ldp = st.Dmax;
-    auto npairs = [&](int lo, int hi) { return hi < lo ? 0 : (hi + 1) * (hi + 2) / 2 - lo * (lo + 1) / 2; };
-    for (int R0 = 0; R0 < nb;) {
-        const int alo = (16 * R0) / 3;
-        int R1 = R0 + 1, ahi = min(M - 1, (16 * R1 - 1) / 3);
-        while (R1 < nb) {
-            const int ah2 = min(M - 1, (16 * (R1 + 1) - 1) / 3);
-            if (npairs(alo, ah2) > capb) break;
-            ++R1;
-            ahi = ah2;
-        }
-        const int kbase = alo * (alo + 1) / 2, nbp = npairs(alo, ahi);
-#pragma unroll 1
-        for (int kk = tid; kk < nbp; kk += 512) {
-            const int k = kbase + kk;
-            int a = (int)((__builtin_amdgcn_sqrtf(8.0f * (float)k + 1.0f) - 1.0f) * 0.5f);
-            if (a * (a + 1) / 2 > k) --a;
-            if ((a + 1) * (a + 2) / 2 <= k) ++a;
-            const int bo = k - a * (a + 1) / 2;
-            const double* Pb = P + (slot[a] + coff[bo]);
-            const double* Ha = ht + 18 * a;
-            const double* Hb = ht + 18 * bo;
-            D2 t[3][3];   // Ha[x] P as three column pairs, P streamed a row at a time
-#pragma unroll
-            for (int x = 0; x < 3; ++x)
-#pragma unroll
-                for (int c = 0; c < 3; ++c) t[x][c] = D2{0, 0};
-#pragma unroll
-            for (int u = 0; u < 6; ++u) {
-                double pr[6];
-                __builtin_memcpy(pr, Pb + u * ldp, 6 * sizeof(double));
-#pragma unroll
-                for (int x = 0; x < 3; ++x) {
-                    const double h = Ha[6 * x + u];
-#pragma unroll
-                    for (int c = 0; c < 3; ++c)
-                        t[x][c] = __builtin_elementwise_fma(D2{h, h}, D2{pr[2 * c], pr[2 * c + 1]}, t[x][c]);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            double* dst = stage + 9 * kk;
-#pragma unroll
-            for (int x = 0; x < 3; ++x) {
-                const double t1[6] = {t[x][0].x, t[x][0].y, t[x][1].x, t[x][1].y, t[x][2].x, t[x][2].y};
-#pragma unroll
-                for (int y = 0; y < 3; ++y) {
-                    double ay = 0.0;
-#pragma unroll
-                    for (int u = 0; u < 6; ++u) ay = fma(t1[u], Hb[6 * y + u], ay);
-                    dst[3 * x + y] = ay;
-                }
-            }
-        }
-        __syncthreads();
-        assemble(R0, R1, kbase);
-        __syncthreads();
-        R0 = R1;
-    }
-
-    bool fail = false;
-    const int csel = rg;
-    // (a runtime loop: every accumulator access is in a slot loop unrolled
-    // inside it, selected by uniform tests -- unrolled over KB, the scheduler
-    // hoisted panel reads across steps and spilled)
-#pragma unroll 1
-    for (int KB = 0; KB < G8_NB; ++KB) {
-        if (4 * KB >= nY || fail) break;
-        for (int sc = 0; sc < 4; ++sc) {
-            const int j = 4 * KB + sc;
-            if (j >= nY) break;
-            const int p0 = 4 * j;
-            double* pb = pan + (j & 1) * (16 * G8_NB * 4);
-            // 1. the owners of block column KB dump its four columns p0 .. p0 + 3
-            //    (slot KB holds block (RB1, KB), slot 16 - KB block (RB0, KB))
-            if ((col_l >> 2) == sc) {
-                double* dd = pb + 4 * rg + (col_l & 3);
-#pragma unroll
-                for (int s = 0; s < G8_SLOTS; ++s) {
-                    const bool hi = s <= RB1;
-                    const int RB = hi ? RB1 : RB0, c = hi ? s : 16 - s;
-                    if (c != KB || RB >= nb || (!hi && RB0 == RB1)) continue;   // uniform
-                    const D4 v = acc[s];
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) dd[4 * (16 * RB + 4 * i)] = v[i];
-                }
-            }
-            LDS_BARRIER();
-            // 2. the 4x4 diagonal A_d = L D L^T, and column csel of -A_d^-1 = -(L^-T D^-1 L^-1)
-            const D4 r0 = *reinterpret_cast<const D4*>(pb + 4 * p0);
-            const D4 r1 = *reinterpret_cast<const D4*>(pb + 4 * p0 + 4);
-            const D4 r2 = *reinterpret_cast<const D4*>(pb + 4 * p0 + 8);
-            const D4 r3 = *reinterpret_cast<const D4*>(pb + 4 * p0 + 12);
-            const double d0 = r0.x, e0 = 1.0 / d0;
-            const double l10 = r1.x * e0, l20 = r2.x * e0, l30 = r3.x * e0;
-            const double d1 = r1.y - l10 * r1.x, e1 = 1.0 / d1;
-            const double m21 = r2.y - l20 * r1.x, m31 = r3.y - l30 * r1.x;
-            const double l21 = m21 * e1, l31 = m31 * e1;
-            const double d2 = r2.z - l20 * r2.x - l21 * m21, e2 = 1.0 / d2;
-            const double m32 = r3.z - l30 * r2.x - l31 * m21;
-            const double l32 = m32 * e2;
-            const double d3 = r3.w - l30 * r3.x - l31 * m31 - l32 * m32;
-            if (!(d0 > 0.0) || !(d1 > 0.0) || !(d2 > 0.0) || !(d3 > 0.0)) { fail = true; break; }   // same in every wave
-            const double e3 = 1.0 / d3;
-            const double i10 = -l10, i21 = -l21, i32 = -l32;
-            const double i20 = -l20 - l21 * i10, i31 = -l31 - l32 * i21;
-            const double i30 = -l30 - l31 * i10 - l32 * i20;
-            const double u0 = csel == 0 ? e0 : 0.0;
-            const double u1 = (csel == 1 ? 1.0 : (csel == 0 ? i10 : 0.0)) * e1;
-            const double u2 = (csel == 2 ? 1.0 : (csel == 1 ? i21 : (csel == 0 ? i20 : 0.0))) * e2;
-            const double u3 = (csel == 3 ? 1.0 : (csel == 2 ? i32 : (csel == 1 ? i31 : i30))) * e3;
-            const double mm3 = -u3;
-            const double mm2 = -fma(i32, u3, u2);
-            const double mm1 = -fma(i31, u3, fma(i21, u2, u1));
-            const double mm0 = -fma(i30, u3, fma(i20, u2, fma(i10, u1, u0)));
-            // 3. B operands of every block column: X itself (row 16 CB + col_l, pivot
-            //    csel; rows of finished pivots zeroed); A operands of this wave's two rows: X m
-            double bv[G8_NB];
-#pragma unroll
-            for (int CB = 0; CB < G8_NB; ++CB) {
-                const double x = pb[4 * (16 * CB + col_l) + csel];
-                bv[CB] = (16 * CB + col_l <= p0 + 3) ? 0.0 : x;
-            }
-            auto aop = [&](int RB) {
-                const D4 x = *reinterpret_cast<const D4*>(pb + 4 * (16 * RB + col_l));
-                const double a = fma(x.w, mm3, fma(x.z, mm2, fma(x.y, mm1, x.x * mm0)));
-                return (16 * RB + col_l <= p0 + 3) ? 0.0 : a;
-            };
-            const double av1 = RB1 >= KB && RB1 < nb ? aop(RB1) : 0.0;
-            const double av0 = RB0 >= KB && RB0 < nb && RB0 != RB1 ? aop(RB0) : 0.0;
-            // 4. the rank-4 update of this wave's blocks right of the panel (after a
-            //    block's last step its own column is finished: skipped)
-            //    -- one uniform branch per slot, operands picked by uniform selects
-#pragma unroll
-            for (int s = 0; s < G8_SLOTS; ++s) {
-                const bool hi = s <= RB1;   // block (RB1, s), else (RB0, 16 - s)
-                const int c = hi ? s : 16 - s, RB = hi ? RB1 : RB0;
-                const bool on = c >= KB && c <= RB && RB < nb && (hi || RB0 != RB1) && !(c == KB && sc == 3);
-                const double a = hi ? av1 : av0;
-                const double bb = hi ? bv[s < G8_NB ? s : 0] : bv[16 - s < G8_NB ? 16 - s : 0];
-                if (on) acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bb, acc[s], 0, 0, 0);
-            }
-        }
-    }
-    // the B rows' 4x4 Schur block: rows / cols 12..15 of block (nb - 1, nb - 1),
-    // element 3 of lanes col_l >= 12 (row 12 + rg)
-    LDS_BARRIER();
-    {
-        const int RB = nb - 1;
-        if (col_l >= 12) {
-#pragma unroll
-            for (int s = 0; s < G8_SLOTS; ++s) {   // compile-time slot indices only (a runtime one sends acc to scratch)
-                const bool hi = s <= RB1;
-                if ((hi ? RB1 : RB0) == RB && (hi ? s : 16 - s) == RB) fin[4 * rg + (col_l - 12)] = acc[s][3];
-            }
-        }
-    }
-    LDS_BARRIER();
-    if (w == 0) {
-        double rn2 = 0.0;
-        for (int o = lane; o < M; o += 64) rn2 += rt[4 * o + 3] * rt[4 * o + 3];
-        rn2 = wave_sum(rn2);
-        if (lane == 0) {
-            const double* a = fin;
-            const double d0 = a[0];
-            const double l10 = a[4] / d0, l20 = a[8] / d0, l30 = a[12] / d0;
-            const double d1 = a[5] - l10 * l10 * d0;
-            const double l21 = (a[9] - l20 * l10 * d0) / d1;
-            const double l31 = (a[13] - l30 * l10 * d0) / d1;
-            const double d2 = a[10] - l20 * l20 * d0 - l21 * l21 * d1;
-            const double l32 = (a[14] - l30 * l20 * d0 - l31 * l21 * d1) / d2;
-            const double d3 = a[15] - l30 * l30 * d0 - l31 * l31 * d1 - l32 * l32 * d2;
-            double gam = -d3 + rn2 / s2;
-            if (fail || !(d0 < 0.0) || !(d1 < 0.0) || !(d2 < 0.0) || !(gam == gam)) gam = INFINITY;
-            fb.gamma[f] = gam;
-            fb.accept[f] = (gam < chi2) ? 1 : 0;
-        }
-    }
-}
-
 template <typename T, int NB, bool MP>
 void launch_cfg(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const FeatBatch<T>& fb,
                 const int* list, int cnt, int Mmax, int capb, int wpb, size_t lds) {
@@ -1174,26 +883,6 @@ void launch_nb(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const
 // fp64 up to NB = 6 (M <= 30): beyond it the accumulators spill (k_gate_wave then)
 bool gate_mfma_fits(int maxM, int ts) { return maxM >= 1 && gm_nb(maxM) <= (ts == 8 ? 6 : 8); }
 bool gate_mfma_wg_fits(int maxM) { return maxM >= 1 && gm_nb(maxM) <= GW_NB; }
-bool gate_mfma_wg64_fits(int maxM) { return maxM >= 1 && gm_nb(maxM) <= G8_NB; }
-
-void launch_gate_mfma_wg64(hipStream_t s, const DevState<double>& st, const Params<double>& prm,
-                           const FeatBatch<double>& fb, const int* list, int cnt, int maxM) {
-    if (cnt <= 0) return;
-    // one workgroup per CU (the accumulators fill the register file): LDS up to
-    // 150 KB, the Y pairs staged in as many passes as that needs
-    const int fixed = gm_head(maxM) + g8_pan() + 2 * ((maxM + 3) & ~3) + 16 + 4;
-    int capb = ((150 * 1024) / (int)sizeof(double) - fixed) / 9;
-    const int nbk = maxM * (maxM + 1) / 2;
-    if (capb > nbk) capb = nbk;
-    if (capb < 6 * maxM) capb = 6 * maxM;
-    const size_t lds = (size_t)g8_doubles(maxM, capb) * sizeof(double);
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_gate_mfma_wg64, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        attr = true;
-    }
-    hipLaunchKernelGGL(k_gate_mfma_wg64, dim3(cnt), dim3(512), lds, s, st, prm, fb, list, maxM, capb);
-}
 
 void launch_gate_mfma_wg(hipStream_t s, const DevState<float>& st, const Params<float>& prm,
                          const FeatBatch<float>& fb, const int* list, int cnt, int maxM) {

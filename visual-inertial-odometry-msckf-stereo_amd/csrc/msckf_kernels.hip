@@ -2618,11 +2618,6 @@ void launch_gate(hipStream_t s, const DevState<T>& st, const Params<T>& prm, con
                 launch_gate_mfma_wg(s, st, prm, fb, list, cnt, maxM);
                 continue;
             }
-        } else {   // fp64 tracks beyond the one-wave MFMA kernel: fp64 MFMA tiles, one workgroup per feature
-            if (c == GateClasses::NC - 2 && gate_mfma_wg64_fits(maxM)) {
-                launch_gate_mfma_wg64(s, st, prm, fb, list, cnt, maxM);
-                continue;
-            }
         }
         if (c == GateClasses::NC - 2) {   // 40 < M <= 82: register tiles, one workgroup per feature
             const int nrow = gate_nt(maxM), tiles = nrow * (nrow + 1) / 2;

@@ -111,11 +111,6 @@ void launch_gate_mfma(hipStream_t, const DevState<T>&, const Params<T>&, const F
                       int maxM);
 // fp32 gating of large tracks (40 < M <= 82) on MFMA tiles, one 4-wave workgroup per feature
 bool gate_mfma_wg_fits(int maxM);
-// fp64 gating of tracks beyond the one-wave kernel (30 < M <= 82) on fp64 MFMA
-// tiles, one 8-wave workgroup per feature
-bool gate_mfma_wg64_fits(int maxM);
-void launch_gate_mfma_wg64(hipStream_t, const DevState<double>&, const Params<double>&, const FeatBatch<double>&,
-                           const int* list, int cnt, int maxM);
 void launch_gate_mfma_wg(hipStream_t, const DevState<float>&, const Params<float>&, const FeatBatch<float>&,
                          const int* list, int cnt, int maxM);
 template <typename T>
