@@ -177,13 +177,20 @@ def _weights(a, b):
     return iw00, iw01, iw10, (1 << W_BITS) - iw00 - iw01 - iw10
 
 
-def _patch(src, x0, y0, win, w):
+def _patch(src, x0, y0, win, w, zero_border=False):
     """Bilinear window (win x win) at integer corner (x0, y0) with fixed-point
-    weights; the image is read with BORDER_REFLECT_101 beyond its edges."""
+    weights.  Beyond the edges the image is read with BORDER_REFLECT_101 (the
+    pyramid's border) and the derivatives as zeros (zero_border): given raw
+    images, calcOpticalFlowPyrLK pads derivI with copyMakeBorder(...,
+    BORDER_CONSTANT) (lkpyramid.cpp), while calcScharrDeriv itself reflects
+    inside the image."""
     H, W = src.shape
-    ys = reflect101(np.arange(y0, y0 + win + 1), H)
-    xs = reflect101(np.arange(x0, x0 + win + 1), W)
-    p = src[ys][:, xs].astype(np.int64)
+    ys, xs = np.arange(y0, y0 + win + 1), np.arange(x0, x0 + win + 1)
+    if zero_border:
+        inside = ((ys >= 0) & (ys < H))[:, None] & ((xs >= 0) & (xs < W))[None, :]
+        p = np.where(inside, src[np.clip(ys, 0, H - 1)][:, np.clip(xs, 0, W - 1)], 0).astype(np.int64)
+    else:
+        p = src[reflect101(ys, H)][:, reflect101(xs, W)].astype(np.int64)
     return p[:-1, :-1] * w[0] + p[:-1, 1:] * w[1] + p[1:, :-1] * w[2] + p[1:, 1:] * w[3]
 
 
@@ -221,8 +228,8 @@ def lk_track(prev_img, next_img, prev_pts, next_pts, win=15, max_level=3, max_it
             a, b = prev_pt[0] - np.float32(ipx), prev_pt[1] - np.float32(ipy)
             w = _weights(a, b)
             ival = _descale(_patch(I, ipx, ipy, win, w), W_BITS - 5)
-            ixv = _descale(_patch(Ix, ipx, ipy, win, w), W_BITS)
-            iyv = _descale(_patch(Iy, ipx, ipy, win, w), W_BITS)
+            ixv = _descale(_patch(Ix, ipx, ipy, win, w, zero_border=True), W_BITS)
+            iyv = _descale(_patch(Iy, ipx, ipy, win, w, zero_border=True), W_BITS)
             # window sums of integer products, exact (cv2 accumulates them in float;
             # the difference is below float32 resolution of the sums' ratio)
             A11 = np.float32(np.sum(ixv * ixv)) * np.float32(FLT_SCALE)
@@ -262,24 +269,35 @@ def lk_track(prev_img, next_img, prev_pts, next_pts, win=15, max_level=3, max_it
 # --------------------------------------------------- camera models ----
 def undistort_points(pts, intrinsics, model, coeffs, R=np.eye(3), new_intrinsics=(1, 1, 0, 0), iters=None):
     """cv2.undistortPoints (radtan: 5 fixed-point iterations, undistort.cpp)
-    or cv2.fisheye.undistortPoints (equidistant: Newton on theta, 10
-    iterations), then the rectification R and the new camera matrix."""
+    or cv2.fisheye.undistortPoints (equidistant: Newton on theta, at most 10
+    steps, stopping below 1e-8; cv2 4.x's rejection of non-converged or
+    sign-flipped theta as (-1e6, -1e6)), then the rectification R and the
+    new camera matrix."""
     pts = np.asarray(pts, float).reshape(-1, 2)
     fx, fy, cx, cy = map(float, intrinsics)
     k = np.asarray(coeffs, float)
     x = (pts[:, 0] - cx) / fx
     y = (pts[:, 1] - cy) / fy
+    bad = np.zeros(len(x), bool)
     if model == "equidistant":
-        td = np.sqrt(x * x + y * y)
+        # cv2 4.x with its default criteria (COUNT + EPS, 10, 1e-8):
+        # theta_d clamped to pi / 2, Newton until |step| < 1e-8, scale 0 at
+        # theta_d <= 1e-8; non-converged or sign-flipped solutions -> (-1e6, -1e6)
+        td = np.minimum(np.sqrt(x * x + y * y), np.pi / 2)
         th = td.copy()
+        conv = td <= 1e-8
         for _ in range(iters or 10):
             t2 = th * th
-            t4, t6, t8 = t2 * t2, t2 * t2 * t2, t2 * t2 * t2 * t2
+            t4 = t2 * t2
+            t6 = t4 * t2
+            t8 = t6 * t2
             k0t2, k1t4, k2t6, k3t8 = k[0] * t2, k[1] * t4, k[2] * t6, k[3] * t8
-            num = th * (1 + k0t2 + k1t4 + k2t6 + k3t8) - td
-            den = 1 + 3 * k0t2 + 5 * k1t4 + 7 * k2t6 + 9 * k3t8
-            th = th - np.where(den != 0, num / np.where(den != 0, den, 1), 0)
-        scale = np.where(td > 1e-8, np.tan(th) / np.where(td > 1e-8, td, 1), 1.0)
+            fix = (th * (1 + k0t2 + k1t4 + k2t6 + k3t8) - td) / (1 + 3 * k0t2 + 5 * k1t4 + 7 * k2t6 + 9 * k3t8)
+            step = ~conv
+            th = np.where(step, th - fix, th)
+            conv = conv | (step & (np.abs(fix) < 1e-8))
+        scale = np.where(td > 1e-8, np.tan(th) / np.where(td > 1e-8, td, 1), 0.0)
+        bad = ~conv | (th < 0)
         x, y = x * scale, y * scale
     else:
         k1, k2, p1, p2 = k[:4]
@@ -297,7 +315,9 @@ def undistort_points(pts, intrinsics, model, coeffs, R=np.eye(3), new_intrinsics
     Y = R[1, 0] * x + R[1, 1] * y + R[1, 2]
     Wz = R[2, 0] * x + R[2, 1] * y + R[2, 2]
     nfx, nfy, ncx, ncy = map(float, new_intrinsics)
-    return np.stack([nfx * X / Wz + ncx, nfy * Y / Wz + ncy], 1)
+    out = np.stack([nfx * X / Wz + ncx, nfy * Y / Wz + ncy], 1)
+    out[bad] = -1000000.0
+    return out
 
 
 def distort_points(pts, intrinsics, model, coeffs):

@@ -107,3 +107,40 @@ def test_rodrigues():
     np.testing.assert_allclose(R @ R.T, np.eye(3), atol=1e-14)
     np.testing.assert_allclose(R @ r, r, atol=1e-14)
     assert np.isclose(np.arccos((np.trace(R) - 1) / 2), np.linalg.norm(r))
+
+
+def test_lk_derivatives_zero_beyond_image():
+    """calcOpticalFlowPyrLK, given raw images, pads the Scharr derivatives
+    with zeros (copyMakeBorder BORDER_CONSTANT, lkpyramid.cpp) while the
+    image pyramid reflects.  Hand-worked window: a horizontal ramp
+    v = 4 x has Ix = 16 (v(x+1) - v(x-1)) = 128 inside the image, 0 in column
+    0 (Scharr's own REFLECT_101 there) and Iy = 0.  The 15 x 15 window at
+    integer corner (-5, 20) with unit weights covers columns -5..9: five
+    zero-padded columns, column 0 and nine columns of 128, so
+    A11 = 15 * 9 * 128^2 (a reflected border would count 14 columns)."""
+    W, H = 64, 48
+    img = np.tile((4 * np.arange(W)).astype(np.uint8), (H, 1))
+    ix, iy = fo.scharr(img)
+    assert (ix[:, 1:W - 1] == 128).all() and (ix[:, 0] == 0).all() and (iy == 0).all()
+    w = (1 << fo.W_BITS, 0, 0, 0)
+    ixv = fo._descale(fo._patch(ix, -5, 20, 15, w, zero_border=True), fo.W_BITS)
+    iyv = fo._descale(fo._patch(iy, -5, 20, 15, w, zero_border=True), fo.W_BITS)
+    assert int(np.sum(ixv.astype(np.int64) ** 2)) == 15 * 9 * 128 ** 2
+    assert int(np.sum(ixv.astype(np.int64) * iyv)) == 0 and int(np.sum(iyv.astype(np.int64) ** 2)) == 0
+    refl = fo._descale(fo._patch(ix, -5, 20, 15, w), fo.W_BITS)   # the image border rule, for contrast
+    assert int(np.sum(refl.astype(np.int64) ** 2)) == 15 * 14 * 128 ** 2
+
+
+def test_fisheye_undistort_rejects_unsolvable_theta():
+    """cv2 4.x fisheye.undistortPoints: Newton stops below 1e-8 and a
+    non-converged or sign-flipped theta comes back as (-1e6, -1e6).  With
+    k = (-1, 0, 0, 0), theta_d = theta (1 - theta^2) peaks at 0.385 (theta =
+    1/sqrt 3): theta_d = 0.6 has no solution, theta_d = 0.2 has one that the
+    forward model maps back."""
+    k = [-1.0, 0.0, 0.0, 0.0]
+    bad = fo.undistort_points([[0.6, 0.0]], (1, 1, 0, 0), "equidistant", k)
+    assert (bad == -1000000.0).all()
+    good = fo.undistort_points([[0.2, 0.1]], (1, 1, 0, 0), "equidistant", k)
+    assert np.isfinite(good).all() and (good > -1000.0).all()
+    back = fo.distort_points(good, (1, 1, 0, 0), "equidistant", k)
+    np.testing.assert_allclose(back, [[0.2, 0.1]], atol=1e-9)

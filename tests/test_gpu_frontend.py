@@ -90,6 +90,18 @@ def test_camera_models_match_oracle(fe, model, coeffs):
     np.testing.assert_allclose(d, fo.distort_points(u, K, name, coeffs), rtol=1e-12, atol=1e-9)
 
 
+def test_fisheye_rejection_matches_oracle(fe):
+    """cv2 4.x fisheye.undistortPoints rejection (non-converged / flipped
+    theta -> (-1e6, -1e6)) and early Newton stop, GPU against the oracle:
+    with k = (-1, 0, 0, 0) theta_d > 0.385 has no solution."""
+    k = [-1.0, 0.0, 0.0, 0.0]
+    px = np.array([[0.6, 0.0], [0.2, 0.1], [0.0, 0.3], [0.5, 0.5], [1e-9, 0.0]])
+    u = fe.undistort(px, np.array([1.0, 1.0, 0.0, 0.0]), 1, k, np.eye(3), [1, 1, 0, 0])
+    o = fo.undistort_points(px, (1, 1, 0, 0), "equidistant", k)
+    np.testing.assert_allclose(u, o, rtol=1e-12, atol=1e-14)
+    assert (u[0] == -1000000.0).all() and (u[3] == -1000000.0).all() and (u[1] > -1).all()
+
+
 StereoMsg = namedtuple("stereo_msg", ["vio_timestamp__", "cam0_image", "cam1_image", "cam0_msg", "cam1_msg"])
 ImgMsg = namedtuple("img_msg", ["vio_timestamp__", "image"])
 ImuMsg = namedtuple("imu_msg", ["vio_timestamp__", "angular_velocity", "linear_acceleration"])

@@ -11,7 +11,7 @@ timeout -k 10 600 python -u bench.py $CPU > $OUT/b.json 2> $OUT/b.err || { tail 
 timeout -k 10 300 python -u tools/profile_frame.py > $OUT/frame.json 2> $OUT/frame.err || { tail -20 $OUT/frame.err; exit 1; }
 if [ "$3" = full ]; then
   timeout -k 10 600 python -u bench.py --N 50 --F 400 --dtype fp64 --no-cpu --no-ate --no-prop > $OUT/b_50x400_fp64.json 2> $OUT/b_50x400_fp64.err || exit 1
-  timeout -k 10 600 python -u bench.py --N 80 --F 1000 --dtype fp64 --no-cpu --no-ate --no-prop > $OUT/b_80x1000_fp64.json 2> $OUT/b_80x1000_fp64.err || exit 1
+  timeout -k 10 600 python -u bench.py --N 80 --F 1000 --dtype fp64 --batch 512 --no-cpu --no-ate --no-prop > $OUT/b_80x1000_fp64.json 2> $OUT/b_80x1000_fp64.err || exit 1
   timeout -k 10 600 python -u tools/bench_sequences.py --seqs 11 > $OUT/seq.json 2> $OUT/seq.err || exit 1
 fi
 cat $OUT/frame.json

@@ -242,6 +242,17 @@ __device__ __forceinline__ int bilinear(const Px* img, int w, int h, int x, int 
     return (int)r0[x0] * w00 + (int)r0[x1] * w01 + (int)r1[x0] * w10 + (int)r1[x1] * w11;
 }
 
+// The derivatives beyond the image are zero: given raw images,
+// calcOpticalFlowPyrLK pads derivI with copyMakeBorder(BORDER_CONSTANT)
+// (lkpyramid.cpp); only the pyramid images use BORDER_REFLECT_101.
+__device__ __forceinline__ int bilinear_zero(const int16_t* img, int w, int h, int x, int y, int w00, int w01,
+                                             int w10, int w11) {
+    auto at = [&](int yy, int xx) -> int {
+        return (xx >= 0 && xx < w && yy >= 0 && yy < h) ? (int)img[(size_t)yy * w + xx] : 0;
+    };
+    return at(y, x) * w00 + at(y, x + 1) * w01 + at(y + 1, x) * w10 + at(y + 1, x + 1) * w11;
+}
+
 __device__ __forceinline__ void lk_weights(float a, float b, int& w00, int& w01, int& w10, int& w11) {
     w00 = (int)rintf((1.f - a) * (1.f - b) * (float)(1 << W_BITS));
     w01 = (int)rintf(a * (1.f - b) * (float)(1 << W_BITS));
@@ -294,8 +305,8 @@ __global__ void __launch_bounds__(64) k_lk(Pyr P, Pyr N, int n, const float* __r
             if (p < npix) {
                 const int yy = p / win, xx = p - yy * win;
                 ival[q] = descale(bilinear(I.img, I.w, I.h, ipx + xx, ipy + yy, w00, w01, w10, w11), W_BITS - 5);
-                ixv[q] = descale(bilinear(I.ix, I.w, I.h, ipx + xx, ipy + yy, w00, w01, w10, w11), W_BITS);
-                iyv[q] = descale(bilinear(I.iy, I.w, I.h, ipx + xx, ipy + yy, w00, w01, w10, w11), W_BITS);
+                ixv[q] = descale(bilinear_zero(I.ix, I.w, I.h, ipx + xx, ipy + yy, w00, w01, w10, w11), W_BITS);
+                iyv[q] = descale(bilinear_zero(I.iy, I.w, I.h, ipx + xx, ipy + yy, w00, w01, w10, w11), W_BITS);
                 s11 += (long long)ixv[q] * ixv[q];
                 s12 += (long long)ixv[q] * iyv[q];
                 s22 += (long long)iyv[q] * iyv[q];
@@ -371,19 +382,34 @@ __global__ void __launch_bounds__(256) k_undistort(CamModel c, int n, const doub
     const int t = blockIdx.x * 256 + threadIdx.x;
     if (t >= n) return;
     double x = (in[2 * t] - c.cx) / c.fx, y = (in[2 * t + 1] - c.cy) / c.fy;
-    if (c.model == MFE_EQUIDISTANT) {   // cv2.fisheye.undistortPoints: Newton on theta
-        const double td = sqrt(x * x + y * y);
-        double th = td;
-        for (int it = 0; it < 10; ++it) {
-            const double t2 = th * th, t4 = t2 * t2, t6 = t2 * t2 * t2, t8 = t2 * t2 * t2 * t2;
-            const double k0t2 = c.k[0] * t2, k1t4 = c.k[1] * t4, k2t6 = c.k[2] * t6, k3t8 = c.k[3] * t8;
-            const double num = th * (1 + k0t2 + k1t4 + k2t6 + k3t8) - td;
-            const double den = 1 + 3 * k0t2 + 5 * k1t4 + 7 * k2t6 + 9 * k3t8;
-            th = th - (den != 0 ? num / den : 0.0);
+    if (c.model == MFE_EQUIDISTANT) {
+        // cv2.fisheye.undistortPoints (4.x) with its default criteria (COUNT +
+        // EPS, 10, 1e-8): theta_d clamped to the model's 180-degree field of
+        // view, Newton on theta until |step| < 1e-8; a solution that did not
+        // converge or flipped sign goes out as (-1e6, -1e6), unrectified
+        const double td = fmin(sqrt(x * x + y * y), M_PI / 2);
+        double th = td, scale = 0.0;
+        bool conv = false;
+        if (td > 1e-8) {
+            for (int it = 0; it < 10; ++it) {
+                const double t2 = th * th, t4 = t2 * t2, t6 = t4 * t2, t8 = t6 * t2;
+                const double k0t2 = c.k[0] * t2, k1t4 = c.k[1] * t4, k2t6 = c.k[2] * t6, k3t8 = c.k[3] * t8;
+                const double fix = (th * (1 + k0t2 + k1t4 + k2t6 + k3t8) - td) /
+                                   (1 + 3 * k0t2 + 5 * k1t4 + 7 * k2t6 + 9 * k3t8);
+                th = th - fix;
+                if (fabs(fix) < 1e-8) { conv = true; break; }
+            }
+            scale = tan(th) / td;
+        } else {
+            conv = true;
         }
-        const double s = td > 1e-8 ? tan(th) / td : 1.0;
-        x = x * s;
-        y = y * s;
+        if (!conv || th < 0) {
+            out[2 * t] = -1000000.0;
+            out[2 * t + 1] = -1000000.0;
+            return;
+        }
+        x = x * scale;
+        y = y * scale;
     } else {   // cv2.undistortPoints: 5 fixed-point iterations
         const double x0 = x, y0 = y, k1 = c.k[0], k2 = c.k[1], p1 = c.k[2], p2 = c.k[3], k3 = 0.0;
         for (int it = 0; it < 5; ++it) {
