@@ -248,7 +248,7 @@ class MSCKF:
         cur = len(self.map_server)
         tracked = 0
         for f in feature_msg.vio_features:
-            z = np.array([f.u0, f.v0, f.u1, f.v1], dtype=float)
+            z = (float(f.u0), float(f.v0), float(f.u1), float(f.v1))   # packed into arrays once per request (_pack)
             feat = self.map_server.get(f.id)
             if feat is None:
                 feat = Feature(f.id)
