@@ -152,13 +152,20 @@ struct msckf_ctx {
     // feature batch
     int nf = 0, maxM = 0, max_nf = 0, max_obs = 0;   // per filter, of the loaded batch
     std::vector<int> h_feat_off;
-    DBuf<int> feat_filter, feat_off, obs_off, obs_cam, row_off, gate_list;
+    // One arena per loaded batch (load_features): the host inputs arrive in ONE
+    // H2D copy, and the per-feature results [valid | p_w | include | gamma]
+    // are one contiguous span for a single D2H copy (read_results).
+    DBuf<unsigned char> batch;
+    int *feat_filter = nullptr, *feat_off = nullptr, *obs_off = nullptr, *obs_cam = nullptr;
+    long long* ysq_off = nullptr;
+    int *gate_list = nullptr, *seg_list = nullptr;
+    unsigned char *obs_z = nullptr, *chi2 = nullptr, *p_w = nullptr, *gamma = nullptr;
+    uint8_t *valid = nullptr, *include = nullptr, *accept = nullptr;
+    size_t out_off = 0;   // arena offset of the result span (valid first)
+    DBuf<int> row_off;
     GateClasses gc;
     SegClasses sc;
-    DBuf<int> seg_list;
-    DBuf<long long> ysq_off;
-    DBuf<unsigned char> obs_z, chi2, p_w, obs_ws, obs_ht, obs_g, tau, ysq, gamma;
-    DBuf<uint8_t> valid, accept, include;
+    DBuf<unsigned char> obs_ws, obs_ht, obs_g, tau, ysq;
     // misc scratch
     DBuf<unsigned char> scratch;
     DBuf<int> iscratch;
@@ -226,24 +233,24 @@ template <typename T>
 FeatBatch<T> feat_batch(msckf_ctx* c) {
     FeatBatch<T> f;
     f.nf = c->nf;
-    f.feat_filter = c->feat_filter.p;
-    f.feat_off = c->feat_off.p;
-    f.obs_off = c->obs_off.p;
-    f.obs_cam = c->obs_cam.p;
-    f.obs_z = reinterpret_cast<const T*>(c->obs_z.p);
-    f.chi2 = reinterpret_cast<const T*>(c->chi2.p);
-    f.ysq_off = c->ysq_off.p;
-    f.p_w = reinterpret_cast<T*>(c->p_w.p);
-    f.valid = c->valid.p;
+    f.feat_filter = c->feat_filter;
+    f.feat_off = c->feat_off;
+    f.obs_off = c->obs_off;
+    f.obs_cam = c->obs_cam;
+    f.obs_z = reinterpret_cast<const T*>(c->obs_z);
+    f.chi2 = reinterpret_cast<const T*>(c->chi2);
+    f.ysq_off = c->ysq_off;
+    f.p_w = reinterpret_cast<T*>(c->p_w);
+    f.valid = c->valid;
     f.obs_ws = reinterpret_cast<T*>(c->obs_ws.p);
     f.obs_ht = reinterpret_cast<T*>(c->obs_ht.p);
     f.obs_g = reinterpret_cast<double*>(c->obs_g.p);
     f.compact = feature_needs_compact(c->maxM) ? 1 : 0;
     f.tau = reinterpret_cast<T*>(c->tau.p);
     f.ysq = reinterpret_cast<T*>(c->ysq.p);
-    f.gamma = reinterpret_cast<T*>(c->gamma.p);
-    f.accept = c->accept.p;
-    f.include = c->include.p;
+    f.gamma = reinterpret_cast<T*>(c->gamma);
+    f.accept = c->accept;
+    f.include = c->include;
     f.row_off = c->row_off.p;
     return f;
 }
@@ -369,15 +376,7 @@ int load_features(msckf_ctx* c, int nf, const int32_t* feat_off, int single_filt
         ysq[f + 1] = ysq[f] + 16LL * M * M;
     }
     const size_t ts = sizeof(T);
-    HIPC(c->feat_filter.ensure(nf + 1));
-    HIPC(c->feat_off.ensure(c->B + 1));
-    HIPC(c->obs_off.ensure(nf + 1));
-    HIPC(c->obs_cam.ensure(nobs + 1));
     HIPC(c->row_off.ensure(nf + 1));
-    HIPC(c->ysq_off.ensure(nf + 1));
-    HIPC(c->obs_z.ensure((nobs * 4 + 4) * ts));
-    HIPC(c->chi2.ensure((nf + 1) * ts));
-    HIPC(c->p_w.ensure((nf * 3 + 3) * ts));
     HIPC(c->obs_ws.ensure(((feature_needs_compact(maxM) ? nobs : 0) * OBS_WS + OBS_WS) * ts));
     HIPC(c->obs_ht.ensure((nobs * OBS_HTS + OBS_HTS) * ts));
     HIPC(c->obs_g.ensure((nobs + 1) * OBG_STRIDE * sizeof(double)));
@@ -388,20 +387,11 @@ int load_features(msckf_ctx* c, int nf, const int32_t* feat_off, int single_filt
         const size_t lds = ((n4 * (n4 + 1) + 1) & ~(size_t)1) * ts + (12 * n4 + 4) * ts + (maxM + 4) * sizeof(int);
         if (lds > 160 * 1024) HIPC(c->ysq.ensure((size_t)(ysq[nf] + 16) * ts));
     }
-    HIPC(c->gamma.ensure((nf + 1) * ts));
-    HIPC(c->valid.ensure(nf + 1));
-    HIPC(c->accept.ensure(nf + 1));
-    HIPC(c->include.ensure(nf + 1));
-    hipStream_t s = c->stream;
-    // every host array goes through the pinned upload ring: nothing below waits on the stream
-    HIPC(upload_raw(c, c->feat_filter.p, h_filt.data(), nf * sizeof(int)));
-    HIPC(upload_raw(c, c->feat_off.p, h_off.data(), (c->B + 1) * sizeof(int)));
-    HIPC(upload_raw(c, c->obs_off.p, obs_off, (nf + 1) * sizeof(int)));
-    if (nobs) HIPC(upload_raw(c, c->obs_cam.p, obs_cam, nobs * sizeof(int)));
-    HIPC(upload_raw(c, c->ysq_off.p, ysq.data(), (nf + 1) * sizeof(long long)));
-    {   // gating size classes, largest first inside the list (long blocks start early)
+    // gating size classes, largest first inside the list (long blocks start early)
+    std::vector<int> gflat;
+    GateClasses gc;
+    {
         std::vector<std::vector<int>> cls(GateClasses::NC);
-        GateClasses gc;
         for (int f = 0; f < nf; ++f) {
             const int M = obs_off[f + 1] - obs_off[f];
             int k = 0;
@@ -409,51 +399,81 @@ int load_features(msckf_ctx* c, int nf, const int32_t* feat_off, int single_filt
             cls[k].push_back(f);
             gc.maxM[k] = std::max(gc.maxM[k], M);
         }
-        std::vector<int> flat;
-        for (int k = GateClasses::NC - 1; k >= 0; --k) {
-            gc.off[k] = 0;
-        }
-        int pos = 0;
         for (int k = 0; k < GateClasses::NC; ++k) {
-            gc.off[k] = pos;
-            flat.insert(flat.end(), cls[k].begin(), cls[k].end());
-            pos += (int)cls[k].size();
+            gc.off[k] = (int)gflat.size();
+            gflat.insert(gflat.end(), cls[k].begin(), cls[k].end());
         }
-        gc.off[GateClasses::NC] = pos;
-        HIPC(c->gate_list.ensure(flat.size() + 1));
-        if (!flat.empty()) HIPC(upload_raw(c, c->gate_list.p, flat.data(), flat.size() * sizeof(int)));
-        gc.list = c->gate_list.p;
-        c->gc = gc;
+        gc.off[GateClasses::NC] = (int)gflat.size();
     }
-    {   // segment classes of the per-feature kernels (M <= S)
-        std::vector<int> flat;
-        SegClasses sc;
-        for (int k = 0; k < SegClasses::NC; ++k) {
-            sc.off[k] = (int)flat.size();
-            for (int f = 0; f < nf; ++f) {
-                const int M = obs_off[f + 1] - obs_off[f];
-                if (M <= SegClasses::S[k] && (k == 0 || M > SegClasses::S[k - 1])) flat.push_back(f);
-            }
+    // segment classes of the per-feature kernels (M <= S)
+    std::vector<int> sflat;
+    SegClasses sc;
+    for (int k = 0; k < SegClasses::NC; ++k) {
+        sc.off[k] = (int)sflat.size();
+        for (int f = 0; f < nf; ++f) {
+            const int M = obs_off[f + 1] - obs_off[f];
+            if (M <= SegClasses::S[k] && (k == 0 || M > SegClasses::S[k - 1])) sflat.push_back(f);
         }
-        sc.off[SegClasses::NC] = (int)flat.size();
-        HIPC(c->seg_list.ensure(flat.size() + 1));
-        if (!flat.empty()) HIPC(upload_raw(c, c->seg_list.p, flat.data(), flat.size() * sizeof(int)));
-        sc.list = c->seg_list.p;
-        c->sc = sc;
     }
-    HIPC(upload<T>(c, c->obs_z.p, obs_z, nobs * 4));
+    sc.off[SegClasses::NC] = (int)sflat.size();
+    // the batch arena: inputs, then the result span [valid | p_w | include | gamma | accept]
+    size_t total = 0;
+    auto seg = [&](size_t bytes) { const size_t o = total; total += (bytes + 255) & ~(size_t)255; return o; };
+    const size_t o_filt = seg(nf * sizeof(int)), o_off = seg((c->B + 1) * sizeof(int));
+    const size_t o_obs = seg((nf + 1) * sizeof(int)), o_cam = seg(nobs * sizeof(int));
+    const size_t o_ysq = seg((nf + 1) * sizeof(long long));
+    const size_t o_gl = seg(gflat.size() * sizeof(int)), o_sl = seg(sflat.size() * sizeof(int));
+    const size_t o_z = seg(nobs * 4 * ts), o_chi = seg(nf * ts);
+    const size_t o_val = seg(nf), o_pw = seg(nf * 3 * ts);
+    const size_t in_bytes = p_w ? total : o_pw;   // p_w uploaded only when given (else triangulation writes it)
+    const size_t o_inc = seg(nf), o_gam = seg(nf * ts), o_acc = seg(nf);
+    HIPC(c->batch.ensure(total + 256));
+    unsigned char* d = c->batch.p;
+    c->feat_filter = reinterpret_cast<int*>(d + o_filt);
+    c->feat_off = reinterpret_cast<int*>(d + o_off);
+    c->obs_off = reinterpret_cast<int*>(d + o_obs);
+    c->obs_cam = reinterpret_cast<int*>(d + o_cam);
+    c->ysq_off = reinterpret_cast<long long*>(d + o_ysq);
+    c->gate_list = reinterpret_cast<int*>(d + o_gl);
+    c->seg_list = reinterpret_cast<int*>(d + o_sl);
+    c->obs_z = d + o_z;
+    c->chi2 = d + o_chi;
+    c->valid = d + o_val;
+    c->p_w = d + o_pw;
+    c->include = d + o_inc;
+    c->gamma = d + o_gam;
+    c->accept = d + o_acc;
+    c->out_off = o_val;
+    gc.list = c->gate_list;
+    sc.list = c->seg_list;
+    c->gc = gc;
+    c->sc = sc;
+    // every host input staged into one pinned buffer, ONE asynchronous copy
+    unsigned char* h = nullptr;
+    HIPC(c->up.get(in_bytes, &h));
+    auto put = [&](size_t o, const void* src, size_t bytes) { if (bytes) std::memcpy(h + o, src, bytes); };
+    auto putT = [&](size_t o, const double* src, size_t n) {
+        T* v = reinterpret_cast<T*>(h + o);
+        for (size_t i = 0; i < n; ++i) v[i] = (T)src[i];
+    };
+    put(o_filt, h_filt.data(), nf * sizeof(int));
+    put(o_off, h_off.data(), (c->B + 1) * sizeof(int));
+    put(o_obs, obs_off, (nf + 1) * sizeof(int));
+    put(o_cam, obs_cam, nobs * sizeof(int));
+    put(o_ysq, ysq.data(), (nf + 1) * sizeof(long long));
+    put(o_gl, gflat.data(), gflat.size() * sizeof(int));
+    put(o_sl, sflat.data(), sflat.size() * sizeof(int));
+    putT(o_z, obs_z, nobs * 4);
     if (chi2) {
-        HIPC(upload<T>(c, c->chi2.p, chi2, nf));
+        putT(o_chi, chi2, nf);
     } else {
-        std::vector<double> big(nf, 1e300);
-        HIPC(upload<T>(c, c->chi2.p, big.data(), nf));
+        T* v = reinterpret_cast<T*>(h + o_chi);
+        for (int i = 0; i < nf; ++i) v[i] = (T)1e300;
     }
-    if (p_w) {
-        HIPC(upload<T>(c, c->p_w.p, p_w, (size_t)nf * 3));
-        HIPC(hipMemsetAsync(c->valid.p, 1, nf, s));
-    } else {
-        HIPC(hipMemsetAsync(c->valid.p, 0, nf, s));
-    }
+    std::memset(h + o_val, p_w ? 1 : 0, nf);
+    if (p_w) putT(o_pw, p_w, (size_t)nf * 3);
+    HIPC(hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, c->stream));
+    HIPC(c->up.mark(c->stream));
     c->nf = nf;
     c->maxM = maxM;
     c->max_nf = c->max_obs = 0;
@@ -520,19 +540,21 @@ int run_update_chain(msckf_ctx* c, int row_cap, bool triangulate) {
 template <typename T>
 int read_results(msckf_ctx* c, uint8_t* accepted_out, double* gamma_out, double* p_w_out, uint8_t* valid_out,
                  int32_t* rows_out) {
-    // every requested array in one pinned D2H batch: a single stream synchronisation
+    // every requested array in one pinned D2H batch, a single stream
+    // synchronisation: the per-feature results are one contiguous span of the
+    // batch arena ([valid | p_w | include | gamma], load_features)
     const int nf = c->nf;
     DownList d;
-    const size_t o_acc = accepted_out && nf ? d.add(c->include.p, nf) : 0;
-    const size_t o_val = valid_out && nf ? d.add(c->valid.p, nf) : 0;
-    const size_t o_gam = gamma_out && nf ? d.add(c->gamma.p, (size_t)nf * sizeof(T)) : 0;
-    const size_t o_pw = p_w_out && nf ? d.add(c->p_w.p, (size_t)nf * 3 * sizeof(T)) : 0;
+    const size_t ts = sizeof(T);
+    const size_t span = nf ? (size_t)(c->gamma - c->valid) + nf * ts : 0;
+    const size_t o_span = span ? d.add(c->valid, span) : 0;
     const size_t o_info = d.add(c->info.p, (size_t)4 * c->B * sizeof(int));
     HIPC(d.run(c));
-    if (accepted_out && nf) std::memcpy(accepted_out, d.at(c, o_acc), nf);
-    if (valid_out && nf) std::memcpy(valid_out, d.at(c, o_val), nf);
-    if (gamma_out && nf) to_double<T>(gamma_out, d.at(c, o_gam), nf);
-    if (p_w_out && nf) to_double<T>(p_w_out, d.at(c, o_pw), (size_t)nf * 3);
+    const unsigned char* base = span ? d.at(c, o_span) : nullptr;
+    if (accepted_out && nf) std::memcpy(accepted_out, base + (c->include - c->valid), nf);
+    if (valid_out && nf) std::memcpy(valid_out, base, nf);
+    if (gamma_out && nf) to_double<T>(gamma_out, base + (c->gamma - c->valid), nf);
+    if (p_w_out && nf) to_double<T>(p_w_out, base + (c->p_w - c->valid), (size_t)nf * 3);
     const int* info = reinterpret_cast<const int*>(d.at(c, o_info));
     int bad = -1;
     for (int b = 0; b < c->B; ++b) {
@@ -819,12 +841,11 @@ int do_triangulate(msckf_ctx* c, int f, int nf, const int32_t* obs_off, const in
     launch_triangulate<T>(c->stream, dev_state<T>(c), make_params<T>(c), feat_batch<T>(c), c->sc);
     c->timer.end(c->stream);
     HIPC(hipGetLastError());
-    DownList d;   // one stream synchronisation
-    const size_t o_pw = d.add(c->p_w.p, (size_t)nf * 3 * sizeof(T));
-    const size_t o_v = d.add(c->valid.p, nf);
+    DownList d;   // one copy of the [valid | p_w] span, one stream synchronisation
+    const size_t o = d.add(c->valid, (size_t)(c->p_w - c->valid) + (size_t)nf * 3 * sizeof(T));
     HIPC(d.run(c));
-    to_double<T>(p_w_out, d.at(c, o_pw), (size_t)nf * 3);
-    std::memcpy(valid_out, d.at(c, o_v), nf);
+    std::memcpy(valid_out, d.at(c, o), nf);
+    to_double<T>(p_w_out, d.at(c, o) + (c->p_w - c->valid), (size_t)nf * 3);
     return 0;
 }
 
@@ -899,17 +920,12 @@ int msckf_destroy(msckf_ctx_t* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->side) (void)hipStreamSynchronize(c->side);
     for (auto* b : {&c->P, &c->imu, &c->cams, &c->P_snap, &c->imu_snap, &c->cams_snap, &c->Hthin, &c->Lc, &c->Vi, &c->Sii, &c->G, &c->Tm, &c->W, &c->Wk,
-                    &c->dx, &c->obs_z, &c->chi2, &c->p_w, &c->obs_ws, &c->obs_ht, &c->obs_g, &c->tau, &c->ysq, &c->gamma, &c->scratch})
+                    &c->dx, &c->batch, &c->obs_ws, &c->obs_ht, &c->obs_g, &c->tau, &c->ysq, &c->scratch})
         b->release();
-    for (auto* b : {&c->ncams, &c->ncams_snap, &c->info, &c->afail, &c->feat_filter, &c->feat_off, &c->obs_off, &c->obs_cam,
-                    &c->row_off, &c->iscratch, &c->gate_list, &c->seg_list})
+    for (auto* b : {&c->ncams, &c->ncams_snap, &c->info, &c->afail, &c->row_off, &c->iscratch})
         b->release();
     c->up.release();
     c->down.release();
-    c->ysq_off.release();
-    c->valid.release();
-    c->accept.release();
-    c->include.release();
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->side) (void)hipStreamDestroy(c->side);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
