@@ -149,7 +149,15 @@ int msckf_batch_triangulate(msckf_ctx_t* ctx);
  * msckf_batch_load copies features for ALL filter slots to HBM once:
  * feat_off[B+1] splits the nf features over slots.  msckf_batch_update then
  * runs triangulation (if flags & MSCKF_TRIANGULATE) + the full update chain on
- * the resident data, asynchronously; msckf_sync waits.  msckf_snapshot /
+ * the resident data, asynchronously; msckf_sync waits.  Triangulation covers
+ * every feature when p_w is NULL, else only the features whose p_w row is not
+ * finite (NaN: "not initialised"): a row given by the host is never
+ * re-triangulated, so one chain serves remove_lost_features' mix of
+ * initialised and new features (msckf.py:640 initialize_position, then
+ * the stacked update).  A feature whose row stays non-finite (no
+ * MSCKF_TRIANGULATE) or whose triangulation fails is not gated (valid = 0).
+ * msckf_batch_results reads everything back with one stream synchronisation,
+ * so a caller may defer it (the drop-in host does, until its next sync point).  msckf_snapshot /
  * msckf_restore copy the whole device state (P, IMU, cams) to / from a
  * shadow buffer on the device (so repeated timed steps do identical work). */
 #define MSCKF_TRIANGULATE 1

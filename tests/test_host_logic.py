@@ -36,3 +36,59 @@ def test_find_redundant_cam_states_matches_reference():
         flt.tracking_rate = tr
         assert flt._find_redundant_cam_states(cams_arr) == [int(c) for c in g[key]]
     assert list(g["rm_3"]) != list(g["rm_9"])
+
+
+class _FakePending:
+    def __init__(self, res):
+        self.res, self.reads = res, 0
+
+    def get(self):
+        self.reads += 1
+        return self.res
+
+
+def test_deferred_update_log_and_fused_triangulation():
+    """The update request goes down without a wait: features to initialise carry
+    NaN positions (triangulated in the same device chain), and the decision
+    log / new positions are applied at the next sync point, in the order the
+    reference's measurement loop logs them (msckf.py:640-682): a failed
+    triangulation is never gated, and logging stops at the row-cap break."""
+    from msckf_amd.msckf import Feature
+    flt = MSCKF.__new__(MSCKF)          # host logic only: no device context
+    flt.cam_ids = list(range(6))
+    flt._n_published = 7
+    flt.gate_log, flt.shape_log, flt._deferred = [], [], []
+    feats = []
+    for k in range(4):
+        f = Feature(k)
+        for c in range(k, k + 3):
+            f.observations[c] = (0.0, 0.0, 0.0, 0.0)
+        f.position = np.array([1.0, 2.0, 3.0 + k])
+        f.is_initialized = k % 2 == 0
+        feats.append(f)
+    to_init = [f for f in feats if not f.is_initialized]           # features 1 and 3
+    cam_lists = [list(f.observations) for f in feats]
+    gen = flt._update(feats, cam_lists, [2] * 4, 15, to_init)
+    req = next(gen)
+    assert req[0] == "update" and req[6] == 15
+    pw = req[4]
+    assert np.isnan(pw[1]).all() and np.isnan(pw[3]).all()
+    np.testing.assert_array_equal(pw[0], [1.0, 2.0, 3.0])
+    # device: feature 1's triangulation fails; 0, 2 and 3 pass the gate (chi2.ppf(0.05, 2) = 0.103)
+    p = np.arange(12.0).reshape(4, 3)
+    res = (np.array([1, 0, 1, 0], bool), np.array([0.01, np.nan, 0.02, 0.03]), p,
+           np.array([1, 0, 1, 1], bool), 18)
+    pend = _FakePending(res)
+    try:
+        gen.send(pend)
+    except StopIteration:
+        pass
+    assert flt.gate_log == [] and pend.reads == 0                   # nothing read yet
+    flt._settle()
+    assert pend.reads == 1
+    # 9 rows each: the cap of 15 breaks after feature 2 (count 18), so 3 is never logged
+    assert flt.gate_log == [(7, 2, 9, 1), (7, 2, 9, 1)]
+    assert flt.shape_log == [(7, 18, 21 + 36)]
+    assert feats[1].is_initialized is False and feats[3].is_initialized is True
+    np.testing.assert_array_equal(feats[3].position, p[3])
+    np.testing.assert_array_equal(feats[0].position, [1.0, 2.0, 3.0])   # given positions untouched

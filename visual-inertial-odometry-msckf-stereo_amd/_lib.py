@@ -164,6 +164,7 @@ class Context:
                                           n_filters, n_cam_capacity, C.byref(h)))
         self.h = h
         self.lock = threading.RLock()
+        self._pending = None   # the loaded batch's results, not read back yet (Pending)
 
     def _check(self, rc):
         if rc < 0:
@@ -226,6 +227,7 @@ class Context:
             self._check(self.lib.msckf_augment(self.h, f))
 
     def triangulate(self, f, obs_off, obs_cam, obs_z):
+        self.settle()
         obs_off, obs_cam = _i32(obs_off), _i32(obs_cam)
         nf = len(obs_off) - 1
         obs_z = _f64(obs_z, (len(obs_cam), 4))
@@ -238,6 +240,7 @@ class Context:
         return p, v.astype(bool)
 
     def update(self, f, obs_off, obs_cam, obs_z, p_w, chi2, row_cap=0):
+        self.settle()
         obs_off, obs_cam = _i32(obs_off), _i32(obs_cam)
         nf = len(obs_off) - 1
         obs_z = _f64(obs_z, (len(obs_cam), 4))
@@ -252,6 +255,33 @@ class Context:
                                               _ptr(chi2, C.c_double), int(row_cap), _ptr(acc, C.c_uint8),
                                               _ptr(gam, C.c_double), C.byref(rows)))
         return acc.astype(bool), gam, rows.value
+
+    def update_async(self, f, obs_off, obs_cam, obs_z, p_w, chi2, row_cap=0):
+        """msckf_update without the wait: the batch of filter ``f`` is loaded
+        and its chain (triangulation of the NaN rows of ``p_w`` fused in front,
+        msckf_hip.h) enqueued; the returned Pending reads (accepted, gamma,
+        p_w, valid, rows) on first use -- or when the next batch is loaded."""
+        nf = len(obs_off) - 1
+        feat_off = np.where(np.arange(self.B + 1) <= f, 0, nf).astype(np.int32)
+        p_w = _f64(p_w, (nf, 3))
+        self.batch_load(feat_off, obs_off, obs_cam, obs_z, p_w, chi2)
+        self.batch_update(row_cap=row_cap, triangulate=not bool(np.isfinite(p_w).all()))
+        return self.pending([(f, 0, nf)])[0]
+
+    def pending(self, ranges):
+        """Deferred results of the loaded batch, one view per (slot, first,
+        end) feature range; the batch is read back once, for all of them."""
+        self.settle()
+        grp = _PendingBatch(self)
+        self._pending = grp
+        return [Pending(grp, s, a, b) for s, a, b in ranges]
+
+    def settle(self):
+        """Reads back the outstanding deferred batch (before its arena is
+        reused by the next load)."""
+        p, self._pending = self._pending, None
+        if p is not None:
+            p.read()
 
     def prune(self, f, slots):
         slots = _i32(slots)
@@ -307,6 +337,7 @@ class Context:
 
     # ---- throughput mode ----
     def batch_load(self, feat_off, obs_off, obs_cam, obs_z, p_w=None, chi2=None):
+        self.settle()
         feat_off, obs_off, obs_cam = _i32(feat_off), _i32(obs_off), _i32(obs_cam)
         obs_z = _f64(obs_z, (len(obs_cam), 4))
         p_w = _f64(p_w) if p_w is not None else None
@@ -359,6 +390,34 @@ class Context:
                                                     buf, 4096))
         names = buf.raw.split(b"\0")[:k]
         return {n.decode(): (float(ms[i]), int(cnt[i])) for i, n in enumerate(names)}
+
+
+class _PendingBatch:
+    """The results of one loaded batch, read back (one synchronisation) on demand."""
+    __slots__ = ("ctx", "res")
+
+    def __init__(self, ctx):
+        self.ctx, self.res = ctx, None
+
+    def read(self):
+        if self.res is None:
+            self.res = self.ctx.batch_results()
+            if self.ctx._pending is self:
+                self.ctx._pending = None
+        return self.res
+
+
+class Pending:
+    """Deferred (accepted, gamma, p_w, valid, rows) of one filter's features."""
+    __slots__ = ("grp", "slot", "a", "b")
+
+    def __init__(self, grp, slot, a, b):
+        self.grp, self.slot, self.a, self.b = grp, slot, a, b
+
+    def get(self):
+        acc, gam, p, v, rows = self.grp.read()
+        a, b = self.a, self.b
+        return acc[a:b].copy(), gam[a:b].copy(), p[a:b].copy(), v[a:b].copy(), int(rows[self.slot])
 
 
 def pack_imu(q, p, v, bg, ba, q_null, p_null, v_null, R_imu_cam0, t_cam0_imu, gravity, alias):

@@ -470,8 +470,17 @@ int load_features(msckf_ctx* c, int nf, const int32_t* feat_off, int single_filt
         T* v = reinterpret_cast<T*>(h + o_chi);
         for (int i = 0; i < nf; ++i) v[i] = (T)1e300;
     }
-    std::memset(h + o_val, p_w ? 1 : 0, nf);
-    if (p_w) putT(o_pw, p_w, (size_t)nf * 3);
+    // valid: 2 = position given by the host (never re-triangulated), 0 = to be
+    // triangulated (p_w NULL, or a NaN row: triangulation fused into the update)
+    if (p_w) {
+        putT(o_pw, p_w, (size_t)nf * 3);
+        for (int f = 0; f < nf; ++f) {
+            const double* r = p_w + 3 * (size_t)f;
+            h[o_val + f] = (std::isfinite(r[0]) && std::isfinite(r[1]) && std::isfinite(r[2])) ? 2 : 0;
+        }
+    } else {
+        std::memset(h + o_val, 0, nf);
+    }
     HIPC(hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, c->stream));
     HIPC(c->up.mark(c->stream));
     c->nf = nf;
@@ -552,7 +561,8 @@ int read_results(msckf_ctx* c, uint8_t* accepted_out, double* gamma_out, double*
     HIPC(d.run(c));
     const unsigned char* base = span ? d.at(c, o_span) : nullptr;
     if (accepted_out && nf) std::memcpy(accepted_out, base + (c->include - c->valid), nf);
-    if (valid_out && nf) std::memcpy(valid_out, base, nf);
+    if (valid_out)
+        for (int f = 0; f < nf; ++f) valid_out[f] = base[f] != 0;
     if (gamma_out && nf) to_double<T>(gamma_out, base + (c->gamma - c->valid), nf);
     if (p_w_out && nf) to_double<T>(p_w_out, base + (c->p_w - c->valid), (size_t)nf * 3);
     const int* info = reinterpret_cast<const int*>(d.at(c, o_info));

@@ -902,7 +902,7 @@ __global__ void __launch_bounds__(256) k_triangulate(DevState<T> st, Params<T> p
         const unsigned long long segmask = S == 64 ? ~0ull : (((1ull << S) - 1) << sl0);
         ok = (bad & segmask) == 0;
     }
-    if ((lane & (S - 1)) == 0 && active) {
+    if ((lane & (S - 1)) == 0 && active && fb.valid[f] != 2) {   // 2: position given by the host
         T pw[3];
         mat3_vec(R0w, pf, pw);
         for (int i = 0; i < 3; ++i) fb.p_w[3 * f + i] = pw[i] + t0w[i];

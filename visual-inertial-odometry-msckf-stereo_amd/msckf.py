@@ -94,6 +94,7 @@ class MSCKF:
         self.gate_log = []                 # (frame, dof, rows, accepted) like tools/gen_golden.py
         self.shape_log = []
         self.reset_log = []                # frames after which online_reset fired
+        self._deferred = []                # (Pending, callback): update results not read back yet
         self._n_published = 0
         T_cam0_imu = np.linalg.inv(config.T_imu_cam0)
         self._T_imu_body = Isometry3d(config.T_imu_body[:3, :3], config.T_imu_body[:3, 3])
@@ -142,7 +143,7 @@ class MSCKF:
         if kind == "triangulate":
             return ctx.triangulate(f, req[1], req[2], req[3])
         if kind == "update":
-            return ctx.update(f, *req[1:])
+            return ctx.update_async(f, *req[1:])
         if kind == "states":
             imu, cams, _ = ctx.get_state(f, want_P=False)
             return imu, cams
@@ -153,6 +154,14 @@ class MSCKF:
         if kind == "set_state":
             return ctx.set_state(f, req[1], req[2], req[3])
         raise ValueError("unknown request %r" % (kind,))
+
+    def _settle(self):
+        """Applies the deferred update results (gate / shape logs, new
+        positions) in request order.  Called at the frame's synchronisation
+        points -- after a ``states`` read, when the device has drained anyway."""
+        d, self._deferred = self._deferred, []
+        for pend, fn in d:
+            fn(*pend.get())
 
     def _drive(self, gen):
         try:
@@ -207,6 +216,7 @@ class MSCKF:
         yield from self._remove_lost_features()
         yield from self._prune_cam_state_buffer()
         imu, _ = yield ("states",)
+        self._settle()
         res = self._publish_from(feature_msg.timestamp, _lib.unpack_imu(imu))
         self._n_published += 1
         yield from self._online_reset()
@@ -283,29 +293,44 @@ class MSCKF:
             f.position = pi
             f.is_initialized = bool(oki)
 
-    def _update(self, feats, cam_lists, dofs, row_cap):
+    def _update(self, feats, cam_lists, dofs, row_cap, to_init=()):
         """Stacked update over ``feats`` in order (device: jacobian, gating,
-        stacking with the row cap, QR, Kalman).  Returns accepted flags."""
+        stacking with the row cap, QR, Kalman), enqueued without a wait.
+        Features in ``to_init`` are triangulated in the same device chain from
+        the observations passed (their p_w rows go down as NaN); those whose
+        triangulation fails take no part, exactly as if the host had dropped
+        them (msckf.py:640-652).  The decision log and the new positions are
+        applied at the next synchronisation point (``_settle``)."""
         if not feats:
-            return np.zeros(0, bool)
+            return
         off, cams, zs = self._pack(feats, cam_lists)
         chi2 = np.array([chi2_threshold(d) for d in dofs])
-        pw = np.array([f.position for f in feats])
-        acc, gam, rows = yield ("update", off, cams, zs, pw, chi2, row_cap)
-        # reproduce the reference's decision log: features after the row-cap
-        # break are never gated (msckf.py:678-679)
-        count = 0
-        D = 21 + 6 * len(self.cam_ids)
-        for i, f in enumerate(feats):
-            k = 4 * len(cam_lists[i]) - 3
-            ok = bool(gam[i] < chi2[i])
-            self.gate_log.append((self._n_published, dofs[i], k, int(ok)))
-            if ok:
-                count += k
-            if row_cap and count > row_cap:
-                break
-        self.shape_log.append((self._n_published, rows, D))
-        return acc
+        init = set(id(f) for f in to_init)
+        pw = np.array([np.full(3, np.nan) if id(f) in init else f.position for f in feats])
+        pend = yield ("update", off, cams, zs, pw, chi2, row_cap)
+        frame, D = self._n_published, 21 + 6 * len(self.cam_ids)
+
+        def apply(acc, gam, p, valid, rows):
+            # reproduce the reference's decision log: features after the row-cap
+            # break are never gated (msckf.py:678-679); failed triangulations
+            # never reach measurement_update
+            for i, f in enumerate(feats):
+                if id(f) in init:
+                    f.is_initialized = bool(valid[i])
+                    f.position = p[i]
+            count = 0
+            for i, f in enumerate(feats):
+                if not valid[i]:
+                    continue
+                k = 4 * len(cam_lists[i]) - 3
+                ok = bool(gam[i] < chi2[i])
+                self.gate_log.append((frame, dofs[i], k, int(ok)))
+                if ok:
+                    count += k
+                if row_cap and count > row_cap:
+                    break
+            self.shape_log.append((frame, rows, D))
+        self._deferred.append((pend, apply))
 
     def _remove_lost_features(self):
         """msckf.py:616-689"""
@@ -321,28 +346,27 @@ class MSCKF:
         # check_motion (always True with the EuRoC config's threshold -1,
         # config.py:10) needs the cam poses; the triangulations are independent
         # of each other, so they are batched into one launch.
+        # The triangulations of the new features ride in the update's device
+        # chain (their observations are the update's own): no wait here.
         thr = self.config.optimization.translation_threshold
+        lost = candidates
         to_init = [f for f in candidates if not f.is_initialized]
         if thr >= 0 and to_init:
             _, cams_arr = yield ("states",)
+            self._settle()
             cams = self._cam_dict(cams_arr)
-            to_init = [f for f in to_init if check_motion(f.observations, cams, thr)]
-        yield from self._triangulate(to_init)
-        processed = []
-        for feat in candidates:
-            if not feat.is_initialized:
-                invalid.append(feat.id)
-            else:
-                processed.append(feat)
+            moved = set(id(f) for f in to_init if check_motion(f.observations, cams, thr))
+            to_init = [f for f in to_init if id(f) in moved]
+            candidates = [f for f in candidates if f.is_initialized or id(f) in moved]
         for fid in invalid:
             del self.map_server[fid]
-        if not processed:
-            return
-        cam_lists = [list(f.observations.keys()) for f in processed]
-        dofs = [len(cl) - 1 for cl in cam_lists]
-        yield from self._update(processed, cam_lists, dofs, self.ROW_CAP)
-        for feat in processed:
+        for feat in lost:   # gone from the map whether or not it initialises
             del self.map_server[feat.id]
+        if not candidates:
+            return
+        cam_lists = [list(f.observations.keys()) for f in candidates]
+        dofs = [len(cl) - 1 for cl in cam_lists]
+        yield from self._update(candidates, cam_lists, dofs, self.ROW_CAP, to_init)
 
     def _find_redundant_cam_states(self, cams_arr):
         """msckf.py:691-727 (host; needs the cam poses)."""
@@ -372,6 +396,7 @@ class MSCKF:
         if len(self.cam_ids) < self.config.max_cam_state_size:
             return
         _, cams_arr = yield ("states",)
+        self._settle()
         rm = self._find_redundant_cam_states(cams_arr)
         thr = self.config.optimization.translation_threshold
         cams = self._cam_dict(cams_arr)
@@ -432,6 +457,7 @@ class MSCKF:
         if thr <= 0:
             return
         d = yield ("cov_diag", 12, 3)
+        self._settle()
         if np.max(np.sqrt(d)) < thr:
             return
         self.cam_ids.clear()

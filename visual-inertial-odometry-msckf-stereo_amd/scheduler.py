@@ -11,7 +11,8 @@ with ONE batched launch:
   propagate   -> msckf_propagate_batch   (IMU propagation fused across filters)
   augment     -> msckf_augment_batch
   triangulate -> msckf_batch_load + msckf_batch_triangulate
-  update      -> msckf_batch_load + msckf_batch_update (per row cap)
+  update      -> msckf_batch_load + msckf_batch_update (per row cap), results
+                 read back at the lanes' next sync point (one read per batch)
   states      -> msckf_get_states_batch  (publish, keyframe selection)
   prune       -> msckf_prune_batch
   cov_diag    -> msckf_get_cov_diag_batch (online reset)
@@ -121,11 +122,11 @@ class MultiMSCKF:
             ctx.batch_triangulate()
             _, _, p, v, _ = ctx.batch_results()
             return self._split(slots, reqs, lambda a, b, _s: (p[a:b].copy(), v[a:b].copy()))
-        if kind == "update":
+        if kind == "update":   # deferred: each lane reads its share at its next sync point
             self._load(slots, reqs, with_pw=True)
-            ctx.batch_update(row_cap=reqs[0][6], triangulate=False)
-            acc, gam, _, _, rows = ctx.batch_results()
-            return self._split(slots, reqs, lambda a, b, s: (acc[a:b].copy(), gam[a:b].copy(), int(rows[s])))
+            tri = any(not np.isfinite(np.asarray(r[4], float)).all() for r in reqs)
+            ctx.batch_update(row_cap=reqs[0][6], triangulate=tri)
+            return ctx.pending([(s,) + self._ranges[s] for s in slots])
         if kind == "states":
             imu, cams = ctx.get_states_batch(slots)
             return [(imu[w], cams[w]) for w in range(len(group))]
