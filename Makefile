@@ -31,3 +31,16 @@ clean:
 	rm -f $(OBJS) $(LIB) $(PROBE)
 
 .PHONY: all clean probe
+
+# experiment builds (tools/exp_bench.py): the same sources with extra -D flags
+#   make exp EXP=kf8 EXPFLAGS=-DMSCKF_IM_KF=8
+EXP      ?= exp
+EXPFLAGS ?=
+EOBJS    := $(patsubst $(SRC)/%.o,tools/exp/obj_$(EXP)/%.o,$(OBJS))
+exp: tools/exp/libmsckf_$(EXP).so
+tools/exp/obj_$(EXP)/%.o: $(SRC)/%.hip $(HDRS)
+	@mkdir -p tools/exp/obj_$(EXP)
+	$(HIPCC) $(HIPFLAGS) $(EXPFLAGS) -c $< -o $@
+tools/exp/libmsckf_$(EXP).so: $(EOBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(EOBJS)
+.PHONY: exp

@@ -2215,6 +2215,8 @@ __global__ void __launch_bounds__(NT) k_info(DevState<T> st, FeatBatch<T> fb, Up
 typedef double v4d __attribute__((ext_vector_type(4)));
 constexpr int IM_NW = 14, IM_PPW = 6, IM_GS = 208;   // waves, tiles per wave, LDS row stride (doubles)
 constexpr int IM_KF = 4;                              // features per staged chunk (3 rows each)
+// (measured in round 3 at 30x200, fp32 context: 8 features per chunk 1.53 ms, 12
+// 1.71 ms, against 1.46 ms for 4 -- profiles/r03/exp_ab_*.json)
 
 __host__ __device__ constexpr size_t info_mfma_lds(int maxnf, int maxobs) {
     return (size_t)3 * IM_KF * IM_GS * sizeof(double) + (3 * IM_KF / 4) * sizeof(unsigned) +
