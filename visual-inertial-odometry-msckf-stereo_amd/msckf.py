@@ -255,18 +255,19 @@ class MSCKF:
     def _add_feature_observations(self, feature_msg):
         """msckf.py:409-427"""
         sid = self.imu_id
-        cur = len(self.map_server)
+        ms = self.map_server
+        get = ms.get
+        cur = len(ms)
         tracked = 0
         for f in feature_msg.vio_features:
             z = (float(f.u0), float(f.v0), float(f.u1), float(f.v1))   # packed into arrays once per request (_pack)
-            feat = self.map_server.get(f.id)
+            feat = get(f.id)
             if feat is None:
                 feat = Feature(f.id)
-                feat.observations[sid] = z
-                self.map_server[f.id] = feat
+                ms[f.id] = feat
             else:
-                feat.observations[sid] = z
                 tracked += 1
+            feat.observations[sid] = z
         self.tracking_rate = tracked / (cur + 1e-5)
 
     # -------------------------------------------------------------- updates --
@@ -275,9 +276,9 @@ class MSCKF:
         off = [0]
         cams, zs = [], []
         for feat, cl in zip(feats, cam_lists):
-            for cid in cl:
-                cams.append(slot[cid])
-                zs.append(feat.observations[cid])
+            obs = feat.observations
+            cams.extend([slot[cid] for cid in cl])
+            zs.extend([obs[cid] for cid in cl])
             off.append(len(cams))
         return (np.array(off, np.int32), np.array(cams, np.int32),
                 np.array(zs, float).reshape(-1, 4))
@@ -400,31 +401,29 @@ class MSCKF:
         rm = self._find_redundant_cam_states(cams_arr)
         thr = self.config.optimization.translation_threshold
         cams = self._cam_dict(cams_arr)
-        to_init = []
+        to_init, involved = [], []   # (feature, its observations of removed cams), map order
         for feat in self.map_server.values():
-            inv = [c for c in rm if c in feat.observations]
-            if len(inv) == 0:
+            obs = feat.observations
+            inv = [c for c in rm if c in obs]
+            if not inv:
                 continue
             if len(inv) == 1:
-                del feat.observations[inv[0]]
+                del obs[inv[0]]
                 continue
+            involved.append((feat, inv))
             if not feat.is_initialized:
                 to_init.append(feat)
         # features that fail check_motion stay uninitialized: their involved
         # observations are dropped below like those of a failed triangulation
         yield from self._triangulate([f for f in to_init if check_motion(f.observations, cams, thr)])
-        for feat in to_init:
-            if not feat.is_initialized:
-                for c in rm:
-                    if c in feat.observations:
-                        del feat.observations[c]
         feats, cam_lists = [], []
-        for feat in self.map_server.values():
-            inv = [c for c in rm if c in feat.observations]
-            if len(inv) == 0:
-                continue
-            feats.append(feat)
-            cam_lists.append(inv)
+        for feat, inv in involved:
+            if feat.is_initialized:
+                feats.append(feat)
+                cam_lists.append(inv)
+            else:
+                for c in inv:
+                    del feat.observations[c]
         if feats:
             yield from self._update(feats, cam_lists, [len(cl) for cl in cam_lists], 0)
         else:   # the reference still calls measurement_update with an empty H

@@ -195,12 +195,14 @@ class Recorder:
         return FeatureStream.from_messages(imu, frames, gt, meta)
 
 
-def replay(flt, stream: FeatureStream, on_result=None) -> Trajectory:
+def replay(flt, stream: FeatureStream, on_result=None, events=None) -> Trajectory:
     """Feeds ``stream`` to a filter exposing the reference API
     (imu_callback / feature_callback -> vio_result | None) and returns the
-    published body trajectory."""
+    published body trajectory.  ``events``: ``stream.events()`` built by the
+    caller beforehand (the messages are the front-end's output, so a timed
+    replay can leave their construction out)."""
     results = []
-    for kind, msg in stream.events():
+    for kind, msg in (stream.events() if events is None else events):
         if kind == 0:
             flt.imu_callback(msg)
         else:
