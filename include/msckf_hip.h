@@ -144,6 +144,15 @@ int msckf_get_states_batch(msckf_ctx_t* ctx, int nfilt, const int32_t* filters, 
                            double* cams_out, int32_t* ncams_out);
 int msckf_get_cov_diag_batch(msckf_ctx_t* ctx, int nfilt, const int32_t* filters, int i0, int n, double* out);
 int msckf_batch_triangulate(msckf_ctx_t* ctx);
+/* A frame's sync point in ONE stream synchronisation (publish, msckf.py:888-908;
+ * find_redundant_cam_states 691-727; online_reset 869-871): the listed filters'
+ * IMU / cam records as msckf_get_states_batch, their covariance diagonal
+ * [i0, i0+n) as msckf_get_cov_diag_batch (n = 0 or cov_out NULL: skipped),
+ * and, if any of the last five pointers is non-NULL, the loaded batch's results
+ * as msckf_batch_results. */
+int msckf_readback(msckf_ctx_t* ctx, int nfilt, const int32_t* filters, double* imu_out, double* cams_out,
+                   int32_t* ncams_out, int i0, int n, double* cov_out, uint8_t* accepted_out,
+                   double* gamma_out, double* p_w_out, uint8_t* valid_out, int32_t* rows_out);
 
 /* ---- throughput mode: B independent filters, one launch chain per step ----
  * msckf_batch_load copies features for ALL filter slots to HBM once:

@@ -68,6 +68,7 @@ _SIGS = {
     "msckf_prune_batch": (C.c_int, [_P, C.c_int, _I, _I, _I]),
     "msckf_get_states_batch": (C.c_int, [_P, C.c_int, _I, _D, _D, _I]),
     "msckf_get_cov_diag_batch": (C.c_int, [_P, C.c_int, _I, C.c_int, C.c_int, _D]),
+    "msckf_readback": (C.c_int, [_P, C.c_int, _I, _D, _D, _I, C.c_int, C.c_int, _D, _U8, _D, _D, _U8, _I]),
     "msckf_batch_triangulate": (C.c_int, [_P]),
     "msckf_batch_load": (C.c_int, [_P, _I, _I, _I, _D, _D, _D]),
     "msckf_batch_update": (C.c_int, [_P, C.c_int, C.c_int]),
@@ -331,6 +332,36 @@ class Context:
             self._check(self.lib.msckf_get_cov_diag_batch(self.h, len(filters), _ptr(filters, C.c_int32), i0, n,
                                                            _ptr(out, C.c_double)))
         return out
+
+    def readback(self, filters, want_cams=True, cov=None):
+        """A frame's sync point with ONE stream synchronisation (msckf_readback):
+        (imu records (n, IMU_LEN), list of cam arrays, covariance diagonals
+        (n, cov[1]) of [cov[0], cov[0] + cov[1]) or None).  An outstanding
+        deferred batch (Pending) is read back in the same copy."""
+        filters = _i32(filters)
+        n = len(filters)
+        imu = np.zeros((n, IMU_LEN))
+        cams = np.zeros((n, self.Nmax, CAM_LEN)) if want_cams else None
+        nc = np.zeros(n, np.int32)
+        i0, ncv = cov if cov else (0, 0)
+        cv = np.zeros((n, ncv)) if ncv else None
+        pend = self._pending if self._pending is not None and self._pending.res is None else None
+        if pend is not None:
+            nf = self._nf
+            acc, gam, p, v = np.zeros(nf, np.uint8), np.zeros(nf), np.zeros((nf, 3)), np.zeros(nf, np.uint8)
+            rows = np.zeros(self.B, np.int32)
+        else:
+            acc = gam = p = v = rows = None
+        with self.lock:
+            self._check(self.lib.msckf_readback(
+                self.h, n, _ptr(filters, C.c_int32), _ptr(imu, C.c_double), _ptr(cams, C.c_double),
+                _ptr(nc, C.c_int32), int(i0), int(ncv), _ptr(cv, C.c_double), _ptr(acc, C.c_uint8),
+                _ptr(gam, C.c_double), _ptr(p, C.c_double), _ptr(v, C.c_uint8), _ptr(rows, C.c_int32)))
+        if pend is not None:
+            pend.res = (acc.astype(bool), gam, p, v.astype(bool), rows)
+            self._pending = None
+        cl = [cams[w, :nc[w]].copy() for w in range(n)] if want_cams else [None] * n
+        return imu, cl, cv
 
     def batch_triangulate(self):
         self._check(self.lib.msckf_batch_triangulate(self.h))

@@ -546,26 +546,32 @@ int run_update_chain(msckf_ctx* c, int row_cap, bool triangulate) {
     return 0;
 }
 
+// The loaded batch's per-feature results: queued on a DownList, unpacked after
+// its (single) synchronisation.  The per-feature results are one contiguous span
+// of the batch arena ([valid | p_w | include | gamma], load_features).
+struct ResultsRead {
+    size_t o_span = 0, o_info = 0, span = 0;
+};
 template <typename T>
-int read_results(msckf_ctx* c, uint8_t* accepted_out, double* gamma_out, double* p_w_out, uint8_t* valid_out,
-                 int32_t* rows_out) {
-    // every requested array in one pinned D2H batch, a single stream
-    // synchronisation: the per-feature results are one contiguous span of the
-    // batch arena ([valid | p_w | include | gamma], load_features)
+ResultsRead add_results(msckf_ctx* c, DownList& d) {
+    ResultsRead r;
     const int nf = c->nf;
-    DownList d;
-    const size_t ts = sizeof(T);
-    const size_t span = nf ? (size_t)(c->gamma - c->valid) + nf * ts : 0;
-    const size_t o_span = span ? d.add(c->valid, span) : 0;
-    const size_t o_info = d.add(c->info.p, (size_t)4 * c->B * sizeof(int));
-    HIPC(d.run(c));
-    const unsigned char* base = span ? d.at(c, o_span) : nullptr;
+    r.span = nf ? (size_t)(c->gamma - c->valid) + nf * sizeof(T) : 0;
+    r.o_span = r.span ? d.add(c->valid, r.span) : 0;
+    r.o_info = d.add(c->info.p, (size_t)4 * c->B * sizeof(int));
+    return r;
+}
+template <typename T>
+int unpack_results(msckf_ctx* c, const DownList& d, const ResultsRead& r, uint8_t* accepted_out, double* gamma_out,
+                   double* p_w_out, uint8_t* valid_out, int32_t* rows_out) {
+    const int nf = c->nf;
+    const unsigned char* base = r.span ? d.at(c, r.o_span) : nullptr;
     if (accepted_out && nf) std::memcpy(accepted_out, base + (c->include - c->valid), nf);
     if (valid_out)
         for (int f = 0; f < nf; ++f) valid_out[f] = base[f] != 0;
     if (gamma_out && nf) to_double<T>(gamma_out, base + (c->gamma - c->valid), nf);
     if (p_w_out && nf) to_double<T>(p_w_out, base + (c->p_w - c->valid), (size_t)nf * 3);
-    const int* info = reinterpret_cast<const int*>(d.at(c, o_info));
+    const int* info = reinterpret_cast<const int*>(d.at(c, r.o_info));
     int bad = -1;
     for (int b = 0; b < c->B; ++b) {
         if (rows_out) rows_out[b] = info[4 * b];
@@ -573,6 +579,15 @@ int read_results(msckf_ctx* c, uint8_t* accepted_out, double* gamma_out, double*
     }
     if (bad >= 0) FAIL(-3, "innovation covariance not positive definite (filter slot %d, %d rows)", bad, info[4 * bad]);
     return 0;
+}
+
+template <typename T>
+int read_results(msckf_ctx* c, uint8_t* accepted_out, double* gamma_out, double* p_w_out, uint8_t* valid_out,
+                 int32_t* rows_out) {
+    DownList d;   // every requested array in one pinned D2H batch, one synchronisation
+    const ResultsRead r = add_results<T>(c, d);
+    HIPC(d.run(c));
+    return unpack_results<T>(c, d, r, accepted_out, gamma_out, p_w_out, valid_out, rows_out);
 }
 
 template <typename T>
@@ -832,6 +847,55 @@ int do_get_states_batch(msckf_ctx* c, int nfilt, const int32_t* filters, double*
     return 0;
 }
 
+// One synchronisation for a frame's sync point: the listed filters' IMU (and
+// cam) records, their covariance diagonal [i0, i0 + n), and -- when any result
+// pointer is given -- the loaded batch's results.
+template <typename T>
+int do_readback(msckf_ctx* c, int nfilt, const int32_t* filters, double* imu_out, double* cams_out,
+                int32_t* ncams_out, int i0, int n, double* cov_out, uint8_t* accepted_out, double* gamma_out,
+                double* p_w_out, uint8_t* valid_out, int32_t* rows_out) {
+    const size_t ts = sizeof(T);
+    const bool cov = nfilt > 0 && n > 0 && cov_out;
+    if (cov) {
+        for (int w = 0; w < nfilt; ++w)
+            if (i0 < 0 || i0 + n > 21 + 6 * c->h_ncams[filters[w]]) FAIL(-1, "diagonal range out of bounds");
+        std::vector<int> fl(filters, filters + nfilt);
+        std::vector<const int*> dl;
+        if (int r = upload_ints(c, {&fl}, dl)) return r;
+        HIPC(c->scratch.ensure((size_t)nfilt * n * ts));
+        launch_cov_diag<T>(c->stream, dev_state<T>(c), nfilt, dl[0], i0, n, reinterpret_cast<T*>(c->scratch.p));
+        HIPC(hipGetLastError());
+    }
+    const bool res = accepted_out || gamma_out || p_w_out || valid_out || rows_out;
+    DownList d;
+    const size_t o_imu = d.add(c->imu.p, (size_t)c->B * IMU_STRIDE * ts);
+    const size_t o_cam = cams_out ? d.add(c->cams.p, (size_t)c->B * c->Nmax * CAM_STRIDE * ts) : 0;
+    const size_t o_cov = cov ? d.add(c->scratch.p, (size_t)nfilt * n * ts) : 0;
+    ResultsRead rr;
+    if (res) rr = add_results<T>(c, d);
+    HIPC(d.run(c));
+    std::vector<double> imu_all((size_t)c->B * IMU_STRIDE);
+    to_double<T>(imu_all.data(), d.at(c, o_imu), imu_all.size());
+    std::vector<double> cams_all;
+    if (cams_out) {
+        cams_all.resize((size_t)c->B * c->Nmax * CAM_STRIDE);
+        to_double<T>(cams_all.data(), d.at(c, o_cam), cams_all.size());
+    }
+    for (int w = 0; w < nfilt; ++w) {
+        const int f = filters[w];
+        if (imu_out)
+            for (int e = 0; e < MSCKF_IMU_LEN; ++e) imu_out[(size_t)w * MSCKF_IMU_LEN + e] = imu_all[(size_t)f * IMU_STRIDE + e];
+        if (cams_out)
+            for (int k = 0; k < c->Nmax; ++k)
+                for (int e = 0; e < MSCKF_CAM_LEN; ++e)
+                    cams_out[((size_t)w * c->Nmax + k) * MSCKF_CAM_LEN + e] =
+                        k < c->h_ncams[f] ? cams_all[((size_t)f * c->Nmax + k) * CAM_STRIDE + e] : 0.0;
+        if (ncams_out) ncams_out[w] = c->h_ncams[f];
+    }
+    if (cov) to_double<T>(cov_out, d.at(c, o_cov), (size_t)nfilt * n);
+    return res ? unpack_results<T>(c, d, rr, accepted_out, gamma_out, p_w_out, valid_out, rows_out) : 0;
+}
+
 template <typename T>
 int run_triangulate_only(msckf_ctx* c) {
     c->timer.begin(c->stream, "triangulate");
@@ -1044,6 +1108,15 @@ int msckf_get_cov_diag_batch(msckf_ctx_t* c, int nfilt, const int32_t* filters, 
     if (int r = check_list(c, nfilt, filters)) return r;
     if (nfilt > 0 && n > 0 && !out) FAIL(-1, "null output");
     return DISPATCH(c, do_cov_diag_batch, c, nfilt, filters, i0, n, out);
+}
+
+int msckf_readback(msckf_ctx_t* c, int nfilt, const int32_t* filters, double* imu_out, double* cams_out,
+                   int32_t* ncams_out, int i0, int n, double* cov_out, uint8_t* accepted_out, double* gamma_out,
+                   double* p_w_out, uint8_t* valid_out, int32_t* rows_out) {
+    if (!c) FAIL(-1, "null context");
+    if (int r = check_list(c, nfilt, filters)) return r;
+    return DISPATCH(c, do_readback, c, nfilt, filters, imu_out, cams_out, ncams_out, i0, n, cov_out, accepted_out,
+                    gamma_out, p_w_out, valid_out, rows_out);
 }
 
 int msckf_batch_triangulate(msckf_ctx_t* c) {

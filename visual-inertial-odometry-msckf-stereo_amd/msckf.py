@@ -144,9 +144,9 @@ class MSCKF:
             return ctx.triangulate(f, req[1], req[2], req[3])
         if kind == "update":
             return ctx.update_async(f, *req[1:])
-        if kind == "states":
-            imu, cams, _ = ctx.get_state(f, want_P=False)
-            return imu, cams
+        if kind == "states":   # ("states"[, i0, n]): one read, with P's diagonal [i0, i0 + n) if asked
+            imu, cams, cv = ctx.readback([f], cov=req[1:3] if len(req) > 1 else None)
+            return (imu[0], cams[0]) if cv is None else (imu[0], cams[0], cv[0])
         if kind == "prune":
             return ctx.prune(f, req[1])
         if kind == "cov_diag":
@@ -215,11 +215,13 @@ class MSCKF:
         self._add_feature_observations(feature_msg)
         yield from self._remove_lost_features()
         yield from self._prune_cam_state_buffer()
-        imu, _ = yield ("states",)
+        # publish and online_reset's position variances in one read
+        thr = self.config.position_std_threshold
+        st = yield (("states", 12, 3) if thr > 0 else ("states",))
         self._settle()
-        res = self._publish_from(feature_msg.timestamp, _lib.unpack_imu(imu))
+        res = self._publish_from(feature_msg.timestamp, _lib.unpack_imu(st[0]))
         self._n_published += 1
-        yield from self._online_reset()
+        yield from self._online_reset(st[2] if thr > 0 else None)
         return res
 
     # ---------------------------------------------------------- propagation --
@@ -450,13 +452,12 @@ class MSCKF:
         t_c_w = s["p"] + T_i_w._vio_R__ @ s["t_cam0_imu"]
         return VioResult(time, T_b_w, body_velocity, Isometry3d(R_w_c.T, t_c_w))
 
-    def _online_reset(self):
-        """msckf.py:859-886"""
+    def _online_reset(self, d):
+        """msckf.py:859-886 (``d``: P's position-block diagonal, read with the
+        publish state)"""
         thr = self.config.position_std_threshold
         if thr <= 0:
             return
-        d = yield ("cov_diag", 12, 3)
-        self._settle()
         if np.max(np.sqrt(d)) < thr:
             return
         self.cam_ids.clear()

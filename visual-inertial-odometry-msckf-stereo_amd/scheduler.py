@@ -13,7 +13,8 @@ with ONE batched launch:
   triangulate -> msckf_batch_load + msckf_batch_triangulate
   update      -> msckf_batch_load + msckf_batch_update (per row cap), results
                  read back at the lanes' next sync point (one read per batch)
-  states      -> msckf_get_states_batch  (publish, keyframe selection)
+  states      -> msckf_readback          (publish + online_reset's diagonal,
+                 keyframe selection; the deferred update results ride along)
   prune       -> msckf_prune_batch
   cov_diag    -> msckf_get_cov_diag_batch (online reset)
 
@@ -88,7 +89,7 @@ class MultiMSCKF:
             if kind == "update":          # the row cap is per call: lost path 1500, prune path none
                 cap = min(pending[i][6] for i in group)
                 group = [i for i in group if pending[i][6] == cap]
-            elif kind == "cov_diag":
+            elif kind in ("cov_diag", "states"):
                 key = pending[group[0]][1:3]
                 group = [i for i in group if pending[i][1:3] == key]
             results = self._serve(kind, group, [pending[i] for i in group])
@@ -127,9 +128,12 @@ class MultiMSCKF:
             tri = any(not np.isfinite(np.asarray(r[4], float)).all() for r in reqs)
             ctx.batch_update(row_cap=reqs[0][6], triangulate=tri)
             return ctx.pending([(s,) + self._ranges[s] for s in slots])
-        if kind == "states":
-            imu, cams = ctx.get_states_batch(slots)
-            return [(imu[w], cams[w]) for w in range(len(group))]
+        if kind == "states":   # one read for the group (with the deferred batch, if any)
+            cov = reqs[0][1:3] if len(reqs[0]) > 1 else None
+            imu, cams, cv = ctx.readback(slots, cov=cov)
+            if cv is None:
+                return [(imu[w], cams[w]) for w in range(len(group))]
+            return [(imu[w], cams[w], cv[w]) for w in range(len(group))]
         if kind == "prune":
             off = np.concatenate([[0], np.cumsum([len(r[1]) for r in reqs])]).astype(np.int32)
             ctx.prune_batch(slots, off, np.concatenate([r[1] for r in reqs]))
