@@ -73,3 +73,41 @@ def test_scheduler_fp32_runs_and_tracks():
         multi.close()
     for st, tr in zip(streams, trajs):
         assert ate(tr, st.gt) < 0.1
+
+
+def test_readback_equals_separate_reads():
+    """msckf_readback (a frame's sync point in one synchronisation) returns what
+    msckf_get_states_batch, msckf_get_cov_diag_batch and msckf_batch_results
+    return separately -- bit for bit -- and settles the outstanding deferred
+    batch, so the Pending needs no read of its own."""
+    g, streams = _streams()
+    ms = MultiMSCKF(3)
+    try:
+        ms.run_streams([s for s in streams])
+        ctx = ms.ctx
+        slots = [0, 2, 1]
+        lane = ms.lanes[0]
+        # one deferred update on lane 0's current features (positions from the map)
+        feats = [f for f in lane.map_server.values() if f.is_initialized and len(f.observations) >= 2][:12]
+        assert feats, "no initialised features left in the map"
+        cl = [list(f.observations) for f in feats]
+        off, cams, zs = lane._pack(feats, cl)
+        pw = np.array([f.position for f in feats])
+        pend = ctx.update_async(0, off, cams, zs, pw, np.full(len(feats), 1e9), 0)
+        imu, cl_rb, cv = ctx.readback(slots, cov=(12, 3))
+        assert ctx._pending is None and pend.grp.res is not None    # settled by the readback
+        acc, gam, p, v, rows = pend.get()
+        imu2, cl2 = ctx.get_states_batch(slots)
+        cv2 = ctx.cov_diag_batch(slots, 12, 3)
+        acc2, gam2, p2, v2, rows2 = ctx.batch_results()
+        np.testing.assert_array_equal(imu, imu2)
+        for a, b in zip(cl_rb, cl2):
+            np.testing.assert_array_equal(a, b)
+        np.testing.assert_array_equal(cv, cv2)
+        np.testing.assert_array_equal(acc, acc2[:len(feats)])
+        np.testing.assert_array_equal(gam, gam2[:len(feats)])
+        np.testing.assert_array_equal(p, p2[:len(feats)])
+        np.testing.assert_array_equal(v, v2[:len(feats)])
+        assert rows == int(rows2[0]) and rows > 0
+    finally:
+        ms.close()
