@@ -872,7 +872,11 @@ void launch_nb(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const
         for (int parts = 2; 4 * per_wave(capb) > (size_t)single_kb * 512 && capb > cmin; ++parts)
             capb = (nbk + parts - 1) / parts > cmin ? (nbk + parts - 1) / parts : cmin;
     const size_t pw = per_wave(capb);
-    const int wpb = 4 * pw <= 160 * 1024 ? 4 : (2 * pw <= 160 * 1024 ? 2 : 1);
+    // one wave per workgroup: a wave's LDS and registers are released as soon as
+    // its feature is done, not when the slowest of four features sharing a
+    // workgroup is (the class's track lengths differ): 2.53 -> 2.49 ms at 30x200,
+    // step 9.19 -> 9.15 ms over four alternated runs (profiles/r03/ab_gate_wpb/)
+    const int wpb = 1;
     if (capb < nbk) launch_cfg<T, NB, true>(s, st, prm, fb, list, cnt, Mmax, capb, wpb, wpb * pw);
     else launch_cfg<T, NB, false>(s, st, prm, fb, list, cnt, Mmax, capb, wpb, wpb * pw);
 }
