@@ -856,13 +856,16 @@ template <typename T, int NB>
 void launch_nb(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const FeatBatch<T>& fb,
                const int* list, int cnt, int Mmax) {
     // Y staging capacity: all M (M + 1) / 2 pair blocks in one pass unless four
-    // waves would then need more than 36 KB; otherwise passes (of
+    // waves would then need more than single_kb KB; otherwise passes (of
     // whole block rows) sized for half of that.  Multi-pass also drops the Y
     // phase's registers (one pair in flight per lane, 82-88 VGPRs), so the
     // classes with nb >= 4 gain a wave per SIMD.  Measured at 30x200 (gate
     // ms): budget 80: 3.46, 60: 3.28, 50: 3.10, 36: 3.05, 20 / 12: 3.06-3.10.
     // (fp64: twice the bytes per element, and at most two waves per SIMD above NB = 3)
-    constexpr int single_kb = 36 * (int)sizeof(T) / 4;
+    // (round 3, one-wave workgroups: fp32 budgets of 40 / 44 / 48 KB per four waves
+    // measured 2.47 ms against 2.52 ms for 36 -- profiles/r03/ab_gate_kb/; fp64
+    // keeps 72, its two waves per SIMD already fill the LDS)
+    constexpr int single_kb = sizeof(T) == 4 ? 44 : 72;
     constexpr int RS = GM<T>::RS;
     const int nbk = Mmax * (Mmax + 1) / 2;
     const int cmin = 6 * Mmax < nbk ? 6 * Mmax : nbk;   // one block row (up to six observation rows) per pass
