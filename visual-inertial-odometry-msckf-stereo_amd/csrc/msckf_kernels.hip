@@ -2203,7 +2203,7 @@ __global__ void __launch_bounds__(NT) k_info(DevState<T> st, FeatBatch<T> fb, Up
 //     A = blockdiag_i(Hx_i^T Hx_i) - Gall^T Gall,   b = sum_i UB_i,
 // and Gall^T Gall is a rank-k update of the lower 16 x 16 tiles of A: the
 // included features are staged KF at a time as dense rows of Gall in LDS,
-// each wave accumulates six of the (at most 78) tiles with
+// each wave accumulates five of the (at most 78) tiles with
 // v_mfma_f64_16x16x4f64 over 4-row k-steps, and a k-step only updates the
 // tiles both of whose column ranges its features touch (per-feature tile
 // masks).  The chunk's G blocks are fetched into registers under the previous
@@ -2213,7 +2213,8 @@ __global__ void __launch_bounds__(NT) k_info(DevState<T> st, FeatBatch<T> fb, Up
 // order.  Output as k_info: [A | b] in H_thin, info[1] = C.
 // ---------------------------------------------------------------------------
 typedef double v4d __attribute__((ext_vector_type(4)));
-constexpr int IM_NW = 14, IM_PPW = 6, IM_GS = 208;   // waves, tiles per wave, LDS row stride (doubles)
+// (round 3: 16 waves x 5 tiles measured 1.43 ms against 1.47 for 14 x 6 -- profiles/r03/ab_info/)
+constexpr int IM_NW = 16, IM_PPW = 5, IM_GS = 208;   // waves, tiles per wave, LDS row stride (doubles)
 constexpr int IM_KF = 4;                              // features per staged chunk (3 rows each)
 // (measured in round 3 at 30x200, fp32 context: 8 features per chunk 1.53 ms, 12
 // 1.71 ms, against 1.46 ms for 4 -- profiles/r03/exp_ab_*.json)
