@@ -15,6 +15,13 @@
  *   - return 0 on success, >0 for a benign no-op, <0 for an error (HIP failure,
  *     bad argument, non-positive-definite innovation covariance).  Nothing
  *     throws across the ABI.  msckf_last_error() gives a message.
+ *   - asynchronous calls (set_state, propagate, augment, prune, their batch
+ *     forms, batch_load / batch_update / batch_triangulate, restore) enqueue
+ *     work on the context's stream and return without waiting.  A kernel fault
+ *     or copy error of such a call is reported by the NEXT synchronising call
+ *     (get_state, readback, batch_results, triangulate, update, sync, ...),
+ *     as that call's -2; its msckf_last_error() message names the last
+ *     asynchronous call enqueued, so the failure is attributed correctly.
  *   - a context holds B independent filters ("filter slots") of one scalar type
  *     (4 = fp32, 8 = fp64) with a fixed cam-state capacity; a context is
  *     single-threaded (the Python wrapper serialises calls with a lock).

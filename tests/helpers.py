@@ -101,3 +101,39 @@ def sequence_config(g):
     if "position_std_threshold" in g:
         cfg.position_std_threshold = float(g["position_std_threshold"])
     return cfg
+
+
+def oracle_state_from_device(imu_rec, cams, P, sigma2=0.035 ** 2):
+    """Oracle FilterState of one device filter slot (ctx.get_state output):
+    cam states keyed by slot, the EuRoC extrinsics and noise of FilterConfig."""
+    from msckf_amd import FilterConfig, _lib
+    imu = _lib.unpack_imu(imu_rec)
+    T = np.asarray(FilterConfig().T_cn_cnm1)
+    Qc = np.diag([0.005 ** 2] * 3 + [0.001 ** 2] * 3 + [0.05 ** 2] * 3 + [0.01 ** 2] * 3)
+    oi = O.ImuState(q=imu["q"], p=imu["p"], v=imu["v"], bg=imu["bg"], ba=imu["ba"], q_null=imu["q_null"],
+                    R_imu_cam0=imu["R_imu_cam0"], t_cam0_imu=imu["t_cam0_imu"])
+    oc = OrderedDict((i, O.CamState(i, float(i), cams[i, 0:4].copy(), cams[i, 4:7].copy(), cams[i, 7:11].copy()))
+                     for i in range(len(cams)))
+    return O.FilterState(oi, oc, P.copy(), imu["gravity"].copy(), T[:3, :3], T[:3, 3], Qc, sigma2)
+
+
+def gamma_basis_spread(st, p_w, obs, n_bases=8, seed=0):
+    """The reference's gamma (msckf.py:606-614: SVD left-nullspace basis,
+    msckf.py:535-539, LU solve) of one feature, and its largest relative change
+    when the nullspace basis is replaced by other orthonormal bases of the same
+    space (H -> Q H, r -> Q r, Q random orthogonal).  In exact arithmetic gamma
+    does not depend on the basis (quirk Q4); a spread far above rounding marks a
+    numerically degenerate feature whose reference decision is rounding noise.
+    A basis in which S is singular counts as an unbounded change."""
+    H, r = O.feature_jacobian(st, p_w, obs)
+    g0 = O.gating_gamma(st, H, r)
+    rng = np.random.default_rng(seed)
+    spread = 0.0
+    for _ in range(n_bases):
+        Q, _ = np.linalg.qr(rng.standard_normal((len(r), len(r))))
+        try:
+            g = O.gating_gamma(st, Q @ H, Q @ r)
+        except np.linalg.LinAlgError:
+            return g0, np.inf
+        spread = max(spread, abs(g / g0 - 1) if g0 != 0 else np.inf)
+    return g0, spread

@@ -209,6 +209,33 @@ def test_load_rejects_duplicate_cam_slots():
         ctx.update(0, [0, 3], [1, 2, 1], d["obs_z"][:3], d["tri_p"][:1], np.array([10.0]))
 
 
+@pytest.mark.parametrize("corrupt", ["indefinite", "nan"])
+def test_update_rejects_corrupted_covariance(corrupt):
+    """Stage A floors only rounding-level pivots (down to -1e-6 x the largest
+    cam variance, msckf_rchol.h pivot_floored): a P_cc set through set_state
+    with a clearly negative eigenvalue, or a NaN, still fails the update with
+    -3 instead of being silently regularised."""
+    d = golden("update_n10_f40")
+    P = d["P"].copy()
+    if corrupt == "indefinite":
+        v = np.zeros(P.shape[0])
+        v[27:33] = 1.0 / np.sqrt(6.0)
+        P -= 10.0 * np.abs(np.diag(P)[21:]).max() * np.outer(v, v)
+    else:
+        P[30, 30] = np.nan
+    assert corrupt == "nan" or np.linalg.eigvalsh(P[21:, 21:]).min() < -1e-3 * np.abs(np.diag(P)[21:]).max()
+    ctx = Context(FilterConfig(), n_filters=1, n_cam_capacity=int(d["N"]) + 2)
+    ctx.set_state(0, imu_record(d), pack_cams(d["cam_q"], d["cam_p"], d["cam_q_null"]), P)
+    sel = [f for f in range(int(d["F"])) if d["tri_ok"][f]]
+    obs = [feature_obs(d, f) for f in sel]
+    off = np.concatenate([[0], np.cumsum([len(o) for o in obs])])
+    cams = [c for o in obs for c, _ in o]
+    zs = [z for o in obs for _, z in o]
+    with pytest.raises(RuntimeError, match="rc=-3"):
+        ctx.update(0, off, cams, zs, d["tri_p"][sel], np.full(len(sel), 1e30))
+    ctx.close()
+
+
 def test_update_empty_is_noop():
     d = golden("update_n10_f40")
     ctx = make_ctx(d)
@@ -366,8 +393,8 @@ def test_gate_fp32_gamma_vs_oracle(N, F, B, cap):
     assert np.quantile(e, 0.99) < 1e-3, np.quantile(e, 0.99)
 
 
-@pytest.mark.parametrize("N,F,B", [(40, 150, 2), (82, 50, 1)])
-def test_gate_fp64_gamma_vs_oracle(N, F, B):
+@pytest.mark.parametrize("N,F,B,nmin", [(40, 150, 2, 200), (82, 50, 1, 40)])
+def test_gate_fp64_gamma_vs_oracle(N, F, B, nmin):
     """fp64 gating against the oracle's gamma (msckf.py:606-614), relative
     1e-9: the one-wave fp64 MFMA kernel (v_mfma_f64_16x16x4_f64, its own
     accumulator row layout) for every class up to 6 blocks (M <= 30, single- and
@@ -383,16 +410,17 @@ def test_gate_fp64_gamma_vs_oracle(N, F, B):
         np.testing.assert_allclose(gam[sl][ok], gam_o[ok], rtol=1e-9)
         np.testing.assert_array_equal(acc[sl], acc_o)
         n += int(ok.sum())
-    assert n > 40
+    assert n > nmin, n
 
 
 def test_gate_fp32_scrambled_observation_order():
     """gamma is invariant under a permutation of a feature's observations (an
     orthogonal row map of the stacked system, quirk Q4), so scrambling them
-    must reproduce the oracle's gamma.  With slots out of order, the
-    filter-resident fp32 gating (k_gate_res) reads P_cc blocks (b, a) of its
-    lower-triangle LDS image transposed: this exercises that path (the sorted
-    case is every other fp32 test).  Tolerance as the fp32 gamma test."""
+    must reproduce the oracle's gamma.  With slots out of order, the one-wave
+    MFMA gating (k_gate_mfma) stages pair blocks Ht_a P_ab Ht_b^T with a > b
+    as well as a < b, i.e. it reads P_cc blocks on both sides of the diagonal
+    (the sorted case is every other fp32 test).  Tolerance as the fp32 gamma
+    test: median <= 1e-4, 99th percentile <= 1e-3."""
     rng = np.random.default_rng(11)
     problems = [synth.make_update_problem(30, 200, seed=500 + b) for b in range(2)]
     ref = [oracle_update(problem_to_dict(p)) for p in problems]
@@ -413,7 +441,7 @@ def test_gate_fp32_scrambled_observation_order():
     e = np.concatenate(errs)
     assert e.size > 300
     assert np.median(e) < 1e-4, np.median(e)
-    assert np.quantile(e, 0.99) < 1e-2, np.quantile(e, 0.99)
+    assert np.quantile(e, 0.99) < 1e-3, np.quantile(e, 0.99)
 
 
 def test_restore_repeats_identically():
@@ -535,22 +563,87 @@ def test_sequence_s4_degenerate():
     """Golden sequence s4 (180 frames, seed 307): landmarks triangulated
     millimetres from the camera make the reference's S singular in fp64
     (test_gate_degenerate_exact), and its non-Joseph covariance update leaves
-    P_cc indefinite at rounding level from frame 2 on.  The drop-in filter
-    must run it to the end -- stage A's pivot floor (msckf_kalman.hip,
-    pcc_pivot_floor) instead of a non-PD abort -- and agree with the
-    reference on every decision before the first degenerate one (frame 5),
-    with a trajectory as close to the ground truth as the reference's own."""
+    P_cc indefinite at rounding level from frame 2 on.  What the HIP path is
+    held to:
+
+    1. it runs the whole stream -- stage A's pivot floor (msckf_rchol.h,
+       pivot_floored) instead of a non-PD abort;
+    2. every frame before the first gating decision that differs from the
+       reference's is within the north-star tolerance: state vector and
+       |P|_F <= 1e-6 relative, decisions and online resets identical;
+    3. the first differing decision is a gamma flip (same frame, dof and rows)
+       of a numerically degenerate feature: at the device's pre-update state,
+       the reference's own gamma formula (SVD nullspace basis, LU solve,
+       msckf.py:535-539, 606-614) changes by more than 50 % under another
+       orthonormal basis of the same nullspace (exactly basis-invariant in
+       exact arithmetic, quirk Q4) -- the reference decision is rounding noise;
+    4. after it, the trajectory stays as close to the ground truth as the
+       reference's own (ATE <= 2 x the reference's + 1 cm)."""
     from msckf_amd.trajectory import Trajectory, ate
     from msckf_amd.replay import FeatureStream
+    from helpers import oracle_state_from_device, gamma_basis_spread
     g = golden("sequence_s4")
     seq = synth.make_sequence(int(g["n_frames"]), int(g["seed"]))
     flt = msckf_amd.MSCKF(sequence_config(g))
+    trace = []
+    orig_update, orig_serve = flt._update, flt._serve
+
+    def traced_update(feats, cam_lists, dofs, row_cap, to_init=()):
+        trace.append(dict(frame=flt._n_published, ids=[f.id for f in feats]))
+        return (yield from orig_update(feats, cam_lists, dofs, row_cap, to_init))
+
+    class _Traced:
+        def __init__(self, pend, entry):
+            self.pend, self.entry = pend, entry
+
+        def get(self):
+            res = self.pend.get()
+            self.entry["res"] = res
+            return res
+
+    def traced_serve(req):
+        if req[0] != "update":
+            return orig_serve(req)
+        e = trace[-1]
+        e["state"] = flt.ctx.get_state(flt.slot)
+        e["req"] = req[1:]
+        return _Traced(orig_serve(req), e)
+
+    flt._update, flt._serve = traced_update, traced_serve
     rec = _run_sequence(flt, seq)
     flt.close()
     assert rec.shape == g["rec"].shape
-    gl, ref_gl = np.array(flt.gate_log), g["gates"]
-    early = ref_gl[:, 0] < 5
-    np.testing.assert_array_equal(gl[:early.sum()], ref_gl[early])
+    gl, ref_gl = [tuple(x) for x in flt.gate_log], [tuple(x) for x in g["gates"]]
+    n = min(len(gl), len(ref_gl))
+    i = next((k for k in range(n) if gl[k] != ref_gl[k]), n)
+    assert i < n, "no decision differs: s4 should then pass test_sequence_golden's bounds"
+    flip_frame = min(gl[i][0], ref_gl[i][0])
+    ref = g["rec"]
+    worst = 0.0
+    for k in range(flip_frame):
+        x, xr = rec[k, 1:29], ref[k, 1:29]
+        dev = np.linalg.norm(x - xr) / np.linalg.norm(xr)
+        worst = max(worst, dev)
+        assert dev <= 1e-6, (k, dev)
+        assert abs(rec[k, 29] - ref[k, 29]) <= 1e-6 * ref[k, 29], k
+    np.testing.assert_array_equal(rec[:flip_frame, 31:34], ref[:flip_frame, 31:34])
+    assert [r for r in flt.reset_log if r < flip_frame] == [r for r in g["resets"] if r < flip_frame]
+    # the first differing decision: a gamma flip of one feature
+    assert gl[i][:3] == ref_gl[i][:3], ("triangulation / stacking diverged first", gl[i], ref_gl[i])
+    fid, gam_dev = flt.gamma_log[i]
+    e = next(e for e in trace if e["frame"] == gl[i][0] and fid in e["ids"])
+    j = e["ids"].index(fid)
+    off, cams, zs = e["req"][0], e["req"][1], e["req"][2]
+    obs = [(int(cams[o]), zs[o]) for o in range(off[j], off[j + 1])]
+    p_w = e["res"][2][j]
+    chi2 = e["req"][4][j]
+    st = oracle_state_from_device(*e["state"])
+    g_ref, spread = gamma_basis_spread(st, p_w, obs)
+    print("s4: frames 0..%d within %.2e of the reference; first flip at frame %d, feature %d (M = %d): "
+          "device gamma %.6g, reference-formula gamma %.6g (basis spread %.3g), chi2 %.6g, reference %s"
+          % (flip_frame - 1, worst, flip_frame, fid, len(obs), gam_dev, g_ref, spread, chi2,
+             "accepts" if ref_gl[i][3] else "rejects"))
+    assert spread > 0.5, spread
     gt = FeatureStream.from_synthetic(seq).gt
     ate_gpu = ate(Trajectory(rec[:, 0], rec[:, 5:8]), gt)
     ate_ref = ate(Trajectory(g["rec"][:, 0], g["rec"][:, 5:8]), gt)

@@ -57,7 +57,7 @@ def test_deferred_update_log_and_fused_triangulation():
     flt = MSCKF.__new__(MSCKF)          # host logic only: no device context
     flt.cam_ids = list(range(6))
     flt._n_published = 7
-    flt.gate_log, flt.shape_log, flt._deferred = [], [], []
+    flt.gate_log, flt.gamma_log, flt.shape_log, flt._deferred = [], [], [], []
     feats = []
     for k in range(4):
         f = Feature(k)
@@ -92,3 +92,17 @@ def test_deferred_update_log_and_fused_triangulation():
     assert feats[1].is_initialized is False and feats[3].is_initialized is True
     np.testing.assert_array_equal(feats[3].position, p[3])
     np.testing.assert_array_equal(feats[0].position, [1.0, 2.0, 3.0])   # given positions untouched
+    assert [fid for fid, _ in flt.gamma_log] == [0, 2]
+    # every candidate needs triangulation and every one fails: the reference's
+    # processed list is empty, so it returns before measurement_update and
+    # logs neither a decision nor a stacked shape (msckf.py:652-654)
+    flt.gate_log, flt.gamma_log, flt.shape_log = [], [], []
+    gen = flt._update(feats[1:4:2], cam_lists[1:4:2], [2] * 2, 15, feats[1:4:2])
+    next(gen)
+    pend = _FakePending((np.zeros(2, bool), np.full(2, np.nan), np.zeros((2, 3)), np.zeros(2, bool), 0))
+    try:
+        gen.send(pend)
+    except StopIteration:
+        pass
+    flt._settle()
+    assert flt.gate_log == [] and flt.shape_log == [] and flt.gamma_log == []

@@ -34,6 +34,18 @@ static thread_local std::string g_err;
                                    __FILE__, __LINE__);                                   \
     } while (0)
 
+// A synchronising call reports the failure of any asynchronous operation
+// enqueued before it (kernel faults, copy errors): the message names the last
+// asynchronous entry point called on the context, which is where to look first.
+#define HIPSYNC(c, x)                                                                           \
+    do {                                                                                        \
+        hipError_t _e = (x);                                                                    \
+        if (_e != hipSuccess)                                                                   \
+            FAIL(-2, "%s failed: %s (%s:%d; errors of asynchronous calls surface here -- last " \
+                     "asynchronous call: %s)", #x, hipGetErrorString(_e), __FILE__, __LINE__,   \
+                 (c)->last_async);                                                              \
+    } while (0)
+
 namespace {
 
 template <typename T>
@@ -170,6 +182,7 @@ struct msckf_ctx {
     DBuf<unsigned char> scratch;
     DBuf<int> iscratch;
     KernelTimer timer;
+    const char* last_async = "none";   // last asynchronous entry point (HIPSYNC's message)
     bool has_snapshot = false;
     PinnedRing up;      // upload staging
     PinnedBuf down;     // download staging
@@ -586,7 +599,7 @@ int read_results(msckf_ctx* c, uint8_t* accepted_out, double* gamma_out, double*
                  int32_t* rows_out) {
     DownList d;   // every requested array in one pinned D2H batch, one synchronisation
     const ResultsRead r = add_results<T>(c, d);
-    HIPC(d.run(c));
+    HIPSYNC(c, d.run(c));
     return unpack_results<T>(c, d, r, accepted_out, gamma_out, p_w_out, valid_out, rows_out);
 }
 
@@ -669,7 +682,7 @@ int do_get_state(msckf_ctx* c, int f, double* imu, double* cams, double* P, int*
     const size_t o_imu = imu ? d.add(c->imu.p + (size_t)f * IMU_STRIDE * ts, IMU_STRIDE * ts) : 0;
     const size_t o_cam = cams && nc ? d.add(c->cams.p + (size_t)f * c->Nmax * CAM_STRIDE * ts, (size_t)nc * CAM_STRIDE * ts) : 0;
     const size_t o_P = P ? d.add(c->P.p + (size_t)f * c->Dmax * c->Dmax * ts, (size_t)c->Dmax * c->Dmax * ts) : 0;
-    HIPC(d.run(c));
+    HIPSYNC(c, d.run(c));
     if (imu) {
         std::vector<double> rec(IMU_STRIDE);
         to_double<T>(rec.data(), d.at(c, o_imu), IMU_STRIDE);
@@ -825,7 +838,7 @@ int do_get_states_batch(msckf_ctx* c, int nfilt, const int32_t* filters, double*
     DownList d;   // one stream synchronisation
     const size_t o_imu = d.add(c->imu.p, (size_t)c->B * IMU_STRIDE * ts);
     const size_t o_cam = cams_out ? d.add(c->cams.p, (size_t)c->B * c->Nmax * CAM_STRIDE * ts) : 0;
-    HIPC(d.run(c));
+    HIPSYNC(c, d.run(c));
     std::vector<double> imu_all((size_t)c->B * IMU_STRIDE);
     to_double<T>(imu_all.data(), d.at(c, o_imu), imu_all.size());
     std::vector<double> cams_all;
@@ -873,7 +886,7 @@ int do_readback(msckf_ctx* c, int nfilt, const int32_t* filters, double* imu_out
     const size_t o_cov = cov ? d.add(c->scratch.p, (size_t)nfilt * n * ts) : 0;
     ResultsRead rr;
     if (res) rr = add_results<T>(c, d);
-    HIPC(d.run(c));
+    HIPSYNC(c, d.run(c));
     std::vector<double> imu_all((size_t)c->B * IMU_STRIDE);
     to_double<T>(imu_all.data(), d.at(c, o_imu), imu_all.size());
     std::vector<double> cams_all;
@@ -917,7 +930,7 @@ int do_triangulate(msckf_ctx* c, int f, int nf, const int32_t* obs_off, const in
     HIPC(hipGetLastError());
     DownList d;   // one copy of the [valid | p_w] span, one stream synchronisation
     const size_t o = d.add(c->valid, (size_t)(c->p_w - c->valid) + (size_t)nf * 3 * sizeof(T));
-    HIPC(d.run(c));
+    HIPSYNC(c, d.run(c));
     std::memcpy(valid_out, d.at(c, o), nf);
     to_double<T>(p_w_out, d.at(c, o) + (c->p_w - c->valid), (size_t)nf * 3);
     return 0;
@@ -1021,6 +1034,7 @@ int msckf_device_info(const msckf_ctx_t* c, int* device_out, char* pci_bus_id, i
 }
 
 int msckf_set_state(msckf_ctx_t* c, int filter, const double* imu, int n_cams, const double* cams, const double* P) {
+    if (c) c->last_async = "msckf_set_state";
     if (int r = check_ctx(c, filter)) return r;
     return DISPATCH(c, do_set_state, c, filter, imu, n_cams, cams, P);
 }
@@ -1037,6 +1051,7 @@ int msckf_get_cov_diag(msckf_ctx_t* c, int filter, int i0, int n, double* out) {
 }
 
 int msckf_propagate(msckf_ctx_t* c, int filter, int n, const double* dt, const double* gyro, const double* acc) {
+    if (c) c->last_async = "msckf_propagate";
     if (int r = check_ctx(c, filter)) return r;
     if (n > 0 && (!dt || !gyro || !acc)) FAIL(-1, "null sample array");
     const int32_t off[2] = {0, n > 0 ? n : 0};
@@ -1045,6 +1060,7 @@ int msckf_propagate(msckf_ctx_t* c, int filter, int n, const double* dt, const d
 
 int msckf_propagate_batch(msckf_ctx_t* c, int nfilt, const int32_t* filters, const int32_t* sample_off,
                           const double* dt, const double* gyro, const double* acc) {
+    if (c) c->last_async = "msckf_propagate_batch";
     if (!c) FAIL(-1, "null context");
     if (int r = check_list(c, nfilt, filters)) return r;
     if (nfilt > 0 && !sample_off) FAIL(-1, "null sample offsets");
@@ -1053,11 +1069,13 @@ int msckf_propagate_batch(msckf_ctx_t* c, int nfilt, const int32_t* filters, con
 }
 
 int msckf_augment(msckf_ctx_t* c, int filter) {
+    if (c) c->last_async = "msckf_augment";
     if (int r = check_ctx(c, filter)) return r;
     return DISPATCH(c, do_augment_batch, c, 1, &filter);
 }
 
 int msckf_augment_batch(msckf_ctx_t* c, int nfilt, const int32_t* filters) {
+    if (c) c->last_async = "msckf_augment_batch";
     if (!c) FAIL(-1, "null context");
     if (int r = check_list(c, nfilt, filters)) return r;
     return DISPATCH(c, do_augment_batch, c, nfilt, filters);
@@ -1073,6 +1091,7 @@ int msckf_triangulate(msckf_ctx_t* c, int filter, int nf, const int32_t* obs_off
 int msckf_update(msckf_ctx_t* c, int filter, int nf, const int32_t* obs_off, const int32_t* obs_cam,
                  const double* obs_z, const double* p_w, const double* chi2, int row_cap, uint8_t* accepted_out,
                  double* gamma_out, int32_t* rows_out) {
+    if (c) c->last_async = "msckf_update";
     if (int r = check_ctx(c, filter)) return r;
     if (nf > 0 && (!obs_off || !obs_cam || !obs_z || !p_w || !chi2)) FAIL(-1, "null argument");
     return DISPATCH(c, do_update, c, filter, nf, obs_off, obs_cam, obs_z, p_w, chi2, row_cap, accepted_out,
@@ -1080,6 +1099,7 @@ int msckf_update(msckf_ctx_t* c, int filter, int nf, const int32_t* obs_off, con
 }
 
 int msckf_prune(msckf_ctx_t* c, int filter, int n, const int32_t* cam_slots) {
+    if (c) c->last_async = "msckf_prune";
     if (int r = check_ctx(c, filter)) return r;
     if (n <= 0) return 1;
     if (!cam_slots) FAIL(-1, "null slot list");
@@ -1089,6 +1109,7 @@ int msckf_prune(msckf_ctx_t* c, int filter, int n, const int32_t* cam_slots) {
 
 int msckf_prune_batch(msckf_ctx_t* c, int nfilt, const int32_t* filters, const int32_t* slot_off,
                       const int32_t* cam_slots) {
+    if (c) c->last_async = "msckf_prune_batch";
     if (!c) FAIL(-1, "null context");
     if (int r = check_list(c, nfilt, filters)) return r;
     if (nfilt > 0 && !slot_off) FAIL(-1, "null slot offsets");
@@ -1120,17 +1141,20 @@ int msckf_readback(msckf_ctx_t* c, int nfilt, const int32_t* filters, double* im
 }
 
 int msckf_batch_triangulate(msckf_ctx_t* c) {
+    if (c) c->last_async = "msckf_batch_triangulate";
     if (!c) FAIL(-1, "null context");
     return DISPATCH(c, run_triangulate_only, c);
 }
 
 int msckf_batch_load(msckf_ctx_t* c, const int32_t* feat_off, const int32_t* obs_off, const int32_t* obs_cam,
                      const double* obs_z, const double* p_w, const double* chi2) {
+    if (c) c->last_async = "msckf_batch_load";
     if (!c || !feat_off || !obs_off || !obs_cam || !obs_z) FAIL(-1, "null argument");
     return DISPATCH(c, load_features, c, 0, feat_off, 0, obs_off, obs_cam, obs_z, p_w, chi2);
 }
 
 int msckf_batch_update(msckf_ctx_t* c, int row_cap, int flags) {
+    if (c) c->last_async = "msckf_batch_update";
     if (!c) FAIL(-1, "null context");
     return DISPATCH(c, run_update_chain, c, row_cap, (flags & MSCKF_TRIANGULATE) != 0);
 }
@@ -1151,12 +1175,13 @@ int msckf_snapshot(msckf_ctx_t* c) {
     HIPC(hipMemcpyAsync(c->imu_snap.p, c->imu.p, c->imu.cap, hipMemcpyDeviceToDevice, c->stream));
     HIPC(hipMemcpyAsync(c->cams_snap.p, c->cams.p, c->cams.cap, hipMemcpyDeviceToDevice, c->stream));
     HIPC(hipMemcpyAsync(c->ncams_snap.p, c->ncams.p, c->B * sizeof(int), hipMemcpyDeviceToDevice, c->stream));
-    HIPC(hipStreamSynchronize(c->stream));
+    HIPSYNC(c, hipStreamSynchronize(c->stream));
     c->has_snapshot = true;
     return 0;
 }
 
 int msckf_restore(msckf_ctx_t* c) {
+    if (c) c->last_async = "msckf_restore";
     if (!c) FAIL(-1, "null context");
     if (!c->has_snapshot) FAIL(-1, "no snapshot");
     c->timer.begin(c->stream, "restore");
@@ -1170,14 +1195,14 @@ int msckf_restore(msckf_ctx_t* c) {
 
 int msckf_sync(msckf_ctx_t* c) {
     if (!c) FAIL(-1, "null context");
-    HIPC(hipStreamSynchronize(c->stream));
+    HIPSYNC(c, hipStreamSynchronize(c->stream));
     c->timer.collect();
     return 0;
 }
 
 int msckf_set_profiling(msckf_ctx_t* c, int on) {
     if (!c) FAIL(-1, "null context");
-    HIPC(hipStreamSynchronize(c->stream));
+    HIPSYNC(c, hipStreamSynchronize(c->stream));
     c->timer.collect();
     c->timer.on = on != 0;
     c->timer.reset();
@@ -1187,7 +1212,7 @@ int msckf_set_profiling(msckf_ctx_t* c, int on) {
 int msckf_kernel_times(msckf_ctx_t* c, int max_k, double* ms_total, int32_t* launches, char* names_out,
                        int names_cap) {
     if (!c) FAIL(-1, "null context");
-    HIPC(hipStreamSynchronize(c->stream));
+    HIPSYNC(c, hipStreamSynchronize(c->stream));
     c->timer.collect();
     int k = std::min<int>(max_k, (int)c->timer.names.size());
     std::string all;
@@ -1212,7 +1237,7 @@ int msckf_debug_workspace(msckf_ctx_t* c, int which, double* out, size_t count) 
     const void* src = which == 0 ? c->Lc.p : which == 1 ? c->Vi.p : which == 2 ? c->Sii.p
                     : which == 3 ? c->G.p : which == 4 ? c->Tm.p : which == 5 ? c->W.p : nullptr;
     if (!src) FAIL(-1, "unknown workspace %d", which);
-    HIPC(hipStreamSynchronize(c->stream));
+    HIPSYNC(c, hipStreamSynchronize(c->stream));
     HIPC(hipMemcpy(out, src, count * sizeof(double), hipMemcpyDeviceToHost));
     return 0;
 }

@@ -36,7 +36,9 @@ typedef double v4d __attribute__((ext_vector_type(4)));
 // (smallest eigenvalue ~ -3e-10 x max diag on synthetic EuRoC-shaped streams);
 // the reference never factors P, so a pivot at or below zero must not abort the
 // update here.  Flooring it factors P_cc + E, E diagonal and ~1e-10 relative:
-// the update moves by that much, far inside the 1e-6 parity tolerance.
+// the update moves by that much, far inside the 1e-6 parity tolerance.  Only
+// pivots down to -PIVOT_FLOOR_NEG x the floor (-1e-6 x max diag) are floored
+// (msckf_rchol.h): a NaN or a deeper negative pivot still fails with -3.
 constexpr double KALMAN_PIVOT_FLOOR = 1e-10;
 
 // workgroup reduction (all threads call; lds: >= 16 doubles of scratch, reused after)
@@ -321,7 +323,7 @@ __global__ void __launch_bounds__(64) k_gchol_diag(DevState<T> st, UpdWs<T> ws, 
     bool bad = false;
     for (int j = 0; j < nb; ++j) {   // right-looking, lane i owns row i
         double piv = d[j][j];
-        if (floor > 0.0 && !(piv >= floor)) piv = floor;
+        piv = pivot_floored(piv, floor);
         if (!(piv > 0.0)) { bad = true; break; }
         const double l = sqrt(piv), inv = 1.0 / l;
         __syncthreads();

@@ -830,12 +830,15 @@ __global__ void __launch_bounds__(256) k_triangulate(DevState<T> st, Params<T> p
         }
         return seg_sum<S>(c);
     };
+    // valid == 2: position given by the host -- never re-triangulated, so the
+    // segment skips the LM iterations (segment-uniform: f is the segment's)
+    const bool given = fb.valid[f] == 2;
     T lam = prm.damping;
     T cost = total_cost(x);
     bool reduced = false;
     T dnorm = T(INFINITY);
     int outer = 0;
-    while (outer < prm.outer_max && dnorm > prm.precision) {
+    while (!given && outer < prm.outer_max && dnorm > prm.precision) {
         // Q2: once a step has been accepted the inner loop never runs again and
         // the solution cannot change any more -> done.
         if (reduced) break;
@@ -902,7 +905,7 @@ __global__ void __launch_bounds__(256) k_triangulate(DevState<T> st, Params<T> p
         const unsigned long long segmask = S == 64 ? ~0ull : (((1ull << S) - 1) << sl0);
         ok = (bad & segmask) == 0;
     }
-    if ((lane & (S - 1)) == 0 && active && fb.valid[f] != 2) {   // 2: position given by the host
+    if ((lane & (S - 1)) == 0 && active && !given) {
         T pw[3];
         mat3_vec(R0w, pf, pw);
         for (int i = 0; i < 3; ++i) fb.p_w[3 * f + i] = pw[i] + t0w[i];

@@ -23,12 +23,18 @@ namespace msckf {
 // all 64 banks (a 128-B stride would put it on two).
 // load(i, j) must be symmetric on the square part (diagonal tiles read both
 // triangles).
-// floor > 0: a pivot below floor (or NaN) is replaced by floor instead of
-// failing -- the factorisation is then the exact one of A + E with E >= 0
-// diagonal, non-zero only at those pivots (a covariance that the reference's
-// non-Joseph update, msckf.py:598-604, has left indefinite at rounding level;
-// the reference never factors it, so it does not fail there either).
+// floor > 0: a pivot in [-PIVOT_FLOOR_NEG x floor, floor) is replaced by
+// floor instead of failing -- the factorisation is then the exact one of
+// A + E with E >= 0 diagonal, non-zero only at those pivots (a covariance that
+// the reference's non-Joseph update, msckf.py:598-604, has left indefinite at
+// rounding level; the reference never factors it, so it does not fail there
+// either).  A NaN pivot or one further below zero is a corrupted covariance,
+// not rounding: it still fails the factorisation.
 // ===========================================================================
+constexpr double PIVOT_FLOOR_NEG = 1e4;   // x floor: the deepest negative pivot still floored
+__device__ __forceinline__ double pivot_floored(double x, double floor) {
+    return (floor > 0.0 && x < floor && x >= -PIVOT_FLOOR_NEG * floor) ? floor : x;
+}
 constexpr int RB = 18;   // doubles per 4-row block of the LDS column buffer
 
 // TILE_LOAD: load(i0, j0, tile) fills a whole 4x4 tile (rows i0.., cols j0..)
@@ -36,7 +42,7 @@ constexpr int RB = 18;   // doubles per 4-row block of the LDS column buffer
 template <int NT, int TPL, class Load, class Panel, class Trail, bool TILE_LOAD = false>
 __device__ __forceinline__ bool rchol_core(int nrow, int ncol, int nelim, double* lds, Load load, Panel panel,
                                            Trail trail, double floor = 0.0) {
-    auto fl = [floor](double x) { return (floor > 0.0 && !(x >= floor)) ? floor : x; };
+    auto fl = [floor](double x) { return pivot_floored(x, floor); };
     const int tid = threadIdx.x;
     const int ntiles = ncol * nrow - ncol * (ncol - 1) / 2;
     int crd[TPL], tlmax[TPL];

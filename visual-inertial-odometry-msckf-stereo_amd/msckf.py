@@ -92,6 +92,7 @@ class MSCKF:
         self.is_gravity_set = False
         self.is_first_img = True
         self.gate_log = []                 # (frame, dof, rows, accepted) like tools/gen_golden.py
+        self.gamma_log = []                # (feature id, gamma), one per gate_log entry
         self.shape_log = []
         self.reset_log = []                # frames after which online_reset fired
         self._deferred = []                # (Pending, callback): update results not read back yet
@@ -328,11 +329,15 @@ class MSCKF:
                 k = 4 * len(cam_lists[i]) - 3
                 ok = bool(gam[i] < chi2[i])
                 self.gate_log.append((frame, dofs[i], k, int(ok)))
+                self.gamma_log.append((f.id, float(gam[i])))
                 if ok:
                     count += k
                 if row_cap and count > row_cap:
                     break
-            self.shape_log.append((frame, rows, D))
+            # no processed feature (every triangulation failed): the reference
+            # returns before measurement_update and logs no shape (msckf.py:652-654)
+            if np.any(valid):
+                self.shape_log.append((frame, rows, D))
         self._deferred.append((pend, apply))
 
     def _remove_lost_features(self):
