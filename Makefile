@@ -6,8 +6,10 @@ LIB      := $(PKG)/libmsckf_hip.so
 HIPCC    ?= /opt/rocm/bin/hipcc
 ARCH     ?= gfx950
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-result -Iinclude -fno-slp-vectorize
-OBJS     := $(SRC)/msckf_kernels.o $(SRC)/msckf_kalman.o $(SRC)/msckf_gate_mfma.o $(SRC)/msckf_api.o $(SRC)/msckf_frontend.o
-HDRS     := $(SRC)/msckf_common.h $(SRC)/msckf_launch.h $(SRC)/msckf_rchol.h include/msckf_hip.h include/msckf_frontend.h
+OBJS     := $(SRC)/msckf_kernels.o $(SRC)/msckf_kalman.o $(SRC)/msckf_gate_mfma.o $(SRC)/msckf_api.o $(SRC)/msckf_frontend.o \
+            $(SRC)/msckf_rccl.o
+HDRS     := $(SRC)/msckf_common.h $(SRC)/msckf_launch.h $(SRC)/msckf_rchol.h include/msckf_hip.h include/msckf_frontend.h \
+            include/msckf_replicas.h
 
 all: $(LIB)
 
@@ -15,7 +17,7 @@ $(SRC)/%.o: $(SRC)/%.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(LIB): $(OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -ldl
 
 # probe build (tools/probes/): same sources with in-kernel phase timers
 PROBE    := tools/probes/libmsckf_probe.so
@@ -25,7 +27,7 @@ tools/probes/obj/%.o: $(SRC)/%.hip $(HDRS)
 	@mkdir -p tools/probes/obj
 	$(HIPCC) $(HIPFLAGS) -DMSCKF_GATE_PROBE -c $< -o $@
 $(PROBE): $(POBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(POBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(POBJS) -ldl
 
 clean:
 	rm -f $(OBJS) $(LIB) $(PROBE)
@@ -42,5 +44,5 @@ tools/exp/obj_$(EXP)/%.o: $(SRC)/%.hip $(HDRS)
 	@mkdir -p tools/exp/obj_$(EXP)
 	$(HIPCC) $(HIPFLAGS) $(EXPFLAGS) -c $< -o $@
 tools/exp/libmsckf_$(EXP).so: $(EOBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(EOBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(EOBJS) -ldl
 .PHONY: exp

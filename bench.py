@@ -21,8 +21,10 @@ cpu_baseline leg, as the checker).
 parent process never touches the GPU) or by an external launcher
 (torch.distributed.run sets WORLD_SIZE).  Ranks are independent replicas
 (the filter does not shard): disjoint problem seeds, no data
-exchange; a host TCP hub (msckf_amd.replicas) carries only the start/stop
-barriers and the max-over-ranks of the elapsed time.
+exchange.  RCCL (msckf_amd.replicas, include/msckf_replicas.h) carries only
+the start/stop barriers, the max-over-ranks of the elapsed time and the device
+gather; a host TCP hub hands out its unique id (and carries the control
+messages itself if RCCL cannot come up -- ``replicas`` in the line says which).
 """
 import argparse
 import json
@@ -443,6 +445,7 @@ def main():
         cpu, refs = cpu_baseline(args, probs[:N_CHECK])
 
     ctx, feat_off = build_batch(args, probs, dtype, grp.local_rank)
+    transport = grp.attach_rccl(ctx.device_info()[0])   # barriers / max / gathers over RCCL from here on
     devs = gather_devices(grp, ctx.device_info())
     el, times = timed_update(ctx, args, grp)
     value = replicas.whole_job_rate(args.batch, grp.world, args.steps, el)
@@ -461,6 +464,7 @@ def main():
                    "cam_states": args.N, "features": args.F, "filters_per_gpu": args.batch,
                    "stacked_rows_mean": float(np.mean(rows)), "parallelism": "replicas%d" % grp.world},
         "devices": devs,
+        "replicas": transport,
         "roofline": roofline_of(times, fl, args, args.dtype),
         "kernel_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in sorted(times.items(), key=lambda kv: -kv[1][0])},
         "canonical_gflop_per_update": round(fl["canonical"] / args.batch / 1e9, 4),

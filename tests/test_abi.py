@@ -47,6 +47,19 @@ def test_frontend_exports_and_binding():
         assert hasattr(lib, s), s
 
 
+def test_replica_transport_exports_and_binding():
+    """include/msckf_replicas.h (RCCL replica transport) is exported by the
+    same library and typed one to one by the binding; librccl itself is opened
+    only when a communicator is made (dlopen), so loading needs no RCCL."""
+    syms = header_symbols("msckf_replicas.h", "msckf_rccl_")
+    assert sorted(_lib.REPLICA_EXPORTED) == syms and len(syms) == 7
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libmsckf_hip.so not built")
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    for s in syms:
+        assert hasattr(lib, s), s
+
+
 def test_load_library_types_functions():
     if not os.path.exists(_lib.LIB_PATH):
         pytest.skip("libmsckf_hip.so not built")

@@ -96,6 +96,19 @@ FRONTEND_SIGS = {
 }
 FRONTEND_EXPORTED = tuple(FRONTEND_SIGS)
 
+# multi-GPU replica transport, RCCL (include/msckf_replicas.h), same library
+REPLICA_SIGS = {
+    "msckf_rccl_unique_id": (C.c_int, [_U8]),
+    "msckf_rccl_init": (C.c_int, [_U8, C.c_int, C.c_int, C.c_int, C.c_double, C.POINTER(_P)]),
+    "msckf_rccl_allreduce": (C.c_int, [_P, _D, C.c_int, C.c_int]),
+    "msckf_rccl_allgather": (C.c_int, [_P, C.c_void_p, C.c_int, C.c_void_p]),
+    "msckf_rccl_count": (C.c_int, [_P, _I, _I]),
+    "msckf_rccl_destroy": (C.c_int, [_P]),
+    "msckf_rccl_last_error": (C.c_char_p, []),
+}
+REPLICA_EXPORTED = tuple(REPLICA_SIGS)
+RCCL_ID_BYTES = 128
+
 
 def load_library(path: str = LIB_PATH):
     """Load and type the shared library (no device work)."""
@@ -107,7 +120,7 @@ def load_library(path: str = LIB_PATH):
             raise MsckfError("HIP extension %s is missing -- build it with `make` "
                              "(or __graft_entry__.build()); there is no CPU fallback" % path)
         lib = C.CDLL(path)
-        for name, (res, args) in list(_SIGS.items()) + list(FRONTEND_SIGS.items()):
+        for name, (res, args) in list(_SIGS.items()) + list(FRONTEND_SIGS.items()) + list(REPLICA_SIGS.items()):
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args

@@ -177,7 +177,8 @@ struct msckf_ctx {
     DBuf<int> row_off;
     GateClasses gc;
     SegClasses sc;
-    DBuf<unsigned char> obs_ws, obs_ht, obs_g, tau, ysq;
+    DBuf<unsigned char> obs_ws, obs_ht, obs_g, fqr, tau, ysq;
+    bool gram = true;   // k_feature writes the Gram records (record-reading assembly)
     // misc scratch
     DBuf<unsigned char> scratch;
     DBuf<int> iscratch;
@@ -258,6 +259,8 @@ FeatBatch<T> feat_batch(msckf_ctx* c) {
     f.obs_ws = reinterpret_cast<T*>(c->obs_ws.p);
     f.obs_ht = reinterpret_cast<T*>(c->obs_ht.p);
     f.obs_g = reinterpret_cast<double*>(c->obs_g.p);
+    f.fqr = reinterpret_cast<double*>(c->fqr.p);
+    f.gram = c->gram ? 1 : 0;
     f.compact = feature_needs_compact(c->maxM) ? 1 : 0;
     f.tau = reinterpret_cast<T*>(c->tau.p);
     f.ysq = reinterpret_cast<T*>(c->ysq.p);
@@ -392,7 +395,7 @@ int load_features(msckf_ctx* c, int nf, const int32_t* feat_off, int single_filt
     HIPC(c->row_off.ensure(nf + 1));
     HIPC(c->obs_ws.ensure(((feature_needs_compact(maxM) ? nobs : 0) * OBS_WS + OBS_WS) * ts));
     HIPC(c->obs_ht.ensure((nobs * OBS_HTS + OBS_HTS) * ts));
-    HIPC(c->obs_g.ensure((nobs + 1) * OBG_STRIDE * sizeof(double)));
+    HIPC(c->fqr.ensure((nf + 1) * FQR_STRIDE * sizeof(double)));
     HIPC(c->tau.ensure((nf * 4 + 4) * ts));
     {   // the (4M)^2 global gating scratch is only needed by features too large
         // for the LDS gating path (M > ~50 in fp32, > ~35 in fp64)
@@ -503,6 +506,14 @@ int load_features(msckf_ctx* c, int nf, const int32_t* feat_off, int single_filt
         c->max_nf = std::max(c->max_nf, h_off[b + 1] - h_off[b]);
         if (h_off[b + 1] > h_off[b]) c->max_obs = std::max(c->max_obs, obs_off[h_off[b + 1]] - obs_off[h_off[b]]);
     }
+    // Gram records only for the record-reading assembly (windows > 32 cams, or
+    // per-filter tables too large for the fused kernel's LDS)
+#ifndef MSCKF_INFO_RECORDS
+    c->gram = !info_fused_fits(c->Nmax, c->max_nf);
+#else
+    c->gram = true;   // experiment builds: force the record path
+#endif
+    if (c->gram) HIPC(c->obs_g.ensure(((size_t)nobs + 1) * OBG_STRIDE * sizeof(double)));
     c->h_feat_off = h_off;
     return 0;
 }
@@ -548,7 +559,7 @@ int run_update_chain(msckf_ctx* c, int row_cap, bool triangulate) {
     launch_select<T>(s, st, fb, ws, row_cap);
     c->timer.end(s);
     c->timer.begin(s, "compress");
-    launch_compress<T>(s, st, fb, ws, c->max_nf, c->max_obs);
+    launch_compress<T>(s, st, prm, fb, ws, c->max_nf, c->max_obs);
     c->timer.end(s);
     if (early_a) {
         HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
@@ -1007,7 +1018,7 @@ int msckf_destroy(msckf_ctx_t* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->side) (void)hipStreamSynchronize(c->side);
     for (auto* b : {&c->P, &c->imu, &c->cams, &c->P_snap, &c->imu_snap, &c->cams_snap, &c->Hthin, &c->Lc, &c->Vi, &c->Sii, &c->G, &c->Tm, &c->W, &c->Wk,
-                    &c->dx, &c->batch, &c->obs_ws, &c->obs_ht, &c->obs_g, &c->tau, &c->ysq, &c->scratch})
+                    &c->dx, &c->batch, &c->obs_ws, &c->obs_ht, &c->obs_g, &c->fqr, &c->tau, &c->ysq, &c->scratch})
         b->release();
     for (auto* b : {&c->ncams, &c->ncams_snap, &c->info, &c->afail, &c->row_off, &c->iscratch})
         b->release();

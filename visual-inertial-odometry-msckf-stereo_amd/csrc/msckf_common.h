@@ -47,6 +47,13 @@ constexpr int OBS_HT = 0, OBS_RT = 18, OBS_HTS = 24;
 // 48-double stride put them on two and made k_info's record reads 4-way
 // bank-conflicted).
 constexpr int OBG_G = 0, OBG_DS = 18, OBG_UB = 39, OBG_CAM = 45, OBG_STRIDE = 46;
+// Per-feature QR record (fp64, always written by the feature kernel): with
+// H_f = Q R the thin Householder QR of the feature's stacked 4M x 3 H_f,
+//   X = R^-1 (upper; x00 x01 x02 x11 x12 x22),  g = (Q^T r)[0:3]
+// so that the fused information assembly (k_info_fused) rebuilds an
+// observation's G_i = (Q^T Hx)[0:3, cam i] = X^T H_f,i^T Hx_i from its own
+// Jacobian blocks instead of reading obs_g.
+constexpr int FQR_X = 0, FQR_G = 6, FQR_STRIDE = 10;
 
 template <typename T>
 struct Params {
@@ -81,7 +88,9 @@ struct FeatBatch {
     uint8_t* valid;           // [nf] triangulation validity (1 if p_w given)
     T* obs_ws;                // [sum M][OBS_WS] (compact-factor consumers only)
     T* obs_ht;                // [sum M][OBS_HTS] gating rows
-    double* obs_g;            // [sum M][OBG_STRIDE] Gram terms (fp64)
+    double* obs_g;            // [sum M][OBG_STRIDE] Gram terms (fp64), written only if gram
+    double* fqr;              // [nf][FQR_STRIDE] R^-1 and (Q^T r)[0:3] of H_f's QR (fp64)
+    int gram;                 // write obs_g (record-reading assembly, k_info / k_info_mfma)
     int compact;              // write V / W / Q^T r / tau (LDS gate fallback, QR path)
     T* tau;                   // [nf][4]
     T* ysq;                   // gating scratch

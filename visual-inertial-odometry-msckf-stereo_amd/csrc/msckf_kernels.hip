@@ -948,7 +948,10 @@ __device__ __forceinline__ void store_pairs(T* dst, const S* src, int n) {
 }
 
 // (one observation per lane: three waves per SIMD -- 168 VGPRs, a 12-byte spill)
-template <typename T, int S, int OPL>
+// GRAM: also write the per-observation Gram records (obs_g) for the
+// record-reading assembly; the fused assembly (k_info_fused) rebuilds them
+// from the Jacobians and needs only the per-feature QR record (fqr).
+template <typename T, int S, int OPL, bool GRAM>
 __global__ void __launch_bounds__(256, OPL == 1 ? 3 : 1) k_feature(DevState<T> st, Params<T> prm, FeatBatch<T> fb,
                                                  const int* __restrict__ flist, int cnt) {
     using CT = double;
@@ -1066,13 +1069,14 @@ __global__ void __launch_bounds__(256, OPL == 1 ? 3 : 1) k_feature(DevState<T> s
             store_pairs(wsr + OBS_HT, Ht, 18);
             store_pairs(wsr + OBS_RT, rt4, 4);
         }
-        for (int c = 0; c < 6; ++c)   // Hx_i^T r_i, before r is reflected
-            u6[s][c] = Hx[s][c] * r[s][0] + Hx[s][6 + c] * r[s][1] + Hx[s][12 + c] * r[s][2] + Hx[s][18 + c] * r[s][3];
+        if constexpr (GRAM)
+            for (int c = 0; c < 6; ++c)   // Hx_i^T r_i, before r is reflected
+                u6[s][c] = Hx[s][c] * r[s][0] + Hx[s][6 + c] * r[s][1] + Hx[s][12 + c] * r[s][2] + Hx[s][18 + c] * r[s][3];
         if (own && fb.compact) store_pairs(fb.obs_ws + (size_t)(o0 + i) * OBS_WS + OBS_R, r[s], 4);
     }
     // ---- Householder QR of H_f across the segment (rows 4i..4i+3 with observation i) ----
     CT V[OPL][12];
-    CT tau[3];
+    CT tau[3], rd[3];   // reflector scalars; R's diagonal (beta_j)
 #pragma unroll
     for (int s = 0; s < OPL; ++s)
         for (int e = 0; e < 12; ++e) V[s][e] = 0;
@@ -1094,6 +1098,7 @@ __global__ void __launch_bounds__(256, OPL == 1 ? 3 : 1) k_feature(DevState<T> s
             scale = CT(1) / (alpha - beta);
         }
         tau[j] = tj;
+        rd[j] = beta;
         // v_j: v[j] = 1, v[row > j] = Hf[row][j] * scale, 0 above
 #pragma unroll
         for (int s = 0; s < OPL; ++s)
@@ -1117,6 +1122,27 @@ __global__ void __launch_bounds__(256, OPL == 1 ? 3 : 1) k_feature(DevState<T> s
                     else r[s][a] -= tj * V[s][3 * a + j] * w;
                 }
         }
+    }
+    // ---- per-feature QR record: X = R^-1 and g = (Q^T r)[0:3] (the segment's
+    // first lane holds observation 0, i.e. rows 0..2 of the reflected H_f and r).
+    // A zero pivot (rank-deficient H_f) drops its direction instead of dividing.
+    if (l == 0 && M > 0) {
+        const CT r01 = Hf[0][1], r02 = Hf[0][2], r12 = Hf[0][5];
+        const CT x00 = rd[0] != CT(0) ? 1 / rd[0] : CT(0), x11 = rd[1] != CT(0) ? 1 / rd[1] : CT(0);
+        const CT x22 = rd[2] != CT(0) ? 1 / rd[2] : CT(0);
+        CT q[FQR_STRIDE];
+        q[FQR_X + 0] = x00;
+        q[FQR_X + 1] = -r01 * x00 * x11;
+        q[FQR_X + 2] = (r01 * r12 * x11 - r02) * x00 * x22;
+        q[FQR_X + 3] = x11;
+        q[FQR_X + 4] = -r12 * x11 * x22;
+        q[FQR_X + 5] = x22;
+        for (int t = 0; t < 3; ++t) q[FQR_G + t] = r[0][t];
+        q[9] = 0;
+        store_pairs(fb.fqr + (size_t)f * FQR_STRIDE, q, FQR_STRIDE);
+    }
+    if constexpr (!GRAM) {
+        if (!fb.compact) return;
     }
     // ---- w_j = v_j^T X_{j-1}: 6 columns per observation, local to the lane ----
     CT d10 = 0, d20 = 0, d21 = 0;
@@ -1159,6 +1185,7 @@ __global__ void __launch_bounds__(256, OPL == 1 ? 3 : 1) k_feature(DevState<T> s
             if (i == 0)
                 for (int j = 0; j < 3; ++j) fb.tau[4 * f + j] = (T)tau[j];
         }
+        if constexpr (!GRAM) continue;
         // Gram terms.  (Q^T Hx)[t][i-block] = [i == 0] Hx_0[t] - sum_j tau_j V_0[t][j] W_j(i)
         CT rec[OBG_STRIDE];   // G | DS | UB | pad, stored as 16-byte pairs
         for (int t = 0; t < 3; ++t)
@@ -2428,6 +2455,311 @@ __global__ void __launch_bounds__(64 * IM_NW) k_info_mfma(DevState<T> st, FeatBa
     if (tid == 0) info[1] = C;
 }
 
+// ---------------------------------------------------------------------------
+// Fused information assembly (windows up to 32 cams): k_info_mfma's SYRK
+// without the per-observation Gram records.  Each staged feature's G_i,
+// Hx_i^T Hx_i and UB_i are rebuilt in the workgroup from the inputs -- the
+// cam poses (a per-cam geometry table in LDS), p_w, z -- and the feature's QR
+// record (fqr: X = R^-1, g = (Q^T r)[0:3], written by k_feature), so k_feature
+// stores 80 bytes per feature instead of 368 per observation and nothing is
+// read back (msckf.py:429-556: measurement_jacobian, feature_jacobian's
+// projection and the QR compression, through the Gram identity of k_info).
+//
+// Per observation (one producer thread each), with Jc the 4 x 3 derivative of
+// z by the cam-0 point (msckf.py:457-475) and B~ = [ [p_c0]x | -R_w_c0 ] with
+// the observability projection (msckf.py:484-490) applied, Hx_i = Jc B~ and
+// H_f,i = -Hx_i[:, 3:6].  With Jc^T Jc = L L^T (3 x 3 Cholesky):
+//     H^ = L^T B~ (3 x 6),  n^ = L^-1 Jc^T r_i
+//     Hx_i^T Hx_i = H^^T H^,  Hx_i^T r_i = H^^T n^,
+//     H_f,i^T Hx_i = F^T H^ with F = -H^[:, 3:6],  G_i = X^T (F^T H^),
+// -- the rank-3 form of the gate's records, in fp64.  The update is invariant
+// to the orthogonal row maps involved (quirk Q4).
+//
+// Pipeline: IF_KF features per chunk; thread (s, c) of the chunk's producer
+// group (IF_KF x 32 threads) builds feature s's observation of cam c into the
+// chunk's LDS rows of Gall (zeros if the feature does not see cam c) and adds
+// its Hx^T Hx / UB terms into the (s, c) slot of an LDS accumulator (summed
+// over s at the end).  Chunk i + 1 is built by one producer group while every
+// wave runs chunk i's MFMAs (double-buffered rows, one barrier per chunk);
+// the groups take turns, so the VALU work is spread over all waves.
+// ---------------------------------------------------------------------------
+constexpr int IF_KF = 8, IF_KR = 3 * IF_KF, IF_NKS = IF_KR / 4, IF_NP = 32 * IF_KF;
+constexpr int IF_ACC = 27, IF_CG = 27;   // doubles per accumulator slot / per cam geometry record
+constexpr int IF_NW = 8;                 // waves per workgroup (two per SIMD: 256 VGPRs for tiles + producer)
+
+__host__ __device__ constexpr size_t info_fused_lds(int maxnf) {
+    return (size_t)(2 * IF_KR * IM_GS + IF_KF * 32 * IF_ACC + 32 * IF_CG) * sizeof(double) + (size_t)maxnf * 48 + 16;
+}
+
+template <typename T, int NW>
+__global__ void __launch_bounds__(64 * NW) k_info_fused(DevState<T> st, Params<T> prm, FeatBatch<T> fb, UpdWs<T> ws,
+                                                        int maxnf) {
+    constexpr int NT = 64 * NW, PPW = (78 + NW - 1) / NW, NG = NT / IF_NP;
+    static_assert(NT % IF_NP == 0 && PPW * NW >= 78 && IF_KR % 4 == 0, "k_info_fused shape");
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, lc = lane & 15, lr = lane >> 4;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    int* info = ws.info + 4 * b;
+    if (info[0] == 0) {   // nothing stacked: empty update
+        if (tid == 0) info[1] = 0;
+        return;
+    }
+    const int nc = st.ncams[b], C = 6 * nc, Cmax = ws.Cmax;
+    const int TT = (C + 15) >> 4, npair = TT * (TT + 1) / 2;
+    double* buf = reinterpret_cast<double*>(smem_raw);          // [2][KR][IM_GS] dense rows of Gall
+    double* acc = buf + 2 * IF_KR * IM_GS;                      // [KF][32][IF_ACC] Hx^T Hx (21) | UB (6)
+    double* camg = acc + IF_KF * 32 * IF_ACC;                   // [32][IF_CG] R0 | R1 | t1 | p | R(q_null) g
+    int* flist = reinterpret_cast<int*>(camg + 32 * IF_CG);     // [maxnf] included features, in order
+    unsigned* ftm = reinterpret_cast<unsigned*>(flist + maxnf); // [maxnf] their tile masks
+    int* fo0 = reinterpret_cast<int*>(ftm + maxnf);             // [maxnf] first observation
+    int* fM = fo0 + maxnf;                                      // [maxnf] observations (0: not included)
+    unsigned char* posb = reinterpret_cast<unsigned char*>(fM + maxnf);   // [maxnf][32] cam -> observation (0xff)
+    int* s_n = reinterpret_cast<int*>(posb + 32 * (size_t)maxnf);
+    const int fbeg = fb.feat_off[b], fend = fb.feat_off[b + 1], nf = fend - fbeg;
+    for (int e = tid; e < 2 * IF_KR * IM_GS + IF_KF * 32 * IF_ACC; e += NT) buf[e] = 0.0;   // rows and accumulators
+    for (int e = tid; e < 8 * nf; e += NT) reinterpret_cast<int*>(posb)[e] = -1;
+    for (int f = tid; f < nf; f += NT) {
+        const int a0 = fb.obs_off[fbeg + f], a1 = fb.obs_off[fbeg + f + 1];
+        fo0[f] = a0;
+        fM[f] = fb.include[fbeg + f] ? a1 - a0 : 0;
+    }
+    double g[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) g[k] = (double)st.imu[(size_t)b * IMU_STRIDE + I_G + k];
+    if (tid < nc) {   // per-cam geometry (k_feature's per-observation poses, once per cam)
+        const T* cq = st.cams + ((size_t)b * st.Nmax + tid) * CAM_STRIDE;
+        double q0[4], qn[4], R0[9], R1[9], Rn[9], R01[9], t01[3], tmp[3];
+        for (int k = 0; k < 4; ++k) { q0[k] = (double)cq[C_Q + k]; qn[k] = (double)cq[C_QN + k]; }
+        for (int k = 0; k < 9; ++k) R01[k] = (double)prm.R01[k];
+        for (int k = 0; k < 3; ++k) t01[k] = (double)prm.t01[k];
+        quat_to_rot(q0, R0);
+        mat3_mul(R01, R0, R1);
+        mat3T_vec(R1, t01, tmp);
+        quat_to_rot(qn, Rn);
+        double* cg = camg + tid * IF_CG;
+        for (int k = 0; k < 9; ++k) { cg[k] = R0[k]; cg[9 + k] = R1[k]; }
+        for (int k = 0; k < 3; ++k) {
+            const double cp = (double)cq[C_P + k];
+            cg[18 + k] = cp - tmp[k];
+            cg[21 + k] = cp;
+        }
+        mat3_vec(Rn, g, cg + 24);
+    }
+    __syncthreads();
+    for (int f = tid >> 5; f < nf; f += NT / 32) {   // cam -> observation, 32 lanes per feature
+        const int o = tid & 31;
+        if (o < fM[f]) posb[32 * f + fb.obs_cam[fo0[f] + o]] = (unsigned char)o;
+    }
+    if (wv == 0) {   // the included features, in order
+        int base = 0;
+        for (int f0 = 0; f0 < nf; f0 += 64) {
+            const int f = f0 + lane;
+            const bool in = f < nf && fM[f] > 0;
+            const unsigned long long bal = __ballot(in);
+            if (in) flist[base + __popcll(bal & ((1ull << lane) - 1ull))] = f;
+            base += __popcll(bal);
+        }
+        if (lane == 0) *s_n = base;
+    }
+    __syncthreads();
+    const int nl = *s_n;
+    for (int i = tid; i < nl; i += NT) {
+        const unsigned char* pb = posb + 32 * flist[i];
+        unsigned m = 0;
+        for (int c = 0; c < nc; ++c)
+            if (pb[c] != 0xff) m |= (1u << ((6 * c) >> 4)) | (1u << ((6 * c + 5) >> 4));
+        ftm[i] = m;
+    }
+    // this wave's tiles (lower, row-major order p -> (ti, tj))
+    int pti[PPW], ptj[PPW];
+    bool pv[PPW];
+    v4d tacc[PPW];
+#pragma unroll
+    for (int q = 0; q < PPW; ++q) {
+        const int p = PPW * wv + q;
+        int ti = (int)((sqrtf(8.0f * (float)p + 1.0f) - 1.0f) * 0.5f);
+        while (ti * (ti + 1) / 2 > p) --ti;
+        while ((ti + 1) * (ti + 2) / 2 <= p) ++ti;
+        pti[q] = __builtin_amdgcn_readfirstlane(ti);
+        ptj[q] = __builtin_amdgcn_readfirstlane(p - ti * (ti + 1) / 2);
+        pv[q] = p < npair;
+        tacc[q] = v4d{0.0, 0.0, 0.0, 0.0};
+    }
+    const int grp = tid / IF_NP, ps = (tid % IF_NP) >> 5, pc = tid & 31;
+    // build chunk [l0, l0 + KF) into row buffer bb (producer thread (ps, pc))
+    auto produce = [&](int l0, int bb) {
+        if (pc >= nc) return;
+        double* dst = buf + (size_t)bb * IF_KR * IM_GS + 3 * ps * IM_GS + 6 * pc;
+        const int li = l0 + ps;
+        const int f = li < nl ? flist[li] : -1;
+        const int o = f >= 0 ? (int)posb[32 * f + pc] : 0xff;
+        if (o == 0xff) {
+#pragma unroll
+            for (int t = 0; t < 3; ++t)
+#pragma unroll
+                for (int u = 0; u < 6; ++u) dst[t * IM_GS + u] = 0.0;
+            return;
+        }
+        const int fg = fbeg + f, og = fo0[f] + o;
+        const double pw[3] = {(double)fb.p_w[3 * fg], (double)fb.p_w[3 * fg + 1], (double)fb.p_w[3 * fg + 2]};
+        const T* zp = fb.obs_z + (size_t)og * 4;
+        const double z0 = (double)zp[0], z1 = (double)zp[1], z2 = (double)zp[2], z3 = (double)zp[3];
+        const double* qr = fb.fqr + (size_t)fg * FQR_STRIDE;
+        const double* cg = camg + pc * IF_CG;
+        double d0[3], d1[3], pc0[3], pc1[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) { d0[k] = pw[k] - cg[21 + k]; d1[k] = pw[k] - cg[18 + k]; }
+        mat3_vec(cg, d0, pc0);
+        mat3_vec(cg + 9, d1, pc1);
+        // Jc (msckf.py:457-475): rows [a00 0 a02], [0 a00 a12], b-rows times R01
+        const double i0 = 1.0 / pc0[2], i1 = 1.0 / pc1[2];
+        const double a00 = i0, a02 = -pc0[0] * i0 * i0, a12 = -pc0[1] * i0 * i0;
+        const double b00 = i1, b02 = -pc1[0] * i1 * i1, b12 = -pc1[1] * i1 * i1;
+        double J2[3], J3[3];
+#pragma unroll
+        for (int m = 0; m < 3; ++m) {
+            J2[m] = b00 * (double)prm.R01[m] + b02 * (double)prm.R01[6 + m];
+            J3[m] = b00 * (double)prm.R01[3 + m] + b12 * (double)prm.R01[6 + m];
+        }
+        const double r0 = z0 - pc0[0] * i0, r1 = z1 - pc0[1] * i0, r2 = z2 - pc1[0] * i1, r3 = z3 - pc1[1] * i1;
+        // L L^T = Jc^T Jc, n^ = L^-1 Jc^T r (a direction with no pivot is dropped)
+        const double m00 = a00 * a00 + J2[0] * J2[0] + J3[0] * J3[0];
+        const double m10 = J2[1] * J2[0] + J3[1] * J3[0];
+        const double m20 = a02 * a00 + J2[2] * J2[0] + J3[2] * J3[0];
+        const double m11 = a00 * a00 + J2[1] * J2[1] + J3[1] * J3[1];
+        const double m21 = a12 * a00 + J2[2] * J2[1] + J3[2] * J3[1];
+        const double m22 = a02 * a02 + a12 * a12 + J2[2] * J2[2] + J3[2] * J3[2];
+        const double n0 = a00 * r0 + J2[0] * r2 + J3[0] * r3;
+        const double n1 = a00 * r1 + J2[1] * r2 + J3[1] * r3;
+        const double n2 = a02 * r0 + a12 * r1 + J2[2] * r2 + J3[2] * r3;
+        const double l00 = sqrt(m00), il0 = l00 > 0 ? 1.0 / l00 : 0.0;
+        const double l10 = m10 * il0, l20 = m20 * il0;
+        const double e11 = m11 - l10 * l10;
+        const double l11 = e11 > 0 ? sqrt(e11) : 0.0, il1 = l11 > 0 ? 1.0 / l11 : 0.0;
+        const double l21 = (m21 - l20 * l10) * il1;
+        const double e22 = m22 - l20 * l20 - l21 * l21;
+        const double l22 = e22 > 0 ? sqrt(e22) : 0.0, il2 = l22 > 0 ? 1.0 / l22 : 0.0;
+        const double h0 = n0 * il0, h1 = (n1 - l10 * h0) * il1, h2 = (n2 - l20 * h0 - l21 * h1) * il2;
+        // B~ = [ [p_c0]x | -R_w_c0 ] (I - u u^T / u^T u), u = [R(q_null) g ; (p_w - p) x g]  (msckf.py:484-490)
+        double u[6];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) u[k] = cg[24 + k];
+        u[3] = d0[1] * g[2] - d0[2] * g[1];
+        u[4] = d0[2] * g[0] - d0[0] * g[2];
+        u[5] = d0[0] * g[1] - d0[1] * g[0];
+        double uu = 0.0;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) uu += u[k] * u[k];
+        const double iuu = 1.0 / uu;
+        double H[3][6];   // B~, then H^ = L^T B~ in place (row a needs rows >= a only)
+        {
+            const double Sk[9] = {0.0, -pc0[2], pc0[1], pc0[2], 0.0, -pc0[0], -pc0[1], pc0[0], 0.0};
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                double row[6];
+#pragma unroll
+                for (int m = 0; m < 3; ++m) { row[m] = Sk[3 * a + m]; row[3 + m] = -cg[3 * a + m]; }
+                double bu = 0.0;
+#pragma unroll
+                for (int m = 0; m < 6; ++m) bu += row[m] * u[m];
+                bu *= iuu;
+#pragma unroll
+                for (int m = 0; m < 6; ++m) H[a][m] = row[m] - bu * u[m];
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < 6; ++m) {
+            H[0][m] = l00 * H[0][m] + l10 * H[1][m] + l20 * H[2][m];
+            H[1][m] = l11 * H[1][m] + l21 * H[2][m];
+            H[2][m] = l22 * H[2][m];
+        }
+        // G_i = X^T (F^T H^), F = -H^[:, 3:6]; rows written as soon as formed
+        const double x00 = qr[FQR_X], x01 = qr[FQR_X + 1], x02 = qr[FQR_X + 2];
+        const double x11 = qr[FQR_X + 3], x12 = qr[FQR_X + 4], x22 = qr[FQR_X + 5];
+        double K[3][6];
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+#pragma unroll
+            for (int m = 0; m < 6; ++m) K[j][m] = -(H[0][3 + j] * H[0][m] + H[1][3 + j] * H[1][m] + H[2][3 + j] * H[2][m]);
+#pragma unroll
+        for (int m = 0; m < 6; ++m) {
+            K[2][m] = x02 * K[0][m] + x12 * K[1][m] + x22 * K[2][m];
+            K[1][m] = x01 * K[0][m] + x11 * K[1][m];
+            K[0][m] = x00 * K[0][m];
+        }
+#pragma unroll
+        for (int t = 0; t < 3; ++t)
+#pragma unroll
+            for (int m = 0; m < 6; ++m) dst[t * IM_GS + m] = K[t][m];
+        // Hx^T Hx (packed lower, as OBG_DS) and UB = Hx^T r - G^T g, into slot (ps, pc)
+        const double gr0 = qr[FQR_G], gr1 = qr[FQR_G + 1], gr2 = qr[FQR_G + 2];
+        double* ac = acc + (ps * 32 + pc) * IF_ACC;
+#pragma unroll
+        for (int x = 0, e = 0; x < 6; ++x)
+#pragma unroll
+            for (int y = 0; y <= x; ++y, ++e) ac[e] += H[0][x] * H[0][y] + H[1][x] * H[1][y] + H[2][x] * H[2][y];
+#pragma unroll
+        for (int x = 0; x < 6; ++x)
+            ac[21 + x] += (H[0][x] * h0 + H[1][x] * h1 + H[2][x] * h2) - (K[0][x] * gr0 + K[1][x] * gr1 + K[2][x] * gr2);
+    };
+    if (nl > 0 && grp == 0) produce(0, 0);
+    __syncthreads();
+    for (int l0 = 0, it = 0; l0 < nl; l0 += IF_KF, ++it) {
+        const int cur = it & 1;
+        // ---- rank-KR update of this wave's tiles from chunk it ----
+        const double* cb = buf + (size_t)cur * IF_KR * IM_GS;
+#pragma unroll
+        for (int ks = 0; ks < IF_NKS; ++ks) {
+            const int sa = l0 + (4 * ks) / 3, sb = l0 + (4 * ks + 3) / 3;
+            unsigned km = (sa < nl ? ftm[sa] : 0u) | (sb < nl ? ftm[sb] : 0u);
+            km = __builtin_amdgcn_readfirstlane(km);
+            const double* brow = cb + (4 * ks + lr) * IM_GS + lc;
+#pragma unroll
+            for (int q = 0; q < PPW; ++q)
+                if (pv[q] && ((km >> pti[q]) & (km >> ptj[q]) & 1u))
+                    tacc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(brow[16 * pti[q]], brow[16 * ptj[q]], tacc[q], 0, 0, 0);
+        }
+        // ---- the next chunk, by the group whose turn it is ----
+        if (l0 + IF_KF < nl && grp == (it + 1) % NG) produce(l0 + IF_KF, cur ^ 1);
+        __syncthreads();
+    }
+    KT* F = ws.Hthin + (size_t)b * Cmax * (Cmax + 1);
+    const int ldf = Cmax + 1;
+#pragma unroll
+    for (int q = 0; q < PPW; ++q) {
+        if (!pv[q]) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int row = 16 * pti[q] + lr + 4 * r, col = 16 * ptj[q] + lc;
+            if (row < C && col < C) {
+                const double v = -tacc[q][r];
+                F[(size_t)row * ldf + col] = v;
+                F[(size_t)col * ldf + row] = v;
+            }
+        }
+    }
+    __syncthreads();   // the tiles' stores are visible to the block-diagonal owners
+    for (int e = tid; e < 27 * nc; e += NT) {   // (cam, element) owners: sum the KF slots
+        const int dc = e / 27, de = e - 27 * dc;
+        double dsum = 0.0;
+#pragma unroll
+        for (int s2 = 0; s2 < IF_KF; ++s2) dsum += acc[(s2 * 32 + dc) * IF_ACC + de];
+        if (de < 21) {
+            int x = (int)((sqrtf(8.0f * (float)de + 1.0f) - 1.0f) * 0.5f);
+            while (x * (x + 1) / 2 > de) --x;
+            while ((x + 1) * (x + 2) / 2 <= de) ++x;
+            const int y = de - x * (x + 1) / 2;
+            const size_t i0 = (size_t)(6 * dc + x) * ldf + 6 * dc + y, i1 = (size_t)(6 * dc + y) * ldf + 6 * dc + x;
+            const double v = F[i0] + dsum;
+            F[i0] = v;
+            if (x != y) F[i1] = v;
+        } else {
+            F[(size_t)(6 * dc + de - 21) * ldf + Cmax] = dsum;
+        }
+    }
+    if (tid == 0) info[1] = C;
+}
+
 // State correction (msckf.py:566-595).
 template <typename T>
 __global__ void __launch_bounds__(64) k_correct(DevState<T> st, UpdWs<T> ws) {
@@ -2538,12 +2870,22 @@ void launch_feature(hipStream_t s, const DevState<T>& st, const Params<T>& prm, 
         const int* list = sc.list + sc.off[c];
         const int lanes = SegClasses::S[c] < 64 ? SegClasses::S[c] : 64;   // S = 128: 2 observations per lane
         const int waves = (cnt * lanes + 63) / 64, blocks = (waves + 3) / 4;
-        switch (SegClasses::S[c]) {
-            case 8: hipLaunchKernelGGL((k_feature<T, 8, 1>), dim3(blocks), dim3(256), 0, s, st, prm, fb, list, cnt); break;
-            case 16: hipLaunchKernelGGL((k_feature<T, 16, 1>), dim3(blocks), dim3(256), 0, s, st, prm, fb, list, cnt); break;
-            case 32: hipLaunchKernelGGL((k_feature<T, 32, 1>), dim3(blocks), dim3(256), 0, s, st, prm, fb, list, cnt); break;
-            case 64: hipLaunchKernelGGL((k_feature<T, 64, 1>), dim3(blocks), dim3(256), 0, s, st, prm, fb, list, cnt); break;
-            default: hipLaunchKernelGGL((k_feature<T, 64, 2>), dim3(blocks), dim3(256), 0, s, st, prm, fb, list, cnt); break;
+        if (fb.gram) {
+            switch (SegClasses::S[c]) {
+                case 8: hipLaunchKernelGGL((k_feature<T, 8, 1, true>), dim3(blocks), dim3(256), 0, s, st, prm, fb, list, cnt); break;
+                case 16: hipLaunchKernelGGL((k_feature<T, 16, 1, true>), dim3(blocks), dim3(256), 0, s, st, prm, fb, list, cnt); break;
+                case 32: hipLaunchKernelGGL((k_feature<T, 32, 1, true>), dim3(blocks), dim3(256), 0, s, st, prm, fb, list, cnt); break;
+                case 64: hipLaunchKernelGGL((k_feature<T, 64, 1, true>), dim3(blocks), dim3(256), 0, s, st, prm, fb, list, cnt); break;
+                default: hipLaunchKernelGGL((k_feature<T, 64, 2, true>), dim3(blocks), dim3(256), 0, s, st, prm, fb, list, cnt); break;
+            }
+        } else {
+            switch (SegClasses::S[c]) {
+                case 8: hipLaunchKernelGGL((k_feature<T, 8, 1, false>), dim3(blocks), dim3(256), 0, s, st, prm, fb, list, cnt); break;
+                case 16: hipLaunchKernelGGL((k_feature<T, 16, 1, false>), dim3(blocks), dim3(256), 0, s, st, prm, fb, list, cnt); break;
+                case 32: hipLaunchKernelGGL((k_feature<T, 32, 1, false>), dim3(blocks), dim3(256), 0, s, st, prm, fb, list, cnt); break;
+                case 64: hipLaunchKernelGGL((k_feature<T, 64, 1, false>), dim3(blocks), dim3(256), 0, s, st, prm, fb, list, cnt); break;
+                default: hipLaunchKernelGGL((k_feature<T, 64, 2, false>), dim3(blocks), dim3(256), 0, s, st, prm, fb, list, cnt); break;
+            }
         }
     }
 }
@@ -2690,9 +3032,23 @@ static void launch_info_cfg(hipStream_t s, const DevState<T>& st, const FeatBatc
                        pre ? maxobs : 0);
 }
 
+bool info_fused_fits(int Nmax, int maxnf) { return Nmax <= 32 && maxnf > 0 && info_fused_lds(maxnf) <= 160 * 1024; }
+
 template <typename T>
-void launch_compress(hipStream_t s, const DevState<T>& st, const FeatBatch<T>& fb, const UpdWs<T>& ws, int maxnf,
-                     int maxobs) {
+void launch_compress(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const FeatBatch<T>& fb,
+                     const UpdWs<T>& ws, int maxnf, int maxobs) {
+    // windows up to 32 cams, no Gram records: the fused assembly (k_info_fused)
+    if (!fb.gram) {
+        const size_t lds = info_fused_lds(maxnf);
+        static size_t attr = 64 * 1024;
+        if (lds > attr) {
+            (void)hipFuncSetAttribute((const void*)k_info_fused<T, IF_NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)lds);
+            attr = lds;
+        }
+        hipLaunchKernelGGL((k_info_fused<T, IF_NW>), dim3(st.B), dim3(64 * IF_NW), lds, s, st, prm, fb, ws, maxnf);
+        return;
+    }
     // windows up to 32 cams: fp64 MFMA tiles (k_info_mfma)
     const size_t lds_m = info_mfma_lds(maxnf, maxobs);
     if (st.Nmax <= 32 && maxobs > 0 && lds_m <= 160 * 1024) {
@@ -2733,7 +3089,7 @@ void launch_kalman(hipStream_t s, const DevState<T>& st, const Params<T>& prm, c
     template void launch_feature<T>(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&, const SegClasses&); \
     template void launch_gate<T>(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&, const GateClasses&); \
     template void launch_select<T>(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const UpdWs<T>&, int); \
-    template void launch_compress<T>(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const UpdWs<T>&, int, int); \
+    template void launch_compress<T>(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&, const UpdWs<T>&, int, int); \
     template void launch_kalman<T>(hipStream_t, const DevState<T>&, const Params<T>&, const UpdWs<T>&, KernelTimer*);
 INSTANTIATE(float)
 INSTANTIATE(double)

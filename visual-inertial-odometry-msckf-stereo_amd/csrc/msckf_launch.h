@@ -116,7 +116,11 @@ void launch_gate_mfma_wg(hipStream_t, const DevState<float>&, const Params<float
 template <typename T>
 void launch_select(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const UpdWs<T>&, int row_cap);
 template <typename T>
-void launch_compress(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const UpdWs<T>&, int maxnf, int maxobs);
+void launch_compress(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&, const UpdWs<T>&, int maxnf,
+                     int maxobs);
+// The fused information assembly (no per-observation Gram records) runs when
+// the window has <= 32 cams and its per-filter tables fit the LDS.
+bool info_fused_fits(int Nmax, int maxnf);
 // The workgroup gating kernels (M > 82) need k_feature's compact QR factors
 bool feature_needs_compact(int maxM);
 bool kalman_chol_supported(int Cmax);

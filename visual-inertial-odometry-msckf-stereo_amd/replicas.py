@@ -5,8 +5,13 @@ few hundred KB and every stage of its update is a chain of small dependent
 factorisations, so there is no data-parallel exchange to make.  N GPUs run N
 independent batches of filters, one process per GPU.  The ranks exchange only
 control: the start / stop barriers of the timed region and the max (or sum)
-of a float.  No collective touches the data path, so none is on a GPU: the
-control messages travel over a host TCP hub (stdlib sockets, no PyTorch).
+of a float.  No collective touches the data path.  On GPUs the control
+messages travel over RCCL (xGMI between the node's GPUs; include/
+msckf_replicas.h, librccl opened at run time, no PyTorch): ``attach_rccl``
+makes one communicator per rank, its unique id handed out over a host TCP
+hub (stdlib sockets) that also carries everything when there is no GPU (the
+--stub tests) or when RCCL cannot be brought up (then every rank falls back
+together and the bench line says why).
 
 Launch modes (both one process per GPU, RANK / LOCAL_RANK / WORLD_SIZE in the
 environment):
@@ -102,6 +107,65 @@ class Hub:
             self.srv.close()
 
 
+class RcclComm:
+    """One RCCL communicator of this rank (msckf_rccl_*, include/
+    msckf_replicas.h): all-reduce of doubles (sum / max, a barrier when the
+    caller needs one) and all-gather of bytes, on the device the rank runs on."""
+
+    def __init__(self, uid: bytes, world: int, rank: int, device: int, timeout_s: float = 60.0):
+        import ctypes as C
+        from . import _lib
+        self._C, self._L = C, _lib.load_library()
+        self.world, self.rank = world, rank
+        h = C.c_void_p()
+        buf = (C.c_uint8 * _lib.RCCL_ID_BYTES).from_buffer_copy(uid)
+        rc = self._L.msckf_rccl_init(buf, world, rank, device, timeout_s, C.byref(h))
+        if rc != 0:
+            raise RuntimeError("msckf_rccl_init: %s (rc=%d)" % (self._L.msckf_rccl_last_error().decode(), rc))
+        self._h = h
+
+    @staticmethod
+    def unique_id() -> bytes:
+        import ctypes as C
+        from . import _lib
+        L = _lib.load_library()
+        buf = (C.c_uint8 * _lib.RCCL_ID_BYTES)()
+        rc = L.msckf_rccl_unique_id(buf)
+        if rc != 0:
+            raise RuntimeError("msckf_rccl_unique_id: %s (rc=%d)" % (L.msckf_rccl_last_error().decode(), rc))
+        return bytes(buf)
+
+    def _check(self, rc, what):
+        if rc != 0:
+            raise RuntimeError("%s: %s (rc=%d)" % (what, self._L.msckf_rccl_last_error().decode(), rc))
+
+    def allreduce(self, x: float, op: str) -> float:
+        C = self._C
+        v = (C.c_double * 1)(float(x))
+        self._check(self._L.msckf_rccl_allreduce(self._h, v, 1, 1 if op == "max" else 0), "msckf_rccl_allreduce")
+        return float(v[0])
+
+    def allgather_bytes(self, b: bytes) -> List[bytes]:
+        C = self._C
+        n = len(b)
+        src = C.create_string_buffer(b, n)
+        dst = C.create_string_buffer(n * self.world)
+        self._check(self._L.msckf_rccl_allgather(self._h, src, n, dst), "msckf_rccl_allgather")
+        raw = dst.raw
+        return [raw[k * n:(k + 1) * n] for k in range(self.world)]
+
+    def count(self):
+        C = self._C
+        n, r = C.c_int32(), C.c_int32()
+        self._check(self._L.msckf_rccl_count(self._h, C.byref(n), C.byref(r)), "msckf_rccl_count")
+        return n.value, r.value
+
+    def close(self):
+        if self._h is not None:
+            self._L.msckf_rccl_destroy(self._h)
+            self._h = None
+
+
 @dataclass
 class ReplicaGroup:
     rank: int
@@ -111,12 +175,59 @@ class ReplicaGroup:
     _lines: Optional[_Lines] = None
     _hub: Optional[Hub] = None
     _rdzv: Optional[str] = None
+    _rccl: Optional[RcclComm] = None
+    transport: str = "none (one rank)"
 
-    def _call(self, op, v=0.0):
+    def _hub_call(self, op, v=0.0):
         if self._sock is None:
             return float(v)
         _send(self._sock, {"op": op, "v": float(v)})
         return float(self._lines.read()["v"])
+
+    def _hub_gather(self, obj):
+        if self._sock is None:
+            return [obj]
+        _send(self._sock, {"op": "gather", "v": obj})
+        return list(self._lines.read()["v"])
+
+    def _call(self, op, v=0.0):
+        if self._rccl is not None:
+            return self._rccl.allreduce(v, "max" if op == "max" else "sum")
+        return self._hub_call(op, v)
+
+    def attach_rccl(self, device: int, timeout_s: float = 60.0) -> dict:
+        """Brings up RCCL on ``device`` for this group's collectives (the
+        north star's multi-GPU transport).  Rank 0 makes the unique id and
+        hands it out over the hub; every rank then reports over the hub
+        whether its communicator came up, and unless all did, all of them stay
+        on the hub.  Returns the transport record for the bench line: the
+        transport used and each rank's ncclCommCount (or the reason)."""
+        uid, err = None, None
+        if self.rank == 0:
+            try:
+                uid = RcclComm.unique_id().hex()
+            except Exception as e:   # noqa: BLE001 -- reported, then the hub carries on
+                err = str(e)
+        uid = self._hub_gather(uid)[0]
+        comm = None
+        if uid is not None:
+            try:
+                comm = RcclComm(bytes.fromhex(uid), self.world, self.rank, device, timeout_s)
+            except Exception as e:   # noqa: BLE001
+                err = str(e)
+        oks = self._hub_gather(comm is not None)
+        errs = self._hub_gather(err)
+        if not all(oks):
+            if comm is not None:
+                comm.close()
+            self.transport = "tcp-hub (rccl unavailable: %s)" % next(e for e in errs if e)
+            return {"transport": self.transport}
+        self._rccl = comm
+        self.transport = "rccl"
+        counts = [json.loads(b.rstrip(b"\0").decode()) for b in
+                  self._rccl.allgather_bytes(json.dumps(list(comm.count())).encode().ljust(32, b"\0"))]
+        return {"transport": "rccl", "rccl_comm_count": [c[0] for c in counts],
+                "rccl_ranks": [c[1] for c in counts]}
 
     def barrier(self):
         self._call("barrier")
@@ -132,14 +243,18 @@ class ReplicaGroup:
     def all_gather(self, obj):
         """Every rank's JSON-serialisable ``obj``, in rank order (control
         data only: e.g. the device each replica ran on)."""
-        if self._sock is None:
-            return [obj]
-        _send(self._sock, {"op": "gather", "v": obj})
-        return list(self._lines.read()["v"])
+        if self._rccl is not None:
+            b = json.dumps(obj).encode()
+            n = int(self._rccl.allreduce(len(b), "max"))
+            return [json.loads(x.rstrip(b"\0").decode()) for x in self._rccl.allgather_bytes(b.ljust(n, b"\0"))]
+        return self._hub_gather(obj)
 
     def close(self):
+        if self._rccl is not None:
+            self._rccl.close()
+            self._rccl = None
         if self._sock is not None:
-            self._call("close")
+            self._hub_call("close")
             self._sock.close()
             self._sock = None
         if self._hub is not None:
