@@ -147,3 +147,28 @@ def test_image_processor_synthetic_stereo():
             assert np.median(np.abs(mv - step)) < 0.05, np.median(np.abs(mv - step))
         prev = feats
     assert ip.num_features["after_tracking"] > 0
+
+
+@pytest.mark.parametrize("name", ["rectified", "euroc"])
+def test_image_processor_vs_reference(name):
+    """The GPU front-end against the reference's own ImageProcessor
+    (tests/golden/frontend_ref.npz, tools/gen_frontend_golden.py: image.py run
+    in the build container on the oracle operators).  The bookkeeping is
+    checked exactly on CPU (tests/test_frontend_ref.py); here the HIP
+    operators run under it: every frame's published ids identical, in order,
+    and the cam0 / cam1 coordinates within 1e-4 px (normalised coordinates x
+    the focal length)."""
+    from conftest import golden
+    from frontend_ref_scenes import scene_config, run_scene, reference_frames
+    g = golden("frontend_ref")
+    ip = fe_mod.ImageProcessor(scene_config(g, name))
+    got = run_scene(ip, g, name)
+    fx = np.array([g[name + "_intrinsics"][0], g[name + "_intrinsics"][1],
+                   g[name + "_intrinsics1"][0], g[name + "_intrinsics1"][1]])
+    worst = 0.0
+    for k, ((ids, uv), (rids, ruv)) in enumerate(zip(got, reference_frames(g, name))):
+        np.testing.assert_array_equal(ids, rids, err_msg="frame %d" % k)
+        err = np.abs(uv - ruv) * fx
+        worst = max(worst, float(err.max()) if err.size else 0.0)
+        assert err.max() <= 1e-4, (k, err.max())
+    print("%s: %d frames, ids identical, worst coordinate deviation %.2e px" % (name, len(got), worst))

@@ -484,11 +484,19 @@ class ImageProcessor:
 
     def undistort_points(self, pts_in, intrinsics, distortion_model, distortion_coeffs,
                          rectification_matrix=np.identity(3), new_intrinsics=np.array([1, 1, 0, 0])):
-        """image.py:640-674 (cv2.undistortPoints / cv2.fisheye.undistortPoints)."""
+        """image.py:640-674 (cv2.undistortPoints / cv2.fisheye.undistortPoints).
+        Quirk kept: for 'equidistant' the reference passes its rectification
+        matrix in cv2.fisheye.undistortPoints' output slot and K_new in its R
+        slot (image.py:669-670, positional arguments), so cv2 rotates by K_new
+        and returns normalised points; the rectification is never applied."""
         if len(pts_in) == 0:
             return np.zeros((0, 2))
-        return self.fe.undistort(pts_in, intrinsics, _model(distortion_model), distortion_coeffs,
-                                 rectification_matrix, new_intrinsics)
+        model = _model(distortion_model)
+        if model == EQUIDISTANT:
+            n = np.asarray(new_intrinsics, float)
+            K_new = np.array([[n[0], 0.0, n[2]], [0.0, n[1], n[3]], [0.0, 0.0, 1.0]])
+            return self.fe.undistort(pts_in, intrinsics, model, distortion_coeffs, K_new, np.array([1.0, 1.0, 0.0, 0.0]))
+        return self.fe.undistort(pts_in, intrinsics, model, distortion_coeffs, rectification_matrix, new_intrinsics)
 
     def distort_points(self, pts_in, intrinsics, distortion_model, distortion_coeffs):
         """image.py:676-702 (cv2.projectPoints / cv2.fisheye.distortPoints)."""
