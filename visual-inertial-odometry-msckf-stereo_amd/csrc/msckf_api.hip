@@ -240,6 +240,7 @@ UpdWs<T> upd_ws(msckf_ctx* c) {
     w.W = reinterpret_cast<KT*>(c->W.p);
     w.Wk = reinterpret_cast<KT*>(c->Wk.p);
     w.wk_stride = kalman_global_ws_doubles(c->Cmax);
+    w.s2 = (double)(T)c->cfg.observation_noise;
     return w;
 }
 
@@ -513,7 +514,9 @@ int load_features(msckf_ctx* c, int nf, const int32_t* feat_off, int single_filt
 #else
     c->gram = true;   // experiment builds: force the record path
 #endif
-    if (c->gram) HIPC(c->obs_g.ensure(((size_t)nobs + 1) * OBG_STRIDE * sizeof(double)));
+    // (allocated in either case: k_feature writes the records of ill-conditioned
+    // features for the fused assembly too -- FQR_FLAG)
+    HIPC(c->obs_g.ensure(((size_t)nobs + 1) * OBG_STRIDE * sizeof(double)));
     c->h_feat_off = h_off;
     return 0;
 }
@@ -1242,11 +1245,12 @@ int msckf_kernel_times(msckf_ctx_t* c, int max_k, double* ms_total, int32_t* lau
 }
 
 // Debug (not in include/msckf_hip.h): copy the first `count` doubles of a
-// Kalman workspace buffer (0 Lc, 1 Vi, 2 Sii, 3 G, 4 Tm, 5 W) to the host.
+// Kalman workspace buffer (0 Lc, 1 Vi, 2 Sii, 3 G, 4 Tm, 5 W, 6 H_thin [A | b], 7 afail (ints)) to the host.
 int msckf_debug_workspace(msckf_ctx_t* c, int which, double* out, size_t count) {
     if (!c || !out) FAIL(-1, "null argument");
     const void* src = which == 0 ? c->Lc.p : which == 1 ? c->Vi.p : which == 2 ? c->Sii.p
-                    : which == 3 ? c->G.p : which == 4 ? c->Tm.p : which == 5 ? c->W.p : nullptr;
+                    : which == 3 ? c->G.p : which == 4 ? c->Tm.p : which == 5 ? c->W.p
+                    : which == 6 ? (const void*)c->Hthin.p : which == 7 ? (const void*)c->afail.p : nullptr;
     if (!src) FAIL(-1, "unknown workspace %d", which);
     HIPSYNC(c, hipStreamSynchronize(c->stream));
     HIPC(hipMemcpy(out, src, count * sizeof(double), hipMemcpyDeviceToHost));

@@ -53,7 +53,8 @@ constexpr int OBG_G = 0, OBG_DS = 18, OBG_UB = 39, OBG_CAM = 45, OBG_STRIDE = 46
 // so that the fused information assembly (k_info_fused) rebuilds an
 // observation's G_i = (Q^T Hx)[0:3, cam i] = X^T H_f,i^T Hx_i from its own
 // Jacobian blocks instead of reading obs_g.
-constexpr int FQR_X = 0, FQR_G = 6, FQR_STRIDE = 10;
+constexpr int FQR_X = 0, FQR_G = 6, FQR_FLAG = 9, FQR_STRIDE = 10;
+constexpr double FQR_RMAX = 1e3, FQR_KAPPA = 1e4;   // FQR_FLAG: Gram records written (k_feature)
 
 template <typename T>
 struct Params {
@@ -123,6 +124,7 @@ struct UpdWs {
     int* afail;  // [B]                  stage A status (1: P_cc not PD), written by every k_kal_a run
     size_t wk_stride;
     int Cp;
+    double s2;   // observation noise variance in the context's type, as Params::sigma2: T >= s2 I
 };
 
 // ------------------------------------------------------------ device math --

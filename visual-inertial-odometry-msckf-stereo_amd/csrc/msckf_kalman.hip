@@ -55,13 +55,14 @@ __device__ double pcc_pivot_floor(const T* P, int ld, int C, double* lds) {
 }
 
 // ---- stage A: [P_cc P_ci; P_ic P_ii] in index space [cams (Cp) | IMU (24)] ----
-template <typename T, int NT, int TPL>
+template <typename T, int NT, int TPL, bool RETRY = false>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 ? 2 : 1))) k_kal_a(DevState<T> st, UpdWs<T> ws) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     // launched before k_select (side stream): every filter is factored, the
     // status goes to afail only, and k_kal_c1 turns it into info[3] for the
     // filters that do update
     const int b = blockIdx.x;
+    if (RETRY && ws.afail[b] == 0) return;   // factored on the first attempt
     const int C = 6 * st.ncams[b], Cp = round4(C);
     const int nrow = (Cp + KW) / 4;
     const T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
@@ -70,10 +71,11 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 2
     KT* Vi = ws.Vi + (size_t)b * KW * Cpw;
     KT* Sii = ws.Sii + (size_t)b * KW * KW;
     auto map = [&](int i) { return i < C ? 21 + i : (i < Cp ? -1 : (i < Cp + 21 ? i - Cp : -1)); };
+    double shift = 0.0;   // retries: P_cc + shift I (see below)
     auto load = [&](int i, int j) -> double {
         const int mi = map(i), mj = map(j);
         if (mi < 0 || mj < 0) return i == j ? 1.0 : 0.0;
-        return (double)P[(size_t)mi * ld + mj];
+        return (double)P[(size_t)mi * ld + mj] + (i == j && i < C ? shift : 0.0);
     };
     auto panel = [&](int r, int c0, double w0, double w1, double w2, double w3) {
         KT* dst = r < Cp ? Lc + (size_t)r * Cpw + c0 : Vi + (size_t)(r - Cp) * Cpw + c0;
@@ -81,8 +83,25 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 2
     };
     auto trail = [&](int i, int j, double v) { Sii[(i - Cp) * KW + (j - Cp)] = v; };
     const double floor = pcc_pivot_floor(P, ld, C, reinterpret_cast<double*>(smem_raw));
-    const bool ok = rchol_core<NT, TPL>(nrow, nrow, Cp / 4, reinterpret_cast<double*>(smem_raw), load, panel, trail,
-                                        floor);
+    // A P_cc that the reference's update (msckf.py:598-604) left indefinite at
+    // rounding level can still defeat the pivot floor: a floored pivot whose
+    // column is not small makes the following pivots large and negative (golden
+    // stream s4 after its degenerate frame-3 update: smallest eigenvalue
+    // -4e-9 x the largest variance, pivots -> -inf).  Such a filter is factored
+    // again as P_cc + shift I, shift = 1e-8 then 1e-6 x the largest cam variance
+    // (the update moves by about that much; a PD P_cc never gets here); a P_cc
+    // that fails even then (a clearly negative eigenvalue, NaN) fails with -3.
+    // The retries run in a second launch (RETRY: only the filters whose first
+    // attempt failed do any work), so the first attempt's register allocation is
+    // the one-shot kernel's.
+    bool ok = false;
+    for (int att = RETRY ? 1 : 0; att < (RETRY ? 3 : 1) && !ok; ++att) {
+        if (att > 0) {
+            shift = (att == 1 ? 1e-8 : 1e-6) * (floor / KALMAN_PIVOT_FLOOR);
+            __syncthreads();   // the previous attempt's LDS panel reads are done
+        }
+        ok = rchol_core<NT, TPL>(nrow, nrow, Cp / 4, reinterpret_cast<double*>(smem_raw), load, panel, trail, floor);
+    }
     if (threadIdx.x == 0) ws.afail[b] = ok ? 0 : 1;   // read by k_kal_c1
 }
 
@@ -125,7 +144,14 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 2
             if (c0 + q < C && c0 + q <= r) dst[c0 + q] = w[q];
     };
     auto trail = [](int, int, double) {};
-    const bool ok = rchol_core<NT, TPL>(nTc, nTc, nTc, reinterpret_cast<double*>(smem_raw), load, panel, trail);
+    // T = s2 I + Lc^T A Lc >= s2 I, so every exact pivot is >= s2; rounding in a
+    // numerically degenerate A (a landmark millimetres from the camera: entries
+    // ~1e9, cond(T) beyond 1/eps) can still push computed pivots below it.  They
+    // are floored at s2 instead of failing the filter -- the reference's LU solve
+    // (msckf.py:560-563) returns its own rounding noise there, without an error.
+    // A NaN pivot still fails.
+    const bool ok = rchol_core<NT, TPL>(nTc, nTc, nTc, reinterpret_cast<double*>(smem_raw), load, panel, trail, ws.s2,
+                                        -INFINITY);
     if (!ok && threadIdx.x == 0) ws.info[4 * b + 3] = -1;
 }
 
@@ -312,18 +338,19 @@ __global__ void __launch_bounds__(64) k_gchol_diag(DevState<T> st, UpdWs<T> ws, 
         const int i = e / nb, j = e - i * nb;
         d[i][j] = j <= i ? A[(size_t)(k + i) * ld + k + j] : 0.0;
     }
-    // stage A: pivots floored as in k_kal_a (pcc_pivot_floor)
-    double floor = 0.0;
+    // stage A: pivots floored as in k_kal_a (pcc_pivot_floor); stage C: at s2 (k_kal_c1)
+    double floor = STAGE == 0 ? 0.0 : ws.s2, lo = -INFINITY;
     if (STAGE == 0) {
         const T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
         for (int i = lane; i < nelim; i += 64) floor = fmax(floor, (double)P[(size_t)(21 + i) * st.Dmax + 21 + i]);
         floor = wave_max(floor) * KALMAN_PIVOT_FLOOR;
+        lo = -PIVOT_FLOOR_NEG * floor;
     }
     __syncthreads();
     bool bad = false;
     for (int j = 0; j < nb; ++j) {   // right-looking, lane i owns row i
         double piv = d[j][j];
-        piv = pivot_floored(piv, floor);
+        piv = pivot_floored(piv, floor, lo);
         if (!(piv > 0.0)) { bad = true; break; }
         const double l = sqrt(piv), inv = 1.0 / l;
         __syncthreads();
@@ -904,6 +931,8 @@ static bool pick_rchol(int tiles, RcholCfg& c) {
 template <typename T, int NT, int TPL>
 static void launch_a_cfg(hipStream_t s, const DevState<T>& st, const UpdWs<T>& ws, size_t lds) {
     hipLaunchKernelGGL((k_kal_a<T, NT, TPL>), dim3(st.B), dim3(NT), lds, s, st, ws);
+    // near-singular P_cc: the shifted retries (only failed filters do work)
+    hipLaunchKernelGGL((k_kal_a<T, NT, TPL, true>), dim3(st.B), dim3(NT), lds, s, st, ws);
 }
 
 // Host side of the blocked global-memory factorisation (large windows).

@@ -1069,9 +1069,8 @@ __global__ void __launch_bounds__(256, OPL == 1 ? 3 : 1) k_feature(DevState<T> s
             store_pairs(wsr + OBS_HT, Ht, 18);
             store_pairs(wsr + OBS_RT, rt4, 4);
         }
-        if constexpr (GRAM)
-            for (int c = 0; c < 6; ++c)   // Hx_i^T r_i, before r is reflected
-                u6[s][c] = Hx[s][c] * r[s][0] + Hx[s][6 + c] * r[s][1] + Hx[s][12 + c] * r[s][2] + Hx[s][18 + c] * r[s][3];
+        for (int c = 0; c < 6; ++c)   // Hx_i^T r_i, before r is reflected
+            u6[s][c] = Hx[s][c] * r[s][0] + Hx[s][6 + c] * r[s][1] + Hx[s][12 + c] * r[s][2] + Hx[s][18 + c] * r[s][3];
         if (own && fb.compact) store_pairs(fb.obs_ws + (size_t)(o0 + i) * OBS_WS + OBS_R, r[s], 4);
     }
     // ---- Householder QR of H_f across the segment (rows 4i..4i+3 with observation i) ----
@@ -1126,6 +1125,16 @@ __global__ void __launch_bounds__(256, OPL == 1 ? 3 : 1) k_feature(DevState<T> s
     // ---- per-feature QR record: X = R^-1 and g = (Q^T r)[0:3] (the segment's
     // first lane holds observation 0, i.e. rows 0..2 of the reflected H_f and r).
     // A zero pivot (rank-deficient H_f) drops its direction instead of dividing.
+    // Ill-conditioned features (|R| > FQR_RMAX -- a landmark millimetres from
+    // the camera -- or cond(R) > FQR_KAPPA) are flagged: k_info_fused's rebuild
+    // G_i = X^T H_f,i^T Hx_i loses about eps cond(R)^2 of A's positive
+    // semidefiniteness, which the Kalman stage cannot absorb there, so this
+    // kernel writes their Householder Gram records (as the record path does)
+    // and the fused assembly reads those instead.  (R's diagonal is the same in
+    // every lane of the segment: the flag is segment-uniform.)
+    const CT rmax = fmax(fabs(rd[0]), fmax(fabs(rd[1]), fabs(rd[2])));
+    const CT rmin = fmin(fabs(rd[0]), fmin(fabs(rd[1]), fabs(rd[2])));
+    const bool ill = !(rmax <= CT(FQR_RMAX)) || !(rmax <= CT(FQR_KAPPA) * rmin);
     if (l == 0 && M > 0) {
         const CT r01 = Hf[0][1], r02 = Hf[0][2], r12 = Hf[0][5];
         const CT x00 = rd[0] != CT(0) ? 1 / rd[0] : CT(0), x11 = rd[1] != CT(0) ? 1 / rd[1] : CT(0);
@@ -1138,12 +1147,11 @@ __global__ void __launch_bounds__(256, OPL == 1 ? 3 : 1) k_feature(DevState<T> s
         q[FQR_X + 4] = -r12 * x11 * x22;
         q[FQR_X + 5] = x22;
         for (int t = 0; t < 3; ++t) q[FQR_G + t] = r[0][t];
-        q[9] = 0;
+        q[FQR_FLAG] = ill ? CT(1) : CT(0);
         store_pairs(fb.fqr + (size_t)f * FQR_STRIDE, q, FQR_STRIDE);
     }
-    if constexpr (!GRAM) {
-        if (!fb.compact) return;
-    }
+    const bool gram = GRAM || ill;
+    if (!gram && !fb.compact) return;   // segment-uniform
     // ---- w_j = v_j^T X_{j-1}: 6 columns per observation, local to the lane ----
     CT d10 = 0, d20 = 0, d21 = 0;
 #pragma unroll
@@ -1185,7 +1193,7 @@ __global__ void __launch_bounds__(256, OPL == 1 ? 3 : 1) k_feature(DevState<T> s
             if (i == 0)
                 for (int j = 0; j < 3; ++j) fb.tau[4 * f + j] = (T)tau[j];
         }
-        if constexpr (!GRAM) continue;
+        if (!gram) continue;
         // Gram terms.  (Q^T Hx)[t][i-block] = [i == 0] Hx_0[t] - sum_j tau_j V_0[t][j] W_j(i)
         CT rec[OBG_STRIDE];   // G | DS | UB | pad, stored as 16-byte pairs
         for (int t = 0; t < 3; ++t)
@@ -2586,25 +2594,58 @@ __global__ void __launch_bounds__(64 * NW) k_info_fused(DevState<T> st, Params<T
         tacc[q] = v4d{0.0, 0.0, 0.0, 0.0};
     }
     const int grp = tid / IF_NP, ps = (tid % IF_NP) >> 5, pc = tid & 31;
-    // build chunk [l0, l0 + KF) into row buffer bb (producer thread (ps, pc))
-    auto produce = [&](int l0, int bb) {
+    // Producer thread (ps, pc) of chunk [l0, l0 + KF): feature ps's observation of
+    // cam pc.  pload issues its global loads (kept raw in registers: a conversion
+    // here would wait for them), pbuild forms the rows one MFMA phase later.
+    struct PIn {
+        int o, og;   // observation of cam pc in the feature (0xff: none), its global index
+        T pw[3], z[4];
+        double x[6], gr[3], ill;   // ill != 0: read the feature's Gram records (k_feature, FQR_FLAG)
+    };
+    auto pload = [&](int l0, PIn& in) {
+        const int li = l0 + ps;
+        const int f = (li < nl && pc < nc) ? flist[li] : -1;
+        in.o = f >= 0 ? (int)posb[32 * f + pc] : 0xff;
+        if (in.o == 0xff) return;
+        const int fg = fbeg + f, og = fo0[f] + in.o;
+        in.og = og;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) in.pw[k] = fb.p_w[3 * fg + k];
+        const T* zp = fb.obs_z + (size_t)og * 4;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) in.z[k] = zp[k];
+        const double* qr = fb.fqr + (size_t)fg * FQR_STRIDE;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) in.x[k] = qr[FQR_X + k];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) in.gr[k] = qr[FQR_G + k];
+        in.ill = qr[FQR_FLAG];
+    };
+    auto pbuild = [&](const PIn& in, int bb) {
         if (pc >= nc) return;
         double* dst = buf + (size_t)bb * IF_KR * IM_GS + 3 * ps * IM_GS + 6 * pc;
-        const int li = l0 + ps;
-        const int f = li < nl ? flist[li] : -1;
-        const int o = f >= 0 ? (int)posb[32 * f + pc] : 0xff;
-        if (o == 0xff) {
+        if (in.o == 0xff) {
 #pragma unroll
             for (int t = 0; t < 3; ++t)
 #pragma unroll
                 for (int u = 0; u < 6; ++u) dst[t * IM_GS + u] = 0.0;
             return;
         }
-        const int fg = fbeg + f, og = fo0[f] + o;
-        const double pw[3] = {(double)fb.p_w[3 * fg], (double)fb.p_w[3 * fg + 1], (double)fb.p_w[3 * fg + 2]};
-        const T* zp = fb.obs_z + (size_t)og * 4;
-        const double z0 = (double)zp[0], z1 = (double)zp[1], z2 = (double)zp[2], z3 = (double)zp[3];
-        const double* qr = fb.fqr + (size_t)fg * FQR_STRIDE;
+        if (in.ill != 0.0) {   // ill-conditioned feature: its Householder Gram record (rare)
+            const double* rec = fb.obs_g + (size_t)in.og * OBG_STRIDE;
+            double* ac = acc + (ps * 32 + pc) * IF_ACC;
+#pragma unroll
+            for (int t = 0; t < 3; ++t)
+#pragma unroll
+                for (int u = 0; u < 6; ++u) dst[t * IM_GS + u] = rec[OBG_G + 6 * t + u];
+#pragma unroll
+            for (int e = 0; e < 21; ++e) ac[e] += rec[OBG_DS + e];
+#pragma unroll
+            for (int x = 0; x < 6; ++x) ac[21 + x] += rec[OBG_UB + x];
+            return;
+        }
+        const double pw[3] = {(double)in.pw[0], (double)in.pw[1], (double)in.pw[2]};
+        const double z0 = (double)in.z[0], z1 = (double)in.z[1], z2 = (double)in.z[2], z3 = (double)in.z[3];
         const double* cg = camg + pc * IF_CG;
         double d0[3], d1[3], pc0[3], pc1[3];
 #pragma unroll
@@ -2674,8 +2715,8 @@ __global__ void __launch_bounds__(64 * NW) k_info_fused(DevState<T> st, Params<T
             H[2][m] = l22 * H[2][m];
         }
         // G_i = X^T (F^T H^), F = -H^[:, 3:6]; rows written as soon as formed
-        const double x00 = qr[FQR_X], x01 = qr[FQR_X + 1], x02 = qr[FQR_X + 2];
-        const double x11 = qr[FQR_X + 3], x12 = qr[FQR_X + 4], x22 = qr[FQR_X + 5];
+        const double x00 = in.x[0], x01 = in.x[1], x02 = in.x[2];
+        const double x11 = in.x[3], x12 = in.x[4], x22 = in.x[5];
         double K[3][6];
 #pragma unroll
         for (int j = 0; j < 3; ++j)
@@ -2692,7 +2733,7 @@ __global__ void __launch_bounds__(64 * NW) k_info_fused(DevState<T> st, Params<T
 #pragma unroll
             for (int m = 0; m < 6; ++m) dst[t * IM_GS + m] = K[t][m];
         // Hx^T Hx (packed lower, as OBG_DS) and UB = Hx^T r - G^T g, into slot (ps, pc)
-        const double gr0 = qr[FQR_G], gr1 = qr[FQR_G + 1], gr2 = qr[FQR_G + 2];
+        const double gr0 = in.gr[0], gr1 = in.gr[1], gr2 = in.gr[2];
         double* ac = acc + (ps * 32 + pc) * IF_ACC;
 #pragma unroll
         for (int x = 0, e = 0; x < 6; ++x)
@@ -2702,25 +2743,49 @@ __global__ void __launch_bounds__(64 * NW) k_info_fused(DevState<T> st, Params<T
         for (int x = 0; x < 6; ++x)
             ac[21 + x] += (H[0][x] * h0 + H[1][x] * h1 + H[2][x] * h2) - (K[0][x] * gr0 + K[1][x] * gr1 + K[2][x] * gr2);
     };
-    if (nl > 0 && grp == 0) produce(0, 0);
+    if (nl > 0 && grp == 0) {
+        PIn in;
+        pload(0, in);
+        pbuild(in, 0);
+    }
     __syncthreads();
     for (int l0 = 0, it = 0; l0 < nl; l0 += IF_KF, ++it) {
         const int cur = it & 1;
-        // ---- rank-KR update of this wave's tiles from chunk it ----
+        // ---- the next chunk's inputs, by the group whose turn it is: loads in
+        // flight under this chunk's MFMAs ----
+        const bool mine = l0 + IF_KF < nl && grp == (it + 1) % NG;
+        PIn in;
+        if (mine) pload(l0 + IF_KF, in);
+        // ---- rank-KR update of this wave's tiles from chunk it: each k-step's
+        // operands are read before its MFMAs (one LDS wait per k-step) ----
         const double* cb = buf + (size_t)cur * IF_KR * IM_GS;
+        unsigned kmv[IF_NKS];
 #pragma unroll
         for (int ks = 0; ks < IF_NKS; ++ks) {
             const int sa = l0 + (4 * ks) / 3, sb = l0 + (4 * ks + 3) / 3;
-            unsigned km = (sa < nl ? ftm[sa] : 0u) | (sb < nl ? ftm[sb] : 0u);
-            km = __builtin_amdgcn_readfirstlane(km);
-            const double* brow = cb + (4 * ks + lr) * IM_GS + lc;
-#pragma unroll
-            for (int q = 0; q < PPW; ++q)
-                if (pv[q] && ((km >> pti[q]) & (km >> ptj[q]) & 1u))
-                    tacc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(brow[16 * pti[q]], brow[16 * ptj[q]], tacc[q], 0, 0, 0);
+            kmv[ks] = (sa < nl ? ftm[sa] : 0u) | (sb < nl ? ftm[sb] : 0u);
         }
-        // ---- the next chunk, by the group whose turn it is ----
-        if (l0 + IF_KF < nl && grp == (it + 1) % NG) produce(l0 + IF_KF, cur ^ 1);
+#pragma unroll
+        for (int ks = 0; ks < IF_NKS; ++ks) {
+            const unsigned km = __builtin_amdgcn_readfirstlane(kmv[ks]);
+            const double* brow = cb + (4 * ks + lr) * IM_GS + lc;
+            constexpr int HQ = (PPW + 1) / 2;   // operands read half a tile list at a time (VGPRs)
+#pragma unroll
+            for (int h = 0; h < PPW; h += HQ) {
+                double oa[HQ], ob[HQ];
+#pragma unroll
+                for (int q = 0; q < HQ; ++q) {
+                    oa[q] = h + q < PPW ? brow[16 * pti[h + q < PPW ? h + q : 0]] : 0.0;
+                    ob[q] = h + q < PPW ? brow[16 * ptj[h + q < PPW ? h + q : 0]] : 0.0;
+                }
+#pragma unroll
+                for (int q = 0; q < HQ; ++q)
+                    if (h + q < PPW && pv[h + q] && ((km >> pti[h + q]) & (km >> ptj[h + q]) & 1u))
+                        tacc[h + q] = __builtin_amdgcn_mfma_f64_16x16x4f64(oa[q], ob[q], tacc[h + q], 0, 0, 0);
+            }
+        }
+        // ---- build the next chunk ----
+        if (mine) pbuild(in, cur ^ 1);
         __syncthreads();
     }
     KT* F = ws.Hthin + (size_t)b * Cmax * (Cmax + 1);

@@ -32,8 +32,12 @@ namespace msckf {
 // not rounding: it still fails the factorisation.
 // ===========================================================================
 constexpr double PIVOT_FLOOR_NEG = 1e4;   // x floor: the deepest negative pivot still floored
+// lo: the lowest pivot still floored (default -PIVOT_FLOOR_NEG x floor); NaN is never floored
+__device__ __forceinline__ double pivot_floored(double x, double floor, double lo) {
+    return (floor > 0.0 && x < floor && x >= lo) ? floor : x;
+}
 __device__ __forceinline__ double pivot_floored(double x, double floor) {
-    return (floor > 0.0 && x < floor && x >= -PIVOT_FLOOR_NEG * floor) ? floor : x;
+    return pivot_floored(x, floor, -PIVOT_FLOOR_NEG * floor);
 }
 constexpr int RB = 18;   // doubles per 4-row block of the LDS column buffer
 
@@ -41,8 +45,10 @@ constexpr int RB = 18;   // doubles per 4-row block of the LDS column buffer
 // instead of being called per element (lets a loader share operands).
 template <int NT, int TPL, class Load, class Panel, class Trail, bool TILE_LOAD = false>
 __device__ __forceinline__ bool rchol_core(int nrow, int ncol, int nelim, double* lds, Load load, Panel panel,
-                                           Trail trail, double floor = 0.0) {
-    auto fl = [floor](double x) { return pivot_floored(x, floor); };
+                                           Trail trail, double floor = 0.0, double floor_lo = 1.0) {
+    // floor_lo > 0 (default): pivots down to -PIVOT_FLOOR_NEG x floor are floored
+    const double lo = floor_lo > 0.0 ? -PIVOT_FLOOR_NEG * floor : floor_lo;
+    auto fl = [floor, lo](double x) { return pivot_floored(x, floor, lo); };
     const int tid = threadIdx.x;
     const int ntiles = ncol * nrow - ncol * (ncol - 1) / 2;
     int crd[TPL], tlmax[TPL];
