@@ -19,6 +19,7 @@
 //                                                                      k_correct
 //   P compaction msckf.py:803-818                                   -> k_prune_*
 #include <type_traits>
+#include <utility>
 
 #include "msckf_common.h"
 #include "msckf_launch.h"
@@ -2483,29 +2484,169 @@ __global__ void __launch_bounds__(64 * IM_NW) k_info_mfma(DevState<T> st, FeatBa
 // -- the rank-3 form of the gate's records, in fp64.  The update is invariant
 // to the orthogonal row maps involved (quirk Q4).
 //
-// Pipeline: IF_KF features per chunk; thread (s, c) of the chunk's producer
-// group (IF_KF x 32 threads) builds feature s's observation of cam c into the
-// chunk's LDS rows of Gall (zeros if the feature does not see cam c) and adds
-// its Hx^T Hx / UB terms into the (s, c) slot of an LDS accumulator (summed
-// over s at the end).  Chunk i + 1 is built by one producer group while every
-// wave runs chunk i's MFMAs (double-buffered rows, one barrier per chunk);
-// the groups take turns, so the VALU work is spread over all waves.
+// Pipeline: IF_KF features per chunk; producer thread (s, c) (waves 0..3,
+// IF_KF x 32 threads) builds feature s's observation of cam c into the chunk's
+// LDS rows of Gall (zeros if the feature does not see cam c) and adds its
+// Hx^T Hx / UB terms into the (s, c) slot of an LDS accumulator (summed over
+// s at the end).  The producers build chunk i + 1 (its global inputs loaded
+// one iteration earlier) while the four tile-owning waves run chunk i's
+// MFMAs (double-buffered rows, one barrier per chunk).  Producers and tile
+// owners run separate code paths, so neither carries the other's registers:
+// the producer's fp64 chain beside 20 accumulator tiles per owner wave.
 // ---------------------------------------------------------------------------
 constexpr int IF_KF = 8, IF_KR = 3 * IF_KF, IF_NKS = IF_KR / 4, IF_NP = 32 * IF_KF;
 constexpr int IF_ACC = 27, IF_CG = 27;   // doubles per accumulator slot / per cam geometry record
-constexpr int IF_NW = 8;                 // waves per workgroup (two per SIMD: 256 VGPRs for tiles + producer)
+constexpr int IF_NPW = IF_NP / 64;       // producer waves
+// Phase timing (probe builds, -DMSCKF_GATE_PROBE; tools/probes/info_phases.py):
+// s_memtime sums of one producer and one tile-owner wave per filter --
+// [0] prologue, [1] producer load issue, [2] producer build, [3] producer
+// barrier wait, [4] owner MFMA phase, [5] owner barrier wait, [6] iterations,
+// [7] filters.
+#ifdef MSCKF_GATE_PROBE
+__device__ unsigned long long g_info_probe[8];
+extern "C" int msckf_info_probe_read(unsigned long long* out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_info_probe), sizeof(g_info_probe)) != hipSuccess) return -1;
+    static unsigned long long zero[8] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_info_probe), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
+}
+#define IPROBE_T(v) const unsigned long long v = __builtin_readcyclecounter()
+#else
+#define IPROBE_T(v) (void)0
+#endif
+constexpr int IF_NW = 8;                 // waves per workgroup: 4 producers + 4 tile owners (two per SIMD)
 
 __host__ __device__ constexpr size_t info_fused_lds(int maxnf) {
     return (size_t)(2 * IF_KR * IM_GS + IF_KF * 32 * IF_ACC + 32 * IF_CG) * sizeof(double) + (size_t)maxnf * 48 + 16;
 }
 
+// Reciprocal and reciprocal square root of the fused producer: the hardware
+// approximations (v_rcp_f64 / v_rsq_f64) and one Newton step each -- within a
+// couple of ulps, against ~10 instructions of an IEEE division / sqrt.  (The
+// assembled information is invariant to these rounding-level choices well
+// inside the 1e-9 fp64 parity bound.)
+__device__ __forceinline__ double if_rcp(double x) {
+    const double r = __builtin_amdgcn_rcp(x);
+    return r * fma(-x, r, 2.0);
+}
+__device__ __forceinline__ double if_rsq(double x) {
+    const double r = __builtin_amdgcn_rsq(x);
+    return r * fma(-0.5 * x * r, r, 1.5);
+}
+
+// f(integral_constant<int, 0>) ... f(integral_constant<int, N - 1>), in order
+template <int N, class Fn>
+__device__ __forceinline__ void static_for(Fn&& f) {
+    if constexpr (N > 0) {
+        static_for<N - 1>(f);
+        f(std::integral_constant<int, N - 1>{});
+    }
+}
+
+// Lower 16 x 16 tile p (row-major lower order) -> row / column tile.
+__host__ __device__ constexpr int lt_row(int p) {
+    int i = 0;
+    while ((i + 1) * (i + 2) / 2 <= p) ++i;
+    return i;
+}
+__host__ __device__ constexpr int lt_col(int p) { return p - lt_row(p) * (lt_row(p) + 1) / 2; }
+
+// Tile-owner wave CW of k_info_fused: tiles p = PPW CW + q.  A tile takes a
+// k-step's rank-4 update iff the k-step's features touch both its column
+// ranges (km bits ti and tj; tiles past the window's last tile row never
+// match, ftm only has bits of real tiles).  Operands of the next batch of
+// five tiles are read before the current batch's MFMAs.
+template <int CW, int PPW>
+__device__ __forceinline__ void info_owner(const double* buf, const unsigned* ftm, int nl, int lane, KT* F, int C,
+                                           int ldf) {
+    const int lc = lane & 15, lr = lane >> 4;
+    v4d tacc[PPW];
+#pragma unroll
+    for (int q = 0; q < PPW; ++q) tacc[q] = v4d{0.0, 0.0, 0.0, 0.0};
+#ifdef MSCKF_GATE_PROBE
+    unsigned long long pr4 = 0, pr5 = 0;
+#endif
+    __syncthreads();   // chunk 0 in buffer 0
+    for (int l0 = 0, it = 0; l0 < nl; l0 += IF_KF, ++it) {
+        IPROBE_T(u0);
+        const double* cb = buf + (size_t)(it & 1) * IF_KR * IM_GS + lr * IM_GS + lc;
+        unsigned kmv[IF_NKS];
+#pragma unroll
+        for (int ks = 0; ks < IF_NKS; ++ks) {
+            const int sa = l0 + (4 * ks) / 3, sb = l0 + (4 * ks + 3) / 3;
+            kmv[ks] = __builtin_amdgcn_readfirstlane((sa < nl ? ftm[sa] : 0u) | (sb < nl ? ftm[sb] : 0u));
+        }
+        constexpr int HQ = 5, NHB = (PPW + HQ - 1) / HQ, NBAT = IF_NKS * NHB;
+        double oa[2][HQ], ob[2][HQ];
+        auto ldb = [&](auto nc) {
+            constexpr int n = decltype(nc)::value, ks = n / NHB, h = (n - ks * NHB) * HQ, sl = n & 1;
+            static_for<HQ>([&](auto qc) {
+                constexpr int q = decltype(qc)::value;
+                if constexpr (h + q < PPW) {
+                    constexpr int p = PPW * CW + h + q;
+                    oa[sl][q] = cb[4 * ks * IM_GS + 16 * lt_row(p)];
+                    ob[sl][q] = cb[4 * ks * IM_GS + 16 * lt_col(p)];
+                }
+            });
+        };
+        auto mfb = [&](auto nc) {
+            constexpr int n = decltype(nc)::value, ks = n / NHB, h = (n - ks * NHB) * HQ, sl = n & 1;
+            const unsigned km = kmv[ks];
+            static_for<HQ>([&](auto qc) {
+                constexpr int q = decltype(qc)::value;
+                if constexpr (h + q < PPW) {
+                    constexpr int p = PPW * CW + h + q;
+                    constexpr unsigned need = (1u << lt_row(p)) | (1u << lt_col(p));
+                    if ((km & need) == need)
+                        tacc[h + q] = __builtin_amdgcn_mfma_f64_16x16x4f64(oa[sl][q], ob[sl][q], tacc[h + q], 0, 0, 0);
+                }
+            });
+        };
+        ldb(std::integral_constant<int, 0>{});
+        static_for<NBAT>([&](auto nc) {
+            constexpr int n = decltype(nc)::value;
+            if constexpr (n + 1 < NBAT) ldb(std::integral_constant<int, n + 1>{});
+            mfb(nc);
+        });
+#ifdef MSCKF_GATE_PROBE
+        for (int q = 0; q < PPW; ++q) asm volatile("" : "+v"(tacc[q]));   // the MFMAs have completed
+        IPROBE_T(u1);
+#endif
+        __syncthreads();
+#ifdef MSCKF_GATE_PROBE
+        IPROBE_T(u2);
+        pr4 += u1 - u0;
+        pr5 += u2 - u1;
+#endif
+    }
+#ifdef MSCKF_GATE_PROBE
+    if (CW == 0 && lane == 0) {
+        atomicAdd(&g_info_probe[4], pr4);
+        atomicAdd(&g_info_probe[5], pr5);
+    }
+#endif
+#pragma unroll
+    for (int q = 0; q < PPW; ++q) {
+        const int p = PPW * CW + q, ti = lt_row(p), tj = lt_col(p);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int row = 16 * ti + lr + 4 * r, col = 16 * tj + lc;
+            if (row < C && col < C) {
+                const double v = -tacc[q][r];
+                F[(size_t)row * ldf + col] = v;
+                F[(size_t)col * ldf + row] = v;
+            }
+        }
+    }
+}
+
 template <typename T, int NW>
 __global__ void __launch_bounds__(64 * NW) k_info_fused(DevState<T> st, Params<T> prm, FeatBatch<T> fb, UpdWs<T> ws,
                                                         int maxnf) {
-    constexpr int NT = 64 * NW, PPW = (78 + NW - 1) / NW, NG = NT / IF_NP;
-    static_assert(NT % IF_NP == 0 && PPW * NW >= 78 && IF_KR % 4 == 0, "k_info_fused shape");
+    // waves 0 .. IF_NPW-1 build the chunks (IF_NP threads), the others own the tiles
+    constexpr int NT = 64 * NW, NCW = NW - IF_NPW, PPW = (78 + NCW - 1) / NCW;
+    static_assert(IF_NP == 64 * IF_NPW && NCW > 0 && PPW * NCW >= 78 && IF_KR % 4 == 0, "k_info_fused shape");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, lc = lane & 15, lr = lane >> 4;
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     int* info = ws.info + 4 * b;
     if (info[0] == 0) {   // nothing stacked: empty update
@@ -2513,7 +2654,6 @@ __global__ void __launch_bounds__(64 * NW) k_info_fused(DevState<T> st, Params<T
         return;
     }
     const int nc = st.ncams[b], C = 6 * nc, Cmax = ws.Cmax;
-    const int TT = (C + 15) >> 4, npair = TT * (TT + 1) / 2;
     double* buf = reinterpret_cast<double*>(smem_raw);          // [2][KR][IM_GS] dense rows of Gall
     double* acc = buf + 2 * IF_KR * IM_GS;                      // [KF][32][IF_ACC] Hx^T Hx (21) | UB (6)
     double* camg = acc + IF_KF * 32 * IF_ACC;                   // [32][IF_CG] R0 | R1 | t1 | p | R(q_null) g
@@ -2578,22 +2718,7 @@ __global__ void __launch_bounds__(64 * NW) k_info_fused(DevState<T> st, Params<T
             if (pb[c] != 0xff) m |= (1u << ((6 * c) >> 4)) | (1u << ((6 * c + 5) >> 4));
         ftm[i] = m;
     }
-    // this wave's tiles (lower, row-major order p -> (ti, tj))
-    int pti[PPW], ptj[PPW];
-    bool pv[PPW];
-    v4d tacc[PPW];
-#pragma unroll
-    for (int q = 0; q < PPW; ++q) {
-        const int p = PPW * wv + q;
-        int ti = (int)((sqrtf(8.0f * (float)p + 1.0f) - 1.0f) * 0.5f);
-        while (ti * (ti + 1) / 2 > p) --ti;
-        while ((ti + 1) * (ti + 2) / 2 <= p) ++ti;
-        pti[q] = __builtin_amdgcn_readfirstlane(ti);
-        ptj[q] = __builtin_amdgcn_readfirstlane(p - ti * (ti + 1) / 2);
-        pv[q] = p < npair;
-        tacc[q] = v4d{0.0, 0.0, 0.0, 0.0};
-    }
-    const int grp = tid / IF_NP, ps = (tid % IF_NP) >> 5, pc = tid & 31;
+    const int ps = (tid % IF_NP) >> 5, pc = tid & 31;
     // Producer thread (ps, pc) of chunk [l0, l0 + KF): feature ps's observation of
     // cam pc.  pload issues its global loads (kept raw in registers: a conversion
     // here would wait for them), pbuild forms the rows one MFMA phase later.
@@ -2653,7 +2778,7 @@ __global__ void __launch_bounds__(64 * NW) k_info_fused(DevState<T> st, Params<T
         mat3_vec(cg, d0, pc0);
         mat3_vec(cg + 9, d1, pc1);
         // Jc (msckf.py:457-475): rows [a00 0 a02], [0 a00 a12], b-rows times R01
-        const double i0 = 1.0 / pc0[2], i1 = 1.0 / pc1[2];
+        const double i0 = if_rcp(pc0[2]), i1 = if_rcp(pc1[2]);
         const double a00 = i0, a02 = -pc0[0] * i0 * i0, a12 = -pc0[1] * i0 * i0;
         const double b00 = i1, b02 = -pc1[0] * i1 * i1, b12 = -pc1[1] * i1 * i1;
         double J2[3], J3[3];
@@ -2673,13 +2798,13 @@ __global__ void __launch_bounds__(64 * NW) k_info_fused(DevState<T> st, Params<T
         const double n0 = a00 * r0 + J2[0] * r2 + J3[0] * r3;
         const double n1 = a00 * r1 + J2[1] * r2 + J3[1] * r3;
         const double n2 = a02 * r0 + a12 * r1 + J2[2] * r2 + J3[2] * r3;
-        const double l00 = sqrt(m00), il0 = l00 > 0 ? 1.0 / l00 : 0.0;
+        const double il0 = m00 > 0 ? if_rsq(m00) : 0.0, l00 = m00 * il0;
         const double l10 = m10 * il0, l20 = m20 * il0;
         const double e11 = m11 - l10 * l10;
-        const double l11 = e11 > 0 ? sqrt(e11) : 0.0, il1 = l11 > 0 ? 1.0 / l11 : 0.0;
+        const double il1 = e11 > 0 ? if_rsq(e11) : 0.0, l11 = e11 * il1;
         const double l21 = (m21 - l20 * l10) * il1;
         const double e22 = m22 - l20 * l20 - l21 * l21;
-        const double l22 = e22 > 0 ? sqrt(e22) : 0.0, il2 = l22 > 0 ? 1.0 / l22 : 0.0;
+        const double il2 = e22 > 0 ? if_rsq(e22) : 0.0, l22 = e22 * il2;
         const double h0 = n0 * il0, h1 = (n1 - l10 * h0) * il1, h2 = (n2 - l20 * h0 - l21 * h1) * il2;
         // B~ = [ [p_c0]x | -R_w_c0 ] (I - u u^T / u^T u), u = [R(q_null) g ; (p_w - p) x g]  (msckf.py:484-490)
         double u[6];
@@ -2691,7 +2816,7 @@ __global__ void __launch_bounds__(64 * NW) k_info_fused(DevState<T> st, Params<T
         double uu = 0.0;
 #pragma unroll
         for (int k = 0; k < 6; ++k) uu += u[k] * u[k];
-        const double iuu = 1.0 / uu;
+        const double iuu = if_rcp(uu);
         double H[3][6];   // B~, then H^ = L^T B~ in place (row a needs rows >= a only)
         {
             const double Sk[9] = {0.0, -pc0[2], pc0[1], pc0[2], 0.0, -pc0[0], -pc0[1], pc0[0], 0.0};
@@ -2743,64 +2868,59 @@ __global__ void __launch_bounds__(64 * NW) k_info_fused(DevState<T> st, Params<T
         for (int x = 0; x < 6; ++x)
             ac[21 + x] += (H[0][x] * h0 + H[1][x] * h1 + H[2][x] * h2) - (K[0][x] * gr0 + K[1][x] * gr1 + K[2][x] * gr2);
     };
-    if (nl > 0 && grp == 0) {
-        PIn in;
-        pload(0, in);
-        pbuild(in, 0);
-    }
-    __syncthreads();
-    for (int l0 = 0, it = 0; l0 < nl; l0 += IF_KF, ++it) {
-        const int cur = it & 1;
-        // ---- the next chunk's inputs, by the group whose turn it is: loads in
-        // flight under this chunk's MFMAs ----
-        const bool mine = l0 + IF_KF < nl && grp == (it + 1) % NG;
-        PIn in;
-        if (mine) pload(l0 + IF_KF, in);
-        // ---- rank-KR update of this wave's tiles from chunk it: each k-step's
-        // operands are read before its MFMAs (one LDS wait per k-step) ----
-        const double* cb = buf + (size_t)cur * IF_KR * IM_GS;
-        unsigned kmv[IF_NKS];
-#pragma unroll
-        for (int ks = 0; ks < IF_NKS; ++ks) {
-            const int sa = l0 + (4 * ks) / 3, sb = l0 + (4 * ks + 3) / 3;
-            kmv[ks] = (sa < nl ? ftm[sa] : 0u) | (sb < nl ? ftm[sb] : 0u);
-        }
-#pragma unroll
-        for (int ks = 0; ks < IF_NKS; ++ks) {
-            const unsigned km = __builtin_amdgcn_readfirstlane(kmv[ks]);
-            const double* brow = cb + (4 * ks + lr) * IM_GS + lc;
-            constexpr int HQ = (PPW + 1) / 2;   // operands read half a tile list at a time (VGPRs)
-#pragma unroll
-            for (int h = 0; h < PPW; h += HQ) {
-                double oa[HQ], ob[HQ];
-#pragma unroll
-                for (int q = 0; q < HQ; ++q) {
-                    oa[q] = h + q < PPW ? brow[16 * pti[h + q < PPW ? h + q : 0]] : 0.0;
-                    ob[q] = h + q < PPW ? brow[16 * ptj[h + q < PPW ? h + q : 0]] : 0.0;
-                }
-#pragma unroll
-                for (int q = 0; q < HQ; ++q)
-                    if (h + q < PPW && pv[h + q] && ((km >> pti[h + q]) & (km >> ptj[h + q]) & 1u))
-                        tacc[h + q] = __builtin_amdgcn_mfma_f64_16x16x4f64(oa[q], ob[q], tacc[h + q], 0, 0, 0);
-            }
-        }
-        // ---- build the next chunk ----
-        if (mine) pbuild(in, cur ^ 1);
-        __syncthreads();
-    }
     KT* F = ws.Hthin + (size_t)b * Cmax * (Cmax + 1);
     const int ldf = Cmax + 1;
-#pragma unroll
-    for (int q = 0; q < PPW; ++q) {
-        if (!pv[q]) continue;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int row = 16 * pti[q] + lr + 4 * r, col = 16 * ptj[q] + lc;
-            if (row < C && col < C) {
-                const double v = -tacc[q][r];
-                F[(size_t)row * ldf + col] = v;
-                F[(size_t)col * ldf + row] = v;
-            }
+#ifdef MSCKF_GATE_PROBE
+    unsigned long long pr[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const unsigned long long t_beg = __builtin_readcyclecounter();
+#endif
+    if (wv < IF_NPW) {
+        // ---- producers: chunk it + 1 is built while the consumers run chunk it;
+        // its global loads were issued one iteration earlier ----
+        PIn nxt;
+        if (nl > 0) {
+            PIn c0;
+            pload(0, c0);
+            pbuild(c0, 0);
+        }
+        if (IF_KF < nl) pload(IF_KF, nxt);
+        __syncthreads();   // chunk 0 in buffer 0
+#ifdef MSCKF_GATE_PROBE
+        pr[0] += __builtin_readcyclecounter() - t_beg;
+#endif
+        for (int l0 = 0, it = 0; l0 < nl; l0 += IF_KF, ++it) {
+            IPROBE_T(t0);
+            PIn far;
+            if (l0 + 2 * IF_KF < nl) pload(l0 + 2 * IF_KF, far);
+            IPROBE_T(t1);
+            if (l0 + IF_KF < nl) pbuild(nxt, (it + 1) & 1);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            IPROBE_T(t2);
+            nxt = far;
+            __syncthreads();
+            IPROBE_T(t3);
+#ifdef MSCKF_GATE_PROBE
+            pr[1] += t1 - t0; pr[2] += t2 - t1; pr[3] += t3 - t2; pr[6] += 1;
+#endif
+        }
+#ifdef MSCKF_GATE_PROBE
+        if (tid == 0) {
+            for (int k = 0; k < 4; ++k) atomicAdd(&g_info_probe[k], pr[k]);
+            atomicAdd(&g_info_probe[6], pr[6]);
+            atomicAdd(&g_info_probe[7], 1ull);
+        }
+#endif
+    } else {
+        // ---- tile owners: one code path per owner wave, so that every tile's
+        // coordinates, LDS operand offsets and activity test are compile-time
+        // constants (a runtime tile list cost ~12 scalar / readlane
+        // instructions of bookkeeping per tile and k-step) ----
+        const int cw = wv - IF_NPW;
+        switch (cw) {
+            case 0: info_owner<0, PPW>(buf, ftm, nl, lane, F, C, ldf); break;
+            case 1: info_owner<1, PPW>(buf, ftm, nl, lane, F, C, ldf); break;
+            case 2: info_owner<2, PPW>(buf, ftm, nl, lane, F, C, ldf); break;
+            default: info_owner<3, PPW>(buf, ftm, nl, lane, F, C, ldf); break;
         }
     }
     __syncthreads();   // the tiles' stores are visible to the block-diagonal owners
