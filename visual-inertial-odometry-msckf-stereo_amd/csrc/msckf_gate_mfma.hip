@@ -74,15 +74,41 @@ __device__ __forceinline__ double gfma(double a, double b, double c) { return fm
 
 __host__ __device__ constexpr int gm_nb(int M) { return (3 * M + 4 + 15) / 16; }
 __host__ __device__ constexpr int gm_head(int Mmax) { return (22 * Mmax + 3) & ~3; }   // Ht rows + [r~ | r_n]
-// Y staging / panel + the junk panel (written up to 128 NB + 12 RS - 1 by the
+// The Y pairs are staged as a dense lower-triangular matrix, row q holding
+// columns 0..q plus two padding slots (a diagonal pair block writes its upper
+// 3 x 3 corner there): row q starts at gm_rowoff(q).  The assembly then reads
+// element (q, 16 CB + col) of every block of a block row at one per-row lane
+// address plus a compile-time offset -- no index arithmetic per element.
+__host__ __device__ constexpr int gm_rowoff(int q) { return (q * q + 5 * q) / 2; }
+// stage elements of observation rows [alo, ahi]
+__host__ __device__ constexpr int gm_dense(int alo, int ahi) {
+    return ahi < alo ? 0 : gm_rowoff(3 * ahi + 3) - gm_rowoff(3 * alo);
+}
+// Y staging / panel + the junk panel (written up to 128 NB + 12 RS + 23 by the
 // lanes that own no pivot column)
-__host__ __device__ constexpr int gm_area(int Mmax, int capb, int RS = 1) {
-    return 9 * capb > 128 * gm_nb(Mmax) + 16 * RS ? ((9 * capb + 3) & ~3) : 128 * gm_nb(Mmax) + 16 * RS;
+__host__ __device__ constexpr int gm_area(int Mmax, int capf, int RS = 1) {
+    return capf > 128 * gm_nb(Mmax) + 16 * RS + 16 ? ((capf + 15) & ~3) : 128 * gm_nb(Mmax) + 16 * RS + 16;
 }
+// the B rows [H_f~^T ; r~^T] (4 x 16 NB, zero beyond 3M) and a zero row (16 NB)
+// the padding rows of the assembly read
+__host__ __device__ constexpr int gm_brows(int Mmax) { return 80 * gm_nb(Mmax); }
 // elements of T per wave (the two int offset tables take T-sized slots)
-__host__ __device__ constexpr int gm_wave_floats(int Mmax, int capb, int RS = 1) {
-    return gm_head(Mmax) + gm_area(Mmax, capb, RS) + 2 * ((Mmax + 3) & ~3);
+__host__ __device__ constexpr int gm_wave_floats(int Mmax, int capf, int RS = 1) {
+    return gm_head(Mmax) + gm_area(Mmax, capf, RS) + gm_brows(Mmax) + 2 * ((Mmax + 3) & ~3);
 }
+// Pair k = a (a + 1) / 2 + b (b <= a) of the Y phase: a | b << 8 | (stage offset
+// of element (3a, 3b)) << 16, one table load instead of a square-root decode.
+constexpr int GM_MAXM = 41;   // gm_nb(41) = 8, the largest one-wave class
+struct GmPairTab {
+    unsigned v[GM_MAXM * (GM_MAXM + 1) / 2];
+    constexpr GmPairTab() : v() {
+        int k = 0;
+        for (int a = 0; a < GM_MAXM; ++a)
+            for (int b = 0; b <= a; ++b) v[k++] = (unsigned)a | ((unsigned)b << 8) | ((unsigned)(gm_rowoff(3 * a) + 3 * b) << 16);
+    }
+};
+static_assert(gm_rowoff(3 * GM_MAXM) < 65536, "pair table offsets are 16-bit");
+__device__ constexpr GmPairTab g_gm_pairs{};
 #ifndef GATE_BIF_BIG
 #define GATE_BIF_BIG 3
 #endif
@@ -125,7 +151,15 @@ __device__ __forceinline__ bool gm_eliminate(typename GM<T>::V4 (&acc)[NB * (NB 
     // this lane's B-operand element of block row RB: panel row 16 RB + col_l, column csel
     const T* bsrc = pan + 4 * col_l + csel;
     const bool owner[4] = {(col_l >> 2) == 0, (col_l >> 2) == 1, (col_l >> 2) == 2, (col_l >> 2) == 3};
-    bool ok = true;
+    // junk slots of the lanes that own no pivot column: the lane's own bank,
+    // except (fp32) that the column 0..3 lanes move 4 sc banks up when another
+    // group owns the step -- the owners' banks are theirs (16 rg + c) then, and
+    // the dump would be 2-way conflicted
+    T* junk[4];
+#pragma unroll
+    for (int sc = 0; sc < 4; ++sc)
+        junk[sc] = pan + 64 * NB + lane + ((RS == 1 && sc > 0 && (col_l >> 2) == 0) ? 4 * sc : 0);
+    T dmin = T(1);   // smallest pivot (a NaN pivot poisons the B rows instead: gm_finish)
 #pragma unroll
     for (int KB = 0; KB < NB; ++KB) {
 #pragma unroll
@@ -137,7 +171,7 @@ __device__ __forceinline__ bool gm_eliminate(typename GM<T>::V4 (&acc)[NB * (NB 
             //    one dword column per lane: no bank conflicts) -- no divergent
             //    branch in the step
             {
-                T* d = owner[sc] ? pan + 4 * (16 * KB + RG * rg) + (col_l & 3) : pan + 64 * NB + lane;
+                T* d = owner[sc] ? pan + 4 * (16 * KB + RG * rg) + (col_l & 3) : junk[sc];
 #pragma unroll
                 for (int RB = KB; RB < NB; ++RB) {
                     const V4 v = acc[bidx(RB, KB)];
@@ -166,7 +200,7 @@ __device__ __forceinline__ bool gm_eliminate(typename GM<T>::V4 (&acc)[NB * (NB 
             const T m32 = r3.z - l30 * r2.x - l31 * m21;
             const T l32 = m32 * e2;
             const T d3 = r3.w - l30 * r3.x - l31 * m31 - l32 * m32;
-            ok = ok && (d0 > T(0)) && (d1 > T(0)) && (d2 > T(0)) && (d3 > T(0));
+            dmin = fmin(dmin, fmin(fmin(d0, d1), fmin(d2, d3)));
             const T e3 = pivot_rcp(d3);
             // 3. the rank-4 update is C -= X A_d^-1 X^T, X = the panel columns: the
             //    B operand is X itself (lane: row 16 RB + col_l, pivot csel), the A
@@ -219,7 +253,7 @@ __device__ __forceinline__ bool gm_eliminate(typename GM<T>::V4 (&acc)[NB * (NB 
                     acc[bidx(RB, CB)] = GM<T>::mfma(av[RB], bv[CB], acc[bidx(RB, CB)]);
         }
     }
-    return !ok;
+    return !(dmin > T(0));
 }
 
 // gamma from the B rows' 4x4 Schur block (negated [[H_f~^T Y~^-1 H_f~, .],
@@ -260,64 +294,64 @@ __device__ __forceinline__ void gm_finish(const typename GM<T>::V4 (&acc)[NB * (
 
 // Matrix assembly into the C-layout blocks of block rows [R0, R1): every
 // element written exactly once -- Y entries (lower, s2 on the diagonal) from
-// the pass's pair stage (kbase = its first pair), B rows [H_f~^T ; r~^T]
-// (H_f~ = -Ht[:, 3:6]) in rows 12..15 of block NB - 1, unit padding pivots,
-// zeros.  The stage offset of Y[q][p] separates into a row part and a
-// column part: 9 (a (a + 1) / 2 + b) + 3 c_q + c_p with a = q / 3, b = p / 3.
+// the pass's dense stage (soff0 = gm_rowoff of its first row), the B rows
+// [H_f~^T ; r~^T] (H_f~ = -Ht[:, 3:6]) from brow, the padding rows (3M <= q <
+// 16 NB - 4: unit pivots) from the zero row, zeros above the diagonal.  Each of
+// the lane's four rows of a block row resolves to one LDS address; element
+// (q, 16 CB + col) is then that address + 16 CB (an instruction offset), so
+// the off-diagonal blocks cost no vector ALU at all.  Rows at or past 3M occur
+// only in the last two block rows (the class is exact: 3M >= 16 NB - 19).
 template <typename T, int NB>
-__device__ __forceinline__ void gm_assemble(typename GM<T>::V4 (&acc)[NB * (NB + 1) / 2], int R0, int R1, int kbase,
-                                            int M3, T s2, const T* stage, const T* ht, const T* rt, int Mmax,
-                                            int lane) {
+__device__ __forceinline__ void gm_assemble(typename GM<T>::V4 (&acc)[NB * (NB + 1) / 2], int R0, int R1, int soff0,
+                                            int M3, T s2, const T* stage, const T* brow, const T* zrow, int lane) {
     using V4 = typename GM<T>::V4;
     constexpr int RS = GM<T>::RS, RG = GM<T>::RG;
-    constexpr int nb = NB;
-    const int nB = 16 * nb - 4, pad_lo = M3;
-    int col_l = lane & 15, rg = lane >> 4;   // opaque copies: index math stays in the pass loop
+    constexpr int nB = 16 * NB - 4;
+    int col_l = lane & 15, rg = lane >> 4;
+    // opaque copies: the row offsets are computed in the pass loop, not hoisted
+    // out of it into registers live across every pass
     asm volatile("" : "+v"(col_l), "+v"(rg));
+    int r[4];
+    bool up[4], dg[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        r[i] = RG * rg + RS * i;
+        up[i] = r[i] < col_l;
+        dg[i] = r[i] == col_l;
+    }
 #pragma unroll
     for (int RB = 0; RB < NB; ++RB) {
         if (RB < R0 || RB >= R1) continue;   // uniform
-        const bool brow = RB == nb - 1 && rg == 3;   // (f32) this lane's 4 rows are the B rows
-        int rofs[4];
+        const T* src[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const int q = 16 * RB + RG * rg + RS * i, oa = q / 3;
-            rofs[i] = 9 * (oa * (oa + 1) / 2 - kbase) + 3 * (q - 3 * oa);
+            const int q = 16 * RB + r[i];
+            const T* ptr = stage + (gm_rowoff(q) - soff0) + col_l;
+            if (RB >= NB - 2) {
+                ptr = q < M3 ? ptr : zrow + col_l;
+                if (RB == NB - 1) ptr = q >= nB ? brow + (q - nB) * (16 * NB) + col_l : ptr;
+            }
+            src[i] = ptr;
         }
 #pragma unroll
         for (int CB = 0; CB <= RB; ++CB) {
-            const int p = 16 * CB + col_l, ob = p / 3, cp = p - 3 * ob;
-            T bval[4] = {T(0), T(0), T(0), T(0)};
-            if (RB == nb - 1) {   // uniform
-                if constexpr (RS == 1) {
-                    const bool pv = brow && p < M3;
-                    const int o = pv ? ob : 0;
-#pragma unroll
-                    for (int i = 0; i < 3; ++i) bval[i] = pv ? -ht[18 * o + 6 * cp + 3 + i] : T(0);
-                    bval[3] = pv ? rt[4 * o + cp] : T(0);
-                } else {   // f64: element 3 of every lane is B row rg (rows 12..15)
-                    const bool pv = p < M3;
-                    const int o = pv ? ob : 0;
-                    const T hv = ht[rg < 3 ? 18 * o + 6 * cp + 3 + rg : 18 * Mmax + 4 * o + cp];
-                    bval[3] = pv ? (rg < 3 ? -hv : hv) : T(0);
-                }
-            }
             V4 a;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int q = 16 * RB + RG * rg + RS * i;
-                const bool take = q < pad_lo && (RB > CB || q >= p);
-                const T y = stage[take ? rofs[i] + 9 * ob + cp : 0];
-                T v = bval[i];
-                if (RB == CB) {
-                    v = (q == p && q >= pad_lo && q < nB) ? T(1) : v;
-                    v = take ? y + (q == p ? s2 : T(0)) : v;
-                } else {
-                    v = take ? y : v;
+            for (int i = 0; i < 4; ++i) a[i] = src[i][16 * CB];
+            if (CB == RB) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int q = 16 * RB + r[i];
+                    const T dv = RB < NB - 2 ? s2 : (q < M3 ? s2 : (q < nB ? T(1) : T(0)));
+                    a[i] = up[i] ? T(0) : (dg[i] ? a[i] + dv : a[i]);
                 }
-                a[i] = v;
             }
             acc[bidx(RB, CB)] = a;
+            // one block's reads in flight at a time: the reads land in the
+            // accumulators themselves, no register peak on top of them (the
+            // scheduler otherwise hoists a whole block row of reads -- 152 VGPRs
+            // spilled in the fp64 NB = 6 class)
+            __builtin_amdgcn_sched_barrier(0);
         }
     }
 }
@@ -332,7 +366,7 @@ __host__ __device__ constexpr int gm_waves(int NB, bool MP, int ts = 4) {
 
 template <typename T, int NB, bool MP>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_waves(NB, MP, sizeof(T))))) k_gate_mfma(DevState<T> st, Params<T> prm, FeatBatch<T> fb,
-                                                   const int* __restrict__ flist, int nlist, int Mmax, int capb) {
+                                                   const int* __restrict__ flist, int nlist, int Mmax, int capf) {
     using V4 = typename GM<T>::V4;
     using V2 = typename GM<T>::V2;
     constexpr int RS = GM<T>::RS;
@@ -356,12 +390,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_wav
     const int o0 = __builtin_amdgcn_readfirstlane(fb.obs_off[f]);
     const int M = __builtin_amdgcn_readfirstlane(fb.obs_off[f + 1]) - o0, M3 = 3 * M;
     constexpr int nb = NB;                 // the size class: gm_nb(M) == NB (gm_class_exact)
-    T* ht = reinterpret_cast<T*>(smem_raw) + (size_t)wv * gm_wave_floats(Mmax, capb, RS);
+    T* ht = reinterpret_cast<T*>(smem_raw) + (size_t)wv * gm_wave_floats(Mmax, capf, RS);
     T* rt = ht + 18 * Mmax;                // [Mmax][4]: r~ (3), r_n
     T* area = ht + gm_head(Mmax);
-    T* stage = area;                       // [capb][9] Y blocks of one pass (row-major lower block order)
+    T* stage = area;                       // [capf] dense lower Y rows of one pass (gm_rowoff)
     T* pan = area;                         // [16 NB][4] panel rows (after the Y phase)
-    int* slot = reinterpret_cast<int*>(area + gm_area(Mmax, capb, RS));
+    T* brow = area + gm_area(Mmax, capf, RS);   // [4][16 NB] B rows
+    T* zrow = brow + 64 * NB;                    // [16 NB] zeros
+    int* slot = reinterpret_cast<int*>(brow + gm_brows(Mmax));
     // The feature's gating records ([M][OBS_HTS] from k_feature: Ht 3 x 6, r~, r_n)
     // as element pairs, and its cam slots: every global load issued before the
     // first wait (one round trip instead of one per loop trip), then scattered
@@ -397,6 +433,21 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_wav
     }
     rn2 = wave_sum(rn2);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // B rows [H_f~^T ; r~^T] over the 16 NB columns (zero past 3M) and the zero row
+#pragma unroll
+    for (int j = 0; j < (16 * NB + 63) / 64; ++j) {
+        const int p = lane + 64 * j;
+        if (p < 16 * NB) {
+            const bool pv = p < M3;
+            const int o = pv ? p / 3 : 0, cp = p - 3 * o;
+            const T* h = ht + 18 * o + 6 * cp + 3;
+            brow[p] = pv ? -h[0] : T(0);
+            brow[16 * NB + p] = pv ? -h[1] : T(0);
+            brow[32 * NB + p] = pv ? -h[2] : T(0);
+            brow[48 * NB + p] = pv ? rt[4 * o + cp] : T(0);
+            zrow[p] = T(0);
+        }
+    }
     GPROBE_T(t_fetched);
     GPROBE_ADD(sizeof(T), NB, 0, t_fetched - t_start);
 #ifdef MSCKF_GATE_PROBE
@@ -406,18 +457,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_wav
     constexpr int NBLK = NB * (NB + 1) / 2;
     V4 acc[NBLK];
     const T s2 = prm.sigma2;
-    auto assemble = [&](int R0, int R1, int kbase) {
-        gm_assemble<T, NB>(acc, R0, R1, kbase, M3, s2, stage, ht, rt, Mmax, lane);
+    auto assemble = [&](int R0, int R1, int soff0) {
+        gm_assemble<T, NB>(acc, R0, R1, soff0, M3, s2, stage, brow, zrow, lane);
     };
 
-    // ---- Y: observation-pair blocks Ht_a P_ab Ht_b^T (a >= b, 3x3) into LDS in
-    // row-major lower order k = a (a + 1) / 2 + b -- consecutive lanes take
-    // consecutive b of one row a, so a load instruction reads consecutive 24-byte
-    // row segments of P (cams of a track are usually consecutive slots) instead
-    // of 64 scattered blocks.  When capb < M (M + 1) / 2 the pairs are staged in
-    // passes aligned to block rows [R0, R1) (observation rows [16 R0 / 3,
-    // (16 R1 - 1) / 3], those straddling a boundary twice), so that every
-    // accumulator block is assembled once, never read back.
+    // ---- Y: observation-pair blocks Ht_a P_ab Ht_b^T (a >= b, 3x3) into the
+    // dense lower stage, pairs enumerated in row-major lower order k = a (a + 1)
+    // / 2 + b (g_gm_pairs) -- consecutive lanes take consecutive b of one row a,
+    // so a load instruction reads consecutive 24-byte row segments of P (cams of
+    // a track are usually consecutive slots) instead of 64 scattered blocks.
+    // When the whole matrix exceeds capf elements the rows are staged in passes
+    // aligned to block rows [R0, R1) (observation rows [16 R0 / 3, (16 R1 - 1) /
+    // 3], those straddling a boundary twice), so that every accumulator block is
+    // assembled once, never read back.
     const T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
     const int ldp = st.Dmax;
     // pair blocks per lane in flight: the Y phase's VGPRs are free up to the
@@ -429,22 +481,26 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_wav
         int R1 = R0 + 1, ahi = min(M - 1, (16 * R1 - 1) / 3);
         while (R1 < nb) {
             const int ah2 = min(M - 1, (16 * (R1 + 1) - 1) / 3);
-            if (npairs(alo, ah2) > capb) break;
+            if (gm_dense(alo, ah2) > capf) break;
             ++R1;
             ahi = ah2;
         }
         const int kbase = alo * (alo + 1) / 2, nbp = npairs(alo, ahi);
+        const int soff0 = gm_rowoff(3 * alo);
+        // stage rows of pair entry e: 3a, 3a + 1, 3a + 2 (row q + 1 starts q + 3 after row q)
+        auto pair_dst = [&](unsigned e, int a, T* (&d)[3]) {
+            d[0] = stage + ((int)(e >> 16) - soff0);
+            d[1] = d[0] + 3 * a + 3;
+            d[2] = d[1] + 3 * a + 4;
+        };
         GPROBE_T(t_p0);
         if constexpr (MP && GM_STREAM) {
             // staged in passes (earlier passes' accumulators live): one pair per
             // lane, P streamed a row at a time into Ha P (3 x 6) -- 18 + 6
             // elements in registers instead of the 6 x 6 block's 36
             for (int kk = lane; kk < nbp; kk += 64) {
-                const int k = kbase + kk;
-                int a = (int)((__builtin_amdgcn_sqrtf(8.0f * (float)k + 1.0f) - 1.0f) * 0.5f);
-                if (a * (a + 1) / 2 > k) --a;
-                if ((a + 1) * (a + 2) / 2 <= k) ++a;
-                const int bo = k - a * (a + 1) / 2;
+                const unsigned pe = g_gm_pairs.v[kbase + kk];
+                const int a = pe & 0xff, bo = (pe >> 8) & 0xff;
                 const T* Pb = P + (slot[a] + coff[bo]);
                 const T* Ha = ht + 18 * a;
                 const T* Hb = ht + 18 * bo;
@@ -466,7 +522,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_wav
                     }
                     __builtin_amdgcn_sched_barrier(0);   // one P row in flight
                 }
-                T* dst = stage + 9 * kk;
+                T* dst[3];
+                pair_dst(pe, a, dst);
 #pragma unroll
                 for (int x = 0; x < 3; ++x) {
                     const T t1[6] = {t[x][0].x, t[x][0].y, t[x][1].x, t[x][1].y, t[x][2].x, t[x][2].y};
@@ -477,26 +534,35 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_wav
                         y01 = __builtin_elementwise_fma(V2{t1[u], t1[u]}, V2{Hb[u], Hb[6 + u]}, y01);
                         y2 = gfma(t1[u], Hb[12 + u], y2);
                     }
-                    dst[3 * x] = y01.x;
-                    dst[3 * x + 1] = y01.y;
-                    dst[3 * x + 2] = y2;
+                    dst[x][0] = y01.x;
+                    dst[x][1] = y01.y;
+                    dst[x][2] = y2;
                 }
             }
         } else
-        for (int k0 = 0; k0 < nbp; k0 += 64 * BIF) {
-            T Pl[BIF][36];
-            int oa[BIF], ob[BIF];
+        {
+        // the next trip's pair entries are loaded under this trip's arithmetic
+        unsigned pen[BIF];
+        auto pload = [&](int k0) {
 #pragma unroll
             for (int j = 0; j < BIF; ++j) {
                 const int kk = k0 + 64 * j + lane;
-                const int k = kbase + (kk < nbp ? kk : 0);
-                // row of pair k: the hardware square root (1 ulp) is enough, the
-                // two integer fix-ups make the decode exact
-                int a = (int)((__builtin_amdgcn_sqrtf(8.0f * (float)k + 1.0f) - 1.0f) * 0.5f);
-                if (a * (a + 1) / 2 > k) --a;
-                if ((a + 1) * (a + 2) / 2 <= k) ++a;
-                oa[j] = a;
-                ob[j] = k - a * (a + 1) / 2;
+                pen[j] = g_gm_pairs.v[kbase + (kk < nbp ? kk : 0)];
+            }
+        };
+        pload(0);
+        for (int k0 = 0; k0 < nbp; k0 += 64 * BIF) {
+            T Pl[BIF][36];
+            int oa[BIF], ob[BIF];
+            unsigned pe[BIF];
+#pragma unroll
+            for (int j = 0; j < BIF; ++j) pe[j] = pen[j];
+            if (k0 + 64 * BIF < nbp) pload(k0 + 64 * BIF);
+#pragma unroll
+            for (int j = 0; j < BIF; ++j) {
+                const int kk = k0 + 64 * j + lane;
+                oa[j] = pe[j] & 0xff;
+                ob[j] = (pe[j] >> 8) & 0xff;
                 const T* Pb = P + (slot[oa[j]] + coff[ob[j]]);
 #pragma unroll
                 for (int u = 0; u < 6; ++u) {
@@ -514,7 +580,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_wav
                 if (kk >= nbp) continue;
                 const T* Ha = ht + 18 * oa[j];
                 const T* Hb = ht + 18 * ob[j];
-                T* dst = stage + 9 * kk;
+                T* dst[3];
+                pair_dst(pe[j], oa[j], dst);
                 V2 hb01[6];   // (Hb[0][u], Hb[1][u])
 #pragma unroll
                 for (int u = 0; u < 6; ++u) hb01[u] = V2{Hb[u], Hb[6 + u]};
@@ -537,15 +604,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_wav
                         y01 = __builtin_elementwise_fma(V2{t1[u], t1[u]}, hb01[u], y01);
                         y2 = gfma(t1[u], Hb[12 + u], y2);
                     }
-                    dst[3 * x] = y01.x;
-                    dst[3 * x + 1] = y01.y;
-                    dst[3 * x + 2] = y2;
+                    dst[x][0] = y01.x;
+                    dst[x][1] = y01.y;
+                    dst[x][2] = y2;
                 }
             }
         }
+        }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // one wave: its stores are visible to all lanes
         GPROBE_T(t_p1);
-        assemble(R0, R1, kbase);
+        assemble(R0, R1, soff0);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads done before the next pass / the panel reuse
 #ifdef MSCKF_GATE_PROBE
         GPROBE_T(t_p2);
@@ -841,7 +909,7 @@ __global__ void __launch_bounds__(256) k_gate_mfma_wg(DevState<float> st, Params
 
 template <typename T, int NB, bool MP>
 void launch_cfg(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const FeatBatch<T>& fb,
-                const int* list, int cnt, int Mmax, int capb, int wpb, size_t lds) {
+                const int* list, int cnt, int Mmax, int capf, int wpb, size_t lds) {
     static size_t attr = 64 * 1024;
     if (lds > attr) {
         (void)hipFuncSetAttribute((const void*)k_gate_mfma<T, NB, MP>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -849,7 +917,7 @@ void launch_cfg(hipStream_t s, const DevState<T>& st, const Params<T>& prm, cons
         attr = lds;
     }
     hipLaunchKernelGGL((k_gate_mfma<T, NB, MP>), dim3((cnt + wpb - 1) / wpb), dim3(64 * wpb), lds, s, st, prm, fb,
-                       list, cnt, Mmax, capb);
+                       list, cnt, Mmax, capf);
 }
 
 template <typename T, int NB>
@@ -865,23 +933,28 @@ void launch_nb(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const
     // (round 3, one-wave workgroups: fp32 budgets of 40 / 44 / 48 KB per four waves
     // measured 2.47 ms against 2.52 ms for 36 -- profiles/r03/ab_gate_kb/; fp64
     // keeps 72, its two waves per SIMD already fill the LDS)
+    // (round 4: the staging is the dense lower matrix, capacities in elements)
     constexpr int single_kb = sizeof(T) == 4 ? 44 : 72;
     constexpr int RS = GM<T>::RS;
-    const int nbk = Mmax * (Mmax + 1) / 2;
-    const int cmin = 6 * Mmax < nbk ? 6 * Mmax : nbk;   // one block row (up to six observation rows) per pass
-    auto per_wave = [&](int cb) { return (size_t)gm_wave_floats(Mmax, cb, RS) * sizeof(T); };
-    int capb = nbk;
-    if (4 * per_wave(capb) > (size_t)single_kb * 1024)
-        for (int parts = 2; 4 * per_wave(capb) > (size_t)single_kb * 512 && capb > cmin; ++parts)
-            capb = (nbk + parts - 1) / parts > cmin ? (nbk + parts - 1) / parts : cmin;
-    const size_t pw = per_wave(capb);
+    const int full = gm_dense(0, Mmax - 1);
+    int cmin = 0;   // one block row per pass at least
+    for (int R = 0; R < gm_nb(Mmax); ++R) {
+        const int alo = 16 * R / 3, ahi = (16 * R + 15) / 3 < Mmax - 1 ? (16 * R + 15) / 3 : Mmax - 1;
+        cmin = gm_dense(alo, ahi) > cmin ? gm_dense(alo, ahi) : cmin;
+    }
+    auto per_wave = [&](int cf) { return (size_t)gm_wave_floats(Mmax, cf, RS) * sizeof(T); };
+    int capf = full;
+    if (4 * per_wave(capf) > (size_t)single_kb * 1024)
+        for (int parts = 2; 4 * per_wave(capf) > (size_t)single_kb * 512 && capf > cmin; ++parts)
+            capf = (full + parts - 1) / parts > cmin ? (full + parts - 1) / parts : cmin;
+    const size_t pw = per_wave(capf);
     // one wave per workgroup: a wave's LDS and registers are released as soon as
     // its feature is done, not when the slowest of four features sharing a
     // workgroup is (the class's track lengths differ): 2.53 -> 2.49 ms at 30x200,
     // step 9.19 -> 9.15 ms over four alternated runs (profiles/r03/ab_gate_wpb/)
     const int wpb = 1;
-    if (capb < nbk) launch_cfg<T, NB, true>(s, st, prm, fb, list, cnt, Mmax, capb, wpb, wpb * pw);
-    else launch_cfg<T, NB, false>(s, st, prm, fb, list, cnt, Mmax, capb, wpb, wpb * pw);
+    if (capf < full) launch_cfg<T, NB, true>(s, st, prm, fb, list, cnt, Mmax, capf, wpb, wpb * pw);
+    else launch_cfg<T, NB, false>(s, st, prm, fb, list, cnt, Mmax, capf, wpb, wpb * pw);
 }
 
 
