@@ -160,6 +160,9 @@ __device__ __forceinline__ bool gm_eliminate(typename GM<T>::V4 (&acc)[NB * (NB 
     for (int sc = 0; sc < 4; ++sc)
         junk[sc] = pan + 64 * NB + lane + ((RS == 1 && sc > 0 && (col_l >> 2) == 0) ? 4 * sc : 0);
     T dmin = T(1);   // smallest pivot (a NaN pivot poisons the B rows instead: gm_finish)
+    T onehot[4];     // e_csel
+#pragma unroll
+    for (int k = 0; k < 4; ++k) onehot[k] = csel == k ? T(1) : T(0);
 #pragma unroll
     for (int KB = 0; KB < NB; ++KB) {
 #pragma unroll
@@ -207,18 +210,17 @@ __device__ __forceinline__ bool gm_eliminate(typename GM<T>::V4 (&acc)[NB * (NB 
             //    operand X m with m = -(column csel of A_d^-1 = L^-T D^-1 L^-1).  Rows
             //    of finished pivots are not masked: exact elimination leaves them
             //    zero, and they only ever feed finished rows / columns.
-            const T i10 = -l10, i21 = -l21, i32 = -l32;
-            const T i20 = -l20 - l21 * i10, i31 = -l31 - l32 * i21;
-            const T i30 = -l30 - l31 * i10 - l32 * i20;
-            // h_j = (L^-1)[j][csel]; u_j = h_j / d_j
-            const T u0 = csel == 0 ? e0 : T(0);
-            const T u1 = (csel == 1 ? T(1) : (csel == 0 ? i10 : T(0))) * e1;
-            const T u2 = (csel == 2 ? T(1) : (csel == 1 ? i21 : (csel == 0 ? i20 : T(0)))) * e2;
-            const T u3 = (csel == 3 ? T(1) : (csel == 2 ? i32 : (csel == 1 ? i31 : i30))) * e3;
-            const T mm3 = -u3;
-            const T mm2 = -gfma(i32, u3, u2);
-            const T mm1 = -gfma(i31, u3, gfma(i21, u2, u1));
-            const T mm0 = -gfma(i30, u3, gfma(i20, u2, gfma(i10, u1, u0)));
+            //    h = L^-1 e_csel (forward, from the lane's one-hot), u = D^-1 h,
+            //    m = L^-T u (backward): 16 FMAs, no per-lane selects
+            const T h0 = onehot[0];
+            const T h1 = gfma(-l10, h0, onehot[1]);
+            const T h2 = gfma(-l21, h1, gfma(-l20, h0, onehot[2]));
+            const T h3 = gfma(-l32, h2, gfma(-l31, h1, gfma(-l30, h0, onehot[3])));
+            const T u0 = h0 * e0, u1 = h1 * e1, u2 = h2 * e2, u3 = h3 * e3;
+            const T m2 = gfma(-l32, u3, u2);
+            const T m1 = gfma(-l31, u3, gfma(-l21, m2, u1));
+            const T m0 = gfma(-l30, u3, gfma(-l20, m2, gfma(-l10, m1, u0)));
+            const T mm3 = -u3, mm2 = -m2, mm1 = -m1, mm0 = -m0;
             if constexpr (STREAM) {
                 // one block row at a time -- its panel row, its A operand, its
                 // blocks' updates -- so that the accumulators and the step's
@@ -401,9 +403,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_wav
     // The feature's gating records ([M][OBS_HTS] from k_feature: Ht 3 x 6, r~, r_n)
     // as element pairs, and its cam slots: every global load issued before the
     // first wait (one round trip instead of one per loop trip), then scattered
-    // into the LDS rows ht [M][18] / rt [M][4].
+    // into the LDS rows ht [M][6][3] (Ht transposed: Ht[x][u] at 3 u + x, so the
+    // Y phase reads the (Ht[0][u], Ht[1][u]) operand pairs as adjacent words) /
+    // rt [M][4].
     int* coff = slot + ((Mmax + 3) & ~3);
-    T rn2 = 0;
     {
         constexpr int MCAP = (16 * NB - 4) / 3;   // the class's largest M (gm_class_exact)
         constexpr int NCH = (12 * MCAP + 63) / 64;
@@ -420,9 +423,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_wav
         for (int j = 0; j < NCH; ++j) {
             const int k = lane + 64 * j, o = k / 12, e = 2 * (k - 12 * o);   // elements e, e + 1 of record o
             if (k < 12 * M) {
-                if (e < OBS_RT) *reinterpret_cast<V2*>(ht + 18 * o + e) = cv[j];
-                else if (e < OBS_RT + 4) *reinterpret_cast<V2*>(rt + 4 * o + (e - OBS_RT)) = cv[j];
-                if (e == OBS_RT + 2) rn2 += cv[j].y * cv[j].y;   // r_n
+                if (e < OBS_RT) {   // Ht[x][u], Ht[x][u + 1] (e even: u <= 4)
+                    const int x = e / 6, u = e - 6 * x;
+                    T* d = ht + 18 * o + 3 * u + x;
+                    d[0] = cv[j].x;
+                    d[3] = cv[j].y;
+                } else if (e < OBS_RT + 4) {
+                    *reinterpret_cast<V2*>(rt + 4 * o + (e - OBS_RT)) = cv[j];
+                }
             }
         }
         // P offsets of the observations' cam blocks: row part (21 + 6 s) ldp + 21, column part 6 s
@@ -431,7 +439,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_wav
             coff[lane] = 6 * sl;
         }
     }
-    rn2 = wave_sum(rn2);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     // B rows [H_f~^T ; r~^T] over the 16 NB columns (zero past 3M) and the zero row
 #pragma unroll
@@ -440,10 +447,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_wav
         if (p < 16 * NB) {
             const bool pv = p < M3;
             const int o = pv ? p / 3 : 0, cp = p - 3 * o;
-            const T* h = ht + 18 * o + 6 * cp + 3;
+            const T* h = ht + 18 * o + 9 + cp;   // Ht[cp][3 + j] at h[3 j] (transposed rows)
             brow[p] = pv ? -h[0] : T(0);
-            brow[16 * NB + p] = pv ? -h[1] : T(0);
-            brow[32 * NB + p] = pv ? -h[2] : T(0);
+            brow[16 * NB + p] = pv ? -h[3] : T(0);
+            brow[32 * NB + p] = pv ? -h[6] : T(0);
             brow[48 * NB + p] = pv ? rt[4 * o + cp] : T(0);
             zrow[p] = T(0);
         }
@@ -515,7 +522,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_wav
                     __builtin_memcpy(pr, Pb + u * ldp, 6 * sizeof(T));
 #pragma unroll
                     for (int x = 0; x < 3; ++x) {
-                        const T h = Ha[6 * x + u];
+                        const T h = Ha[3 * u + x];
 #pragma unroll
                         for (int c = 0; c < 3; ++c)
                             t[x][c] = __builtin_elementwise_fma(V2{h, h}, V2{pr[2 * c], pr[2 * c + 1]}, t[x][c]);
@@ -531,8 +538,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_wav
                     T y2 = 0;
 #pragma unroll
                     for (int u = 0; u < 6; ++u) {
-                        y01 = __builtin_elementwise_fma(V2{t1[u], t1[u]}, V2{Hb[u], Hb[6 + u]}, y01);
-                        y2 = gfma(t1[u], Hb[12 + u], y2);
+                        y01 = __builtin_elementwise_fma(V2{t1[u], t1[u]}, V2{Hb[3 * u], Hb[3 * u + 1]}, y01);
+                        y2 = gfma(t1[u], Hb[3 * u + 2], y2);
                     }
                     dst[x][0] = y01.x;
                     dst[x][1] = y01.y;
@@ -584,13 +591,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_wav
                 pair_dst(pe[j], oa[j], dst);
                 V2 hb01[6];   // (Hb[0][u], Hb[1][u])
 #pragma unroll
-                for (int u = 0; u < 6; ++u) hb01[u] = V2{Hb[u], Hb[6 + u]};
+                for (int u = 0; u < 6; ++u) hb01[u] = V2{Hb[3 * u], Hb[3 * u + 1]};
 #pragma unroll
                 for (int x = 0; x < 3; ++x) {
                     V2 t2[3] = {V2{0, 0}, V2{0, 0}, V2{0, 0}};   // Ha[x] P as three column pairs
 #pragma unroll
                     for (int u = 0; u < 6; ++u) {
-                        const T h = Ha[6 * x + u];
+                        const T h = Ha[3 * u + x];
 #pragma unroll
                         for (int c = 0; c < 3; ++c)
                             t2[c] = __builtin_elementwise_fma(V2{h, h}, V2{Pl[j][6 * u + 2 * c], Pl[j][6 * u + 2 * c + 1]},
@@ -602,7 +609,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_wav
 #pragma unroll
                     for (int u = 0; u < 6; ++u) {
                         y01 = __builtin_elementwise_fma(V2{t1[u], t1[u]}, hb01[u], y01);
-                        y2 = gfma(t1[u], Hb[12 + u], y2);
+                        y2 = gfma(t1[u], Hb[3 * u + 2], y2);
                     }
                     dst[x][0] = y01.x;
                     dst[x][1] = y01.y;
@@ -629,6 +636,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_wav
 
     // ---- blocked LDL^T, 4 pivots per step, MFMA trailing updates ----
     const bool fail = gm_eliminate<T, NB>(acc, pan, lane);
+    // |r_n|^2 from the LDS records (rt is outside the stage / panel area): not
+    // held in a register across the whole kernel
+    T rn2 = lane < M ? rt[4 * lane + 3] * rt[4 * lane + 3] : T(0);
+    rn2 = wave_sum(rn2);
     GPROBE_T(t_e1);
     gm_finish<T, NB>(acc, pan, NB, lane, fail, rn2, s2, chi2, fb, f);
     GPROBE_T(t_end);

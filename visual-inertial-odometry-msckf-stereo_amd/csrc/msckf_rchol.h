@@ -40,6 +40,14 @@ __device__ __forceinline__ double pivot_floored(double x, double floor) {
     return pivot_floored(x, floor, -PIVOT_FLOOR_NEG * floor);
 }
 constexpr int RB = 18;   // doubles per 4-row block of the LDS column buffer
+// 1 / sqrt(x): the hardware reciprocal square root plus one Newton step (about
+// 1 ulp); the pivot is x * rchol_rsq(x).  No square root or division on the
+// diagonal factor's dependent chain, which every thread of the workgroup waits
+// for once per step.  x <= 0 or NaN gives NaN or a zero pivot: the step fails.
+__device__ __forceinline__ double rchol_rsq(double x) {
+    const double r = __builtin_amdgcn_rsq(x);
+    return r * fma(-0.5 * x * r, r, 1.5);
+}
 
 // TILE_LOAD: load(i0, j0, tile) fills a whole 4x4 tile (rows i0.., cols j0..)
 // instead of being called per element (lets a loader share operands).
@@ -95,17 +103,13 @@ __device__ __forceinline__ bool rchol_core(int nrow, int ncol, int nelim, double
 #pragma unroll
                 for (int y = 0; y < 4; ++y) dst[4 * x + y] = a[s][x][y];
             if (RTI(s) == tj) {   // the diagonal tile's owner factors it once for everyone
-                const double l00 = sqrt(fl(a[s][0][0]));
-                const double i00 = 1.0 / l00;
+                const double p0 = fl(a[s][0][0]), i00 = rchol_rsq(p0), l00 = p0 * i00;
                 const double l10 = a[s][1][0] * i00, l20 = a[s][2][0] * i00, l30 = a[s][3][0] * i00;
-                const double l11 = sqrt(fl(a[s][1][1] - l10 * l10));
-                const double i11 = 1.0 / l11;
+                const double p1 = fl(a[s][1][1] - l10 * l10), i11 = rchol_rsq(p1), l11 = p1 * i11;
                 const double l21 = (a[s][2][1] - l20 * l10) * i11, l31 = (a[s][3][1] - l30 * l10) * i11;
-                const double l22 = sqrt(fl(a[s][2][2] - l20 * l20 - l21 * l21));
-                const double i22 = 1.0 / l22;
+                const double p2 = fl(a[s][2][2] - l20 * l20 - l21 * l21), i22 = rchol_rsq(p2), l22 = p2 * i22;
                 const double l32 = (a[s][3][2] - l30 * l20 - l31 * l21) * i22;
-                const double l33 = sqrt(fl(a[s][3][3] - l30 * l30 - l31 * l31 - l32 * l32));
-                const double i33 = 1.0 / l33;
+                const double p3 = fl(a[s][3][3] - l30 * l30 - l31 * l31 - l32 * l32), i33 = rchol_rsq(p3), l33 = p3 * i33;
                 fj[0] = l00; fj[1] = l10; fj[2] = l20; fj[3] = l30;
                 fj[4] = l11; fj[5] = l21; fj[6] = l31; fj[7] = l22;
                 fj[8] = l32; fj[9] = l33; fj[10] = i00; fj[11] = i11;
