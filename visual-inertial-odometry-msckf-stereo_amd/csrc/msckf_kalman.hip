@@ -917,6 +917,213 @@ __global__ void __launch_bounds__(64 * NW) k_kal_e1(DevState<T> st, Params<T> pr
 }
 
 // ===========================================================================
+// Stages A and C1 on the matrix cores (round 4, k_kal_mchol): the partial
+// Cholesky of rchol_core, 4 pivots per step, with the matrix held as 16 x 16
+// fp64 MFMA accumulator blocks (result layout: lane l holds rows (l >> 4) + 4 i
+// of column l & 15) spread round-robin over NW waves, and the trailing rank-4
+// update of each block one v_mfma_f64_16x16x4f64:
+//     C -= X A_d^-1 X^T = C + (X m) X^T,   m = -A_d^-1 e_(l >> 4),
+// X = the step's four pivot columns, dumped to a double-buffered LDS panel by
+// the lanes that own them (one barrier per step).  Every lane factors the 4 x 4
+// A_d = L D L^T itself from the panel (one fp64 chain: hardware reciprocals
+// with a Newton step, no division or square root), the Cholesky columns
+// Y = X L_d^-T of the step (Lc / Vc_i in A, L_T in C1) are formed one panel row
+// per thread and stored.  Pivot floors as rchol_core (stage A: rounding-level
+// negatives; C1: T >= s2 I).  Stage A retries a failed filter with a shifted
+// P_cc in the same launch (rare; the register-tile kernel needed a second
+// launch over every filter for it).
+// ===========================================================================
+constexpr int MK_PS = 4;   // doubles per panel row (the step's four columns)
+
+__device__ __forceinline__ double mk_rcp(double x) {   // 1 / x: hardware reciprocal + one Newton step
+    const double r = __builtin_amdgcn_rcp(x);
+    return r * fma(-x, r, 2.0);
+}
+
+__host__ __device__ constexpr int mk_lds_doubles(int NBR) { return 2 * 16 * NBR * MK_PS + 16; }
+
+// One factorisation of filter b (stage A: P_cc + shift I).  Returns false on a
+// failed pivot; all outputs written on success.
+template <typename T, int NW, int NBR, int STAGE>
+__device__ __forceinline__ bool mk_factor(const DevState<T>& st, const UpdWs<T>& ws, int b, double shift,
+                                          double floor, double lo, double* pan0) {
+    constexpr int NBLK = NBR * (NBR + 1) / 2, SL = (NBLK + NW - 1) / NW;
+    const int tid = threadIdx.x, lane = tid & 63, lc = lane & 15, lr = lane >> 4;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int C = 6 * st.ncams[b], Cp = round4(C);
+    const int nrows = STAGE == 0 ? Cp + KW : C;   // rows beyond: identity padding up to 16 NBR
+    const int nsteps = Cp / 4;
+    const int ld = st.Dmax, Cpw = ws.Cp, ldt = ws.Cmax + 1;
+    const T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
+    KT* Lc = ws.Lc + (size_t)b * Cpw * Cpw;
+    KT* Vi = ws.Vi + (size_t)b * KW * Cpw;
+    KT* Sii = ws.Sii + (size_t)b * KW * KW;
+    const KT* Tm = ws.Tm + (size_t)b * ws.Cmax * ldt;
+    KT* LT = ws.G + (size_t)b * ws.Cmax * ldt;
+    // stage A index space [cams (Cp) | IMU (24)]: P row of index i (-1: padding)
+    auto map = [&](int i) { return i < C ? 21 + i : (i < Cp ? -1 : (i < Cp + 21 ? i - Cp : -1)); };
+    auto load = [&](int i, int j) -> double {
+        if (STAGE == 0) {
+            const int mi = map(i), mj = map(j);
+            if (mi < 0 || mj < 0) return i == j ? 1.0 : 0.0;
+            return (double)P[(size_t)mi * ld + mj] + (i == j && i < C ? shift : 0.0);
+        } else {
+            if (i >= C || j >= C) return i == j ? 1.0 : 0.0;
+            return i >= j ? Tm[(size_t)i * ldt + j] : Tm[(size_t)j * ldt + i];
+        }
+    };
+    // blocks of this wave: t = wv + NW j, column-major lower order
+    int brow[SL], bcol[SL];
+#pragma unroll
+    for (int j = 0; j < SL; ++j) {
+        const int t = wv + NW * j;
+        int cb = 0, rem = t;
+        while (cb < NBR && rem >= NBR - cb) { rem -= NBR - cb; ++cb; }
+        brow[j] = t < NBLK ? cb + rem : -1;
+        bcol[j] = t < NBLK ? cb : NBR;   // an empty slot matches no column
+    }
+    using v4d_t = double __attribute__((ext_vector_type(4)));
+    v4d_t acc[SL];
+#pragma unroll
+    for (int j = 0; j < SL; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            acc[j][q] = brow[j] >= 0 ? load(16 * brow[j] + lr + 4 * q, 16 * bcol[j] + lc) : 0.0;
+#ifdef MSCKF_MK_SB
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+    const double oh[4] = {lr == 0 ? 1.0 : 0.0, lr == 1 ? 1.0 : 0.0, lr == 2 ? 1.0 : 0.0, lr == 3 ? 1.0 : 0.0};
+    for (int s = 0; s < nsteps; ++s) {
+        const int KB = s >> 2, sc = s & 3, p0 = 4 * s;
+        double* pan = pan0 + (s & 1) * 16 * NBR * MK_PS;
+        // 1. the owners of columns p0 .. p0 + 3 dump them (rows of block column KB)
+        if ((lc >> 2) == sc) {
+#pragma unroll
+            for (int j = 0; j < SL; ++j) {
+                if (bcol[j] != KB) continue;   // uniform
+                double* d = pan + (16 * brow[j] + lr) * MK_PS + (lc & 3);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) d[4 * q * MK_PS] = acc[j][q];
+            }
+        }
+        __syncthreads();
+        // 2. A_d = L D L^T (lower entries of the panel's rows p0 .. p0 + 3), floored pivots
+        const double* ad = pan + p0 * MK_PS;
+        const double a10 = ad[4], a20 = ad[8], a30 = ad[12];
+        const double a21 = ad[9], a31 = ad[13], a32 = ad[14];
+        const double d0 = pivot_floored(ad[0], floor, lo), e0 = mk_rcp(d0);
+        const double l10 = a10 * e0, l20 = a20 * e0, l30 = a30 * e0;
+        const double d1 = pivot_floored(ad[5] - l10 * a10, floor, lo), e1 = mk_rcp(d1);
+        const double m21 = a21 - l20 * a10, m31 = a31 - l30 * a10;
+        const double l21 = m21 * e1, l31 = m31 * e1;
+        const double d2 = pivot_floored(ad[10] - l20 * a20 - l21 * m21, floor, lo), e2 = mk_rcp(d2);
+        const double m32 = a32 - l30 * a20 - l31 * m21;
+        const double l32 = m32 * e2;
+        const double d3 = pivot_floored(ad[15] - l30 * a30 - l31 * m31 - l32 * m32, floor, lo), e3 = mk_rcp(d3);
+        if (!(d0 > 0.0) || !(d1 > 0.0) || !(d2 > 0.0) || !(d3 > 0.0)) {   // uniform
+            __syncthreads();   // every wave's panel reads are done before a retry's dumps
+            return false;
+        }
+        // 3. Cholesky columns p0 .. p0 + 3: y = x L_u^-T D^-1/2, one panel row per thread
+        {
+            const int r = p0 + tid;
+            if (r < nrows) {
+                const double* x = pan + r * MK_PS;
+                const double z0 = x[0], z1 = x[1] - l10 * z0, z2 = x[2] - l20 * z0 - l21 * z1;
+                const double z3 = x[3] - l30 * z0 - l31 * z1 - l32 * z2;
+                const int k = r - p0;   // rows of the diagonal block: zeros above the diagonal
+                const double y0 = z0 * rchol_rsq(d0);
+                const double y1 = k >= 1 ? z1 * rchol_rsq(d1) : 0.0;
+                const double y2 = k >= 2 ? z2 * rchol_rsq(d2) : 0.0;
+                const double y3 = k >= 3 ? z3 * rchol_rsq(d3) : 0.0;
+                if (STAGE == 0) {
+                    KT* dst = r < Cp ? Lc + (size_t)r * Cpw + p0 : Vi + (size_t)(r - Cp) * Cpw + p0;
+                    dst[0] = y0; dst[1] = y1; dst[2] = y2; dst[3] = y3;
+                } else {
+                    KT* dst = LT + (size_t)r * ldt + p0;
+                    dst[0] = y0;
+                    if (p0 + 1 < C) dst[1] = y1;
+                    if (p0 + 2 < C) dst[2] = y2;
+                    if (p0 + 3 < C) dst[3] = y3;
+                }
+            }
+        }
+        // 4. m = -A_d^-1 e_lr (h = L^-1 e, u = D^-1 h, m = L^-T u), then the
+        //    rank-4 update of every block right of the pivots
+        const double h0 = oh[0];
+        const double h1 = fma(-l10, h0, oh[1]);
+        const double h2 = fma(-l21, h1, fma(-l20, h0, oh[2]));
+        const double h3 = fma(-l32, h2, fma(-l31, h1, fma(-l30, h0, oh[3])));
+        const double u0 = h0 * e0, u1 = h1 * e1, u2 = h2 * e2, u3 = h3 * e3;
+        const double w2 = fma(-l32, u3, u2);
+        const double w1 = fma(-l31, u3, fma(-l21, w2, u1));
+        const double w0 = fma(-l30, u3, fma(-l20, w2, fma(-l10, w1, u0)));
+#pragma unroll
+        for (int j = 0; j < SL; ++j) {
+            if (brow[j] < 0 || bcol[j] < KB || (bcol[j] == KB && sc == 3)) continue;   // uniform
+            const double* xr = pan + (16 * brow[j] + lc) * MK_PS;
+            const double av = -(xr[0] * w0 + xr[1] * w1 + xr[2] * w2 + xr[3] * u3);
+            const double bv = pan[(16 * bcol[j] + lc) * MK_PS + lr];
+            acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[j], 0, 0, 0);
+#ifdef MSCKF_MK_SB
+            __builtin_amdgcn_sched_barrier(0);   // one slot's operands in flight
+#endif
+        }
+    }
+    if (STAGE == 0) {   // S_ii: the Schur complement left in rows / columns >= Cp (lower part)
+#pragma unroll
+        for (int j = 0; j < SL; ++j) {
+            if (brow[j] < 0 || 16 * bcol[j] + 15 < Cp) continue;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int i = 16 * brow[j] + lr + 4 * q, c = 16 * bcol[j] + lc;
+                if (i >= Cp && c >= Cp && c <= i && i < Cp + KW) Sii[(i - Cp) * KW + (c - Cp)] = acc[j][q];
+            }
+        }
+    }
+    __syncthreads();
+    return true;
+}
+
+// one workgroup per filter (RETRY: stage A's shifted retries, a few
+// workgroups looping over the filters whose first factorisation failed)
+// two filters per CU: NW / 2 waves per SIMD each
+__host__ __device__ constexpr int mk_wpe(int NW) { return NW <= 4 ? 2 : (NW <= 8 ? 4 : 8); }
+
+template <typename T, int NW, int NBR, int STAGE, bool RETRY = false>
+__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(mk_wpe(NW))))
+k_kal_mchol(DevState<T> st, UpdWs<T> ws) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    double* pan0 = reinterpret_cast<double*>(smem_raw);   // [2][16 NBR][MK_PS]
+    double* red = pan0 + 2 * 16 * NBR * MK_PS;             // 16 doubles of reduction scratch
+    const int tid = threadIdx.x;
+    if (STAGE == 1) {
+        const int b = blockIdx.x;
+        if (ws.info[4 * b] == 0) return;
+        if (ws.afail[b]) {   // stage A failed (P_cc not PD): no update for this filter
+            if (tid == 0) ws.info[4 * b + 3] = -1;
+            return;
+        }
+        // T = s2 I + Lc^T A Lc >= s2 I: pivots below s2 are rounding (k_kal_c1)
+        const bool ok = mk_factor<T, NW, NBR, 1>(st, ws, b, 0.0, ws.s2, -INFINITY, pan0);
+        if (!ok && tid == 0) ws.info[4 * b + 3] = -1;
+        return;
+    }
+    for (int b = blockIdx.x; b < st.B; b += gridDim.x) {
+        if (RETRY && ws.afail[b] == 0) continue;   // uniform
+        const int C = 6 * st.ncams[b];
+        const double floor = pcc_pivot_floor(st.P + (size_t)b * st.Dmax * st.Dmax, st.Dmax, C, red);
+        bool ok = false;
+        for (int att = RETRY ? 1 : 0; att < (RETRY ? 3 : 1) && !ok; ++att) {
+            const double shift = att == 0 ? 0.0 : (att == 1 ? 1e-8 : 1e-6) * (floor / KALMAN_PIVOT_FLOOR);
+            ok = mk_factor<T, NW, NBR, 0>(st, ws, b, shift, floor, -PIVOT_FLOOR_NEG * floor, pan0);
+        }
+        if (tid == 0) ws.afail[b] = ok ? 0 : 1;   // read by stage C
+        if (!RETRY) break;
+    }
+}
+
+// ===========================================================================
 // Host side
 // ===========================================================================
 struct RcholCfg { int nt, tpl; };
@@ -1002,9 +1209,43 @@ static void launch_b(hipStream_t s, const DevState<T>& st, const Params<T>& prm,
     hipLaunchKernelGGL((k_kal_b<T, NW, WR, WC, NTM>), dim3(st.B), dim3(64 * NW), lds, s, st, prm, ws);
 }
 
+// k_kal_mchol launches: NBR = block rows (exact for the bench window, 12 / 13),
+// NW waves per filter
+#ifndef MSCKF_MK_NW
+#define MSCKF_MK_NW 4
+#endif
+template <typename T, int STAGE, int NBR>
+static void launch_mk_nbr(hipStream_t s, const DevState<T>& st, const UpdWs<T>& ws) {
+    constexpr int NW = NBR <= 6 ? 4 : MSCKF_MK_NW;
+    const size_t lds = mk_lds_doubles(NBR) * sizeof(double);
+    hipLaunchKernelGGL((k_kal_mchol<T, NW, NBR, STAGE>), dim3(st.B), dim3(64 * NW), lds, s, st, ws);
+    // stage A near-singular P_cc: shifted retries of the failed filters only
+    // (64 workgroups walk the filter list; none do any work on a healthy batch)
+    if constexpr (STAGE == 0)
+        hipLaunchKernelGGL((k_kal_mchol<T, NW, NBR, STAGE, true>), dim3(st.B < 64 ? st.B : 64), dim3(64 * NW), lds, s,
+                           st, ws);
+}
+template <typename T, int STAGE>
+static void launch_mk(hipStream_t s, const DevState<T>& st, const UpdWs<T>& ws, int nbr) {
+    if (nbr <= 4) launch_mk_nbr<T, STAGE, 4>(s, st, ws);
+    else if (nbr <= 6) launch_mk_nbr<T, STAGE, 6>(s, st, ws);
+    else if (nbr <= 8) launch_mk_nbr<T, STAGE, 8>(s, st, ws);
+    else if (nbr <= 10) launch_mk_nbr<T, STAGE, 10>(s, st, ws);
+    else if (nbr <= 11) launch_mk_nbr<T, STAGE, 11>(s, st, ws);
+    else if (nbr <= 12) launch_mk_nbr<T, STAGE, 12>(s, st, ws);
+    else if (nbr <= 13) launch_mk_nbr<T, STAGE, 13>(s, st, ws);
+    else launch_mk_nbr<T, STAGE, 14>(s, st, ws);
+}
+
 template <typename T>
 void launch_kalman_a_reg(hipStream_t s, const DevState<T>& st, const UpdWs<T>& ws, KernelTimer* kt) {
     const int Cp = (ws.Cmax + 3) & ~3;
+#ifndef MSCKF_KAL_RCHOL
+    kt->begin(s, "kalman_a");
+    launch_mk<T, 0>(s, st, ws, (Cp + KW + 15) / 16);
+    kt->end(s);
+    return;
+#endif
     const int nrow = (Cp + KW) / 4;   // stage A, 4x4 register tiles
     RcholCfg c;
     pick_rchol(nrow * (nrow + 1) / 2, c);
@@ -1019,7 +1260,7 @@ void launch_kalman_a_reg(hipStream_t s, const DevState<T>& st, const UpdWs<T>& w
 template <typename T>
 void launch_kalman_chol(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const UpdWs<T>& ws,
                         KernelTimer* kt) {
-    const int Cp = (ws.Cmax + 3) & ~3, Cmax = ws.Cmax;
+    const int Cmax = ws.Cmax;
     const bool reg = kalman_chol_supported(Cmax);   // else large window: global-memory stages A and C
     const int Cq = (Cmax + 15) & ~15;
     if (!reg) {   // (register-tile stage A: launch_kalman_a_reg, on the side stream)
@@ -1040,13 +1281,17 @@ void launch_kalman_chol(hipStream_t s, const DevState<T>& st, const Params<T>& p
     kt->end(s);
     kt->begin(s, "kalman_c");
     if (reg) {   // C1: Cholesky of T (register tiles); C2: MFMA forward substitution of the extra rows
-        const int nTc = Cp / 4;
+#ifndef MSCKF_KAL_RCHOL
+        launch_mk<T, 1>(s, st, ws, (Cmax + 15) / 16);
+#else
+        const int nTc = ((Cmax + 3) & ~3) / 4;
         RcholCfg c;
         pick_rchol(nTc * (nTc + 1) / 2, c);
         const size_t lds = rchol_lds_doubles(nTc) * sizeof(double);
         if (c.nt == 256 && c.tpl == 4) launch_c1<T, 256, 4>(s, st, ws, lds);
         else if (c.nt == 256) launch_c1<T, 256, 6>(s, st, ws, lds);
         else launch_c1<T, 512, 4>(s, st, ws, lds);
+#endif
         if (Cq <= 16 * 8) launch_c2<T, 7, 2, 8>(s, st, ws);
         else launch_c2<T, 13, 1, 12>(s, st, ws);
     } else {
