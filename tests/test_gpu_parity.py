@@ -295,6 +295,25 @@ def test_batched_fp64_vs_oracle(N, F, B, cap):
         np.testing.assert_allclose(unpack_imu(imu)["p"], st.imu.p, atol=1e-10)
 
 
+@pytest.mark.parametrize("kal", ["mfma", "tiles"])
+@pytest.mark.parametrize("N,F,B,cap", [(30, 200, 2, 30), (32, 80, 1, None), (20, 120, 3, None)])
+def test_kalman_cholesky_paths_vs_oracle(kal, N, F, B, cap, monkeypatch):
+    """Both implementations of the Kalman stages A / C1 on the same inputs
+    (MSCKF_KALMAN_CHOL forces one; by default batches of >= 64 filters take
+    the fp64 MFMA partial Cholesky k_kal_mchol, smaller ones the register
+    tiles of msckf_rchol.h): fp64 context against the oracle, P <= 1e-9."""
+    monkeypatch.setenv("MSCKF_KALMAN_CHOL", kal)
+    problems = [synth.make_update_problem(N, F, seed=300 + b) for b in range(B)]
+    ctx, ds, feat_off, acc, gam, pw, valid, rows = _batched(problems, np.float64, cap=cap)
+    for b, d in enumerate(ds):
+        st, acc_o, tri_p, tri_ok, gam_o = oracle_update(d)
+        sl = slice(feat_off[b], feat_off[b + 1])
+        np.testing.assert_array_equal(acc[sl], acc_o)
+        imu, cams, P = ctx.get_state(b)
+        assert rel(P, st.P) < 1e-9
+        np.testing.assert_allclose(cams[:, 4:7], np.stack([c.p for c in st.cams.values()]), atol=1e-10)
+
+
 def check_fp32_batch(problems, cap):
     """fp32 context (P, state, triangulation and gating in fp32; Jacobians,
     assembly and Kalman in fp64) against the oracle, in two parts:
@@ -495,6 +514,17 @@ def test_sequence_golden(name):
     tolerance).  s1: EuRoC config, 200 frames; s2: check_motion at translation
     threshold 0.2 (feature.py:124-165); s3: online_reset firing at position
     std 0.11 m (msckf.py:859-886).  (s4: test_sequence_s4_degenerate.)"""
+    _check_sequence(name)
+
+
+def test_sequence_s1_mfma_cholesky(monkeypatch):
+    """s1 with the Kalman stages A / C1 forced onto k_kal_mchol (a batch of
+    one takes the register tiles by default)."""
+    monkeypatch.setenv("MSCKF_KALMAN_CHOL", "mfma")
+    _check_sequence("sequence_s1")
+
+
+def _check_sequence(name):
     g = golden(name)
     seq = synth.make_sequence(int(g["n_frames"]), int(g["seed"]))
     flt = msckf_amd.MSCKF(sequence_config(g))

@@ -528,13 +528,15 @@ int run_update_chain(msckf_ctx* c, int row_cap, bool triangulate) {
     Params<T> prm = make_params<T>(c);
     FeatBatch<T> fb = feat_batch<T>(c);
     UpdWs<T> ws = upd_ws<T>(c);
+    // stage A (register-tile windows) under the Jacobians and gating
+    const bool early_a = kalman_chol_supported(c->Cmax);
+#ifndef MSCKF_A_FORK_EARLY
     if (triangulate) {
         c->timer.begin(s, "triangulate");
         launch_triangulate<T>(s, st, prm, fb, c->sc);
         c->timer.end(s);
     }
-    // stage A (register-tile windows) under the Jacobians and gating
-    const bool early_a = kalman_chol_supported(c->Cmax);
+#endif
     // Once stage A is on the side stream, every exit path joins it: an early
     // return must not leave k_kal_a reading P while a later call (restore,
     // set_state) on the main stream overwrites it.
@@ -552,6 +554,13 @@ int run_update_chain(msckf_ctx* c, int row_cap, bool triangulate) {
         launch_kalman_a_reg<T>(c->side, st, ws, &c->timer);
         HIPC(hipEventRecord(c->ev_join, c->side));
     }
+#ifdef MSCKF_A_FORK_EARLY
+    if (triangulate) {
+        c->timer.begin(s, "triangulate");
+        launch_triangulate<T>(s, st, prm, fb, c->sc);
+        c->timer.end(s);
+    }
+#endif
     c->timer.begin(s, "feature_jacobian");
     launch_feature<T>(s, st, prm, fb, c->sc);
     c->timer.end(s);

@@ -945,7 +945,10 @@ void launch_nb(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const
     // measured 2.47 ms against 2.52 ms for 36 -- profiles/r03/ab_gate_kb/; fp64
     // keeps 72, its two waves per SIMD already fill the LDS)
     // (round 4: the staging is the dense lower matrix, capacities in elements)
-    constexpr int single_kb = sizeof(T) == 4 ? 44 : 72;
+#ifndef GATE_SINGLE_KB
+#define GATE_SINGLE_KB 44
+#endif
+    constexpr int single_kb = sizeof(T) == 4 ? GATE_SINGLE_KB : 72;
     constexpr int RS = GM<T>::RS;
     const int full = gm_dense(0, Mmax - 1);
     int cmin = 0;   // one block row per pass at least
@@ -954,10 +957,11 @@ void launch_nb(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const
         cmin = gm_dense(alo, ahi) > cmin ? gm_dense(alo, ahi) : cmin;
     }
     auto per_wave = [&](int cf) { return (size_t)gm_wave_floats(Mmax, cf, RS) * sizeof(T); };
+    // single pass if four waves' LDS fits single_kb, else the largest stage
+    // that does (at least one block row)
     int capf = full;
-    if (4 * per_wave(capf) > (size_t)single_kb * 1024)
-        for (int parts = 2; 4 * per_wave(capf) > (size_t)single_kb * 512 && capf > cmin; ++parts)
-            capf = (full + parts - 1) / parts > cmin ? (full + parts - 1) / parts : cmin;
+    while (capf > cmin && 4 * per_wave(capf) > (size_t)single_kb * 1024) capf -= 32;
+    if (capf < cmin) capf = cmin;
     const size_t pw = per_wave(capf);
     // one wave per workgroup: a wave's LDS and registers are released as soon as
     // its feature is done, not when the slowest of four features sharing a

@@ -21,6 +21,8 @@
 #include "msckf_launch.h"
 #include "msckf_rchol.h"
 
+#include <stdlib.h>
+
 namespace msckf {
 
 constexpr int KW = 24;   // IMU block padded to a multiple of 4
@@ -1237,15 +1239,36 @@ static void launch_mk(hipStream_t s, const DevState<T>& st, const UpdWs<T>& ws, 
     else launch_mk_nbr<T, STAGE, 14>(s, st, ws);
 }
 
+// Batches large enough to fill the chip run stages A / C1 on the matrix cores
+// (throughput: two filters per CU, VALU-light); a handful of filters (the
+// drop-in per-frame path, B = 1) keeps the register tiles, whose 4-pivot
+// steps have the shorter latency (B = 1, 20 cams, fp64: A 57 vs 68 us).
+#ifndef MSCKF_MK_MIN_B
+#define MSCKF_MK_MIN_B 64
+#endif
+// MSCKF_KALMAN_CHOL=mfma / tiles (environment, read per launch) forces one
+// path -- the parity tests run both on the same inputs.
+template <typename T> static bool use_mk(const DevState<T>& st) {
+#ifdef MSCKF_KAL_RCHOL
+    return false;
+#else
+    if (const char* e = getenv("MSCKF_KALMAN_CHOL")) {
+        if (e[0] == 'm') return true;
+        if (e[0] == 't') return false;
+    }
+    return st.B >= MSCKF_MK_MIN_B;
+#endif
+}
+
 template <typename T>
 void launch_kalman_a_reg(hipStream_t s, const DevState<T>& st, const UpdWs<T>& ws, KernelTimer* kt) {
     const int Cp = (ws.Cmax + 3) & ~3;
-#ifndef MSCKF_KAL_RCHOL
-    kt->begin(s, "kalman_a");
-    launch_mk<T, 0>(s, st, ws, (Cp + KW + 15) / 16);
-    kt->end(s);
-    return;
-#endif
+    if (use_mk(st)) {
+        kt->begin(s, "kalman_a");
+        launch_mk<T, 0>(s, st, ws, (Cp + KW + 15) / 16);
+        kt->end(s);
+        return;
+    }
     const int nrow = (Cp + KW) / 4;   // stage A, 4x4 register tiles
     RcholCfg c;
     pick_rchol(nrow * (nrow + 1) / 2, c);
@@ -1281,17 +1304,17 @@ void launch_kalman_chol(hipStream_t s, const DevState<T>& st, const Params<T>& p
     kt->end(s);
     kt->begin(s, "kalman_c");
     if (reg) {   // C1: Cholesky of T (register tiles); C2: MFMA forward substitution of the extra rows
-#ifndef MSCKF_KAL_RCHOL
-        launch_mk<T, 1>(s, st, ws, (Cmax + 15) / 16);
-#else
-        const int nTc = ((Cmax + 3) & ~3) / 4;
-        RcholCfg c;
-        pick_rchol(nTc * (nTc + 1) / 2, c);
-        const size_t lds = rchol_lds_doubles(nTc) * sizeof(double);
-        if (c.nt == 256 && c.tpl == 4) launch_c1<T, 256, 4>(s, st, ws, lds);
-        else if (c.nt == 256) launch_c1<T, 256, 6>(s, st, ws, lds);
-        else launch_c1<T, 512, 4>(s, st, ws, lds);
-#endif
+        if (use_mk(st)) {
+            launch_mk<T, 1>(s, st, ws, (Cmax + 15) / 16);
+        } else {
+            const int nTc = ((Cmax + 3) & ~3) / 4;
+            RcholCfg c;
+            pick_rchol(nTc * (nTc + 1) / 2, c);
+            const size_t lds = rchol_lds_doubles(nTc) * sizeof(double);
+            if (c.nt == 256 && c.tpl == 4) launch_c1<T, 256, 4>(s, st, ws, lds);
+            else if (c.nt == 256) launch_c1<T, 256, 6>(s, st, ws, lds);
+            else launch_c1<T, 512, 4>(s, st, ws, lds);
+        }
         if (Cq <= 16 * 8) launch_c2<T, 7, 2, 8>(s, st, ws);
         else launch_c2<T, 13, 1, 12>(s, st, ws);
     } else {
