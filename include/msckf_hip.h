@@ -190,6 +190,10 @@ int msckf_sync(msckf_ctx_t* ctx);
 /* Per-kernel device time (HIP events on the context stream), accumulated
  * while profiling is on.  names: NUL-separated list written to names_out. */
 int msckf_set_profiling(msckf_ctx_t* ctx, int on);
+/* Profiling of ONE timer stage (e.g. "gate"): every other stage records no
+ * events, so the timed stream carries two event packets per step instead of
+ * two per stage.  stage == NULL turns profiling off. */
+int msckf_set_profiling_stage(msckf_ctx_t* ctx, const char* stage);
 int msckf_kernel_times(msckf_ctx_t* ctx, int max_k, double* ms_total, int32_t* launches,
                        char* names_out, int names_cap);
 

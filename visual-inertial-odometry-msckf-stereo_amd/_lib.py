@@ -77,6 +77,7 @@ _SIGS = {
     "msckf_restore": (C.c_int, [_P]),
     "msckf_sync": (C.c_int, [_P]),
     "msckf_set_profiling": (C.c_int, [_P, C.c_int]),
+    "msckf_set_profiling_stage": (C.c_int, [_P, C.c_char_p]),
     "msckf_kernel_times": (C.c_int, [_P, C.c_int, _D, _I, C.c_char_p, C.c_int]),
 }
 
@@ -425,6 +426,10 @@ class Context:
 
     def set_profiling(self, on=True):
         self._check(self.lib.msckf_set_profiling(self.h, 1 if on else 0))
+
+    def set_profiling_stage(self, stage):
+        """Time one stage only (None: profiling off)."""
+        self._check(self.lib.msckf_set_profiling_stage(self.h, None if stage is None else stage.encode()))
 
     def kernel_times(self):
         ms = np.zeros(64)

@@ -1228,6 +1228,17 @@ int msckf_set_profiling(msckf_ctx_t* c, int on) {
     HIPSYNC(c, hipStreamSynchronize(c->stream));
     c->timer.collect();
     c->timer.on = on != 0;
+    c->timer.only.clear();
+    c->timer.reset();
+    return 0;
+}
+
+int msckf_set_profiling_stage(msckf_ctx_t* c, const char* stage) {
+    if (!c) FAIL(-1, "null context");
+    HIPSYNC(c, hipStreamSynchronize(c->stream));
+    c->timer.collect();
+    c->timer.on = stage != nullptr;
+    c->timer.only = stage ? stage : "";
     c->timer.reset();
     return 0;
 }

@@ -1121,7 +1121,6 @@ k_kal_mchol(DevState<T> st, UpdWs<T> ws) {
             ok = mk_factor<T, NW, NBR, 0>(st, ws, b, shift, floor, -PIVOT_FLOOR_NEG * floor, pan0);
         }
         if (tid == 0) ws.afail[b] = ok ? 0 : 1;   // read by stage C
-        if (!RETRY) break;
     }
 }
 
@@ -1220,7 +1219,13 @@ template <typename T, int STAGE, int NBR>
 static void launch_mk_nbr(hipStream_t s, const DevState<T>& st, const UpdWs<T>& ws) {
     constexpr int NW = NBR <= 6 ? 4 : MSCKF_MK_NW;
     const size_t lds = mk_lds_doubles(NBR) * sizeof(double);
-    hipLaunchKernelGGL((k_kal_mchol<T, NW, NBR, STAGE>), dim3(st.B), dim3(64 * NW), lds, s, st, ws);
+    // stage A co-runs with k_feature / the gate on the side stream: a grid of
+    // MSCKF_A_GRID workgroups walking the filters leaves them CU room
+#ifndef MSCKF_A_GRID
+#define MSCKF_A_GRID 0
+#endif
+    const int grid = (STAGE == 0 && MSCKF_A_GRID > 0 && st.B > MSCKF_A_GRID) ? MSCKF_A_GRID : st.B;
+    hipLaunchKernelGGL((k_kal_mchol<T, NW, NBR, STAGE>), dim3(grid), dim3(64 * NW), lds, s, st, ws);
     // stage A near-singular P_cc: shifted retries of the failed filters only
     // (64 workgroups walk the filter list; none do any work on a healthy batch)
     if constexpr (STAGE == 0)

@@ -14,6 +14,8 @@ namespace msckf {
 // launch stream (so the measurement sees exactly the stream the kernel runs on).
 struct KernelTimer {
     bool on = false;
+    std::string only;    // non-empty: time this stage only (the others record no events)
+    bool open = false;   // the last begin() recorded an event
     struct Pending { std::string name; hipEvent_t a, b; };
     std::vector<Pending> pending;
     std::vector<std::string> names;
@@ -28,14 +30,16 @@ struct KernelTimer {
         return e;
     }
     void begin(hipStream_t s, const char* name) {
-        if (!on) return;
+        open = on && (only.empty() || only == name);
+        if (!open) return;
         Pending p{name, get(), get()};
         (void)hipEventRecord(p.a, s);
         pending.push_back(p);
     }
     void end(hipStream_t s) {
-        if (!on || pending.empty()) return;
+        if (!open || pending.empty()) return;
         (void)hipEventRecord(pending.back().b, s);
+        open = false;
     }
     // call after the stream is synchronised
     void collect() {
