@@ -479,6 +479,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_wav
     // assembled once, never read back.
     const T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
     const int ldp = st.Dmax;
+    const T* Prow[6];
+#pragma unroll
+    for (int u = 0; u < 6; ++u) Prow[u] = P + u * ldp;
     // pair blocks per lane in flight: the Y phase's VGPRs are free up to the
     // elimination's peak once the accumulators outgrow them (NB >= 5)
     constexpr int BIF = (MP || sizeof(T) == 8) ? 1 : (NB >= 5 ? GATE_BIF_BIG : 2);
@@ -508,7 +511,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_wav
             for (int kk = lane; kk < nbp; kk += 64) {
                 const unsigned pe = g_gm_pairs.v[kbase + kk];
                 const int a = pe & 0xff, bo = (pe >> 8) & 0xff;
-                const T* Pb = P + (slot[a] + coff[bo]);
+                const unsigned boff = (unsigned)(slot[a] + coff[bo]) * (unsigned)sizeof(T);
                 const T* Ha = ht + 18 * a;
                 const T* Hb = ht + 18 * bo;
                 V2 t[3][3];   // Ha[x] P as three column pairs
@@ -519,7 +522,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_wav
 #pragma unroll
                 for (int u = 0; u < 6; ++u) {
                     T pr[6];
-                    __builtin_memcpy(pr, Pb + u * ldp, 6 * sizeof(T));
+                    __builtin_memcpy(pr, reinterpret_cast<const char*>(Prow[u]) + boff, 6 * sizeof(T));
 #pragma unroll
                     for (int x = 0; x < 3; ++x) {
                         const T h = Ha[3 * u + x];
@@ -570,11 +573,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_wav
                 const int kk = k0 + 64 * j + lane;
                 oa[j] = pe[j] & 0xff;
                 ob[j] = (pe[j] >> 8) & 0xff;
-                const T* Pb = P + (slot[oa[j]] + coff[ob[j]]);
+                // row u of the block: the wave-uniform row base P + u ldp (SGPRs)
+                // plus the lane's 32-bit element offset -- no 64-bit address
+                // arithmetic per row
+                const unsigned boff = (unsigned)(slot[oa[j]] + coff[ob[j]]) * (unsigned)sizeof(T);
 #pragma unroll
                 for (int u = 0; u < 6; ++u) {
                     if (kk < nbp) {
-                        __builtin_memcpy(Pl[j] + 6 * u, Pb + u * ldp, 6 * sizeof(T));
+                        __builtin_memcpy(Pl[j] + 6 * u, reinterpret_cast<const char*>(Prow[u]) + boff, 6 * sizeof(T));
                     } else {
 #pragma unroll
                         for (int c2 = 0; c2 < 6; ++c2) Pl[j][6 * u + c2] = T(0);
