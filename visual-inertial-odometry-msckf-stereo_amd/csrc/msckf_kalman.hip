@@ -233,12 +233,23 @@ __global__ void __launch_bounds__(64 * NW) k_kal_c2(DevState<T> st, UpdWs<T> ws)
             pf[q] = e < 16 * w ? -Lv(16 * J + i, col) : 0.0;
         }
     };
+    // (C2_DB: block row J staged in buffer J & 1 -- the closing barrier of each
+    // step is then not needed, a later step's put never overwrites a buffer
+    // another wave may still read.  Measured equal to two barriers per step,
+    // 1.184-1.187 vs 1.187-1.188 ms; four accumulator chains instead of two:
+    // 1.42 ms, profiles/r04/ab_c2_*)
+#ifndef C2_DB
+#define C2_DB 1
+#endif
+    constexpr int IMGB = 16 * NTM * C2S;
+    auto imgJ = [&](int J) { return C2_DB ? img + (J & 1) * IMGB : img; };
     auto put = [&](int J) {
         const int w = 16 * J;
+        double* im = imgJ(J);
 #pragma unroll
         for (int q = 0; q < PFN; ++q) {
             const int e = tid + NT * q, i = e / w, col = e - i * w;
-            if (e < 16 * w) img[col * C2S + i] = pf[q];
+            if (e < 16 * w) im[col * C2S + i] = pf[q];
         }
     };
     __syncthreads();   // the diagonal-block scratch in img is dead
@@ -265,11 +276,12 @@ __global__ void __launch_bounds__(64 * NW) k_kal_c2(DevState<T> st, UpdWs<T> ws)
 #pragma unroll
                 for (int q = 0; q < 4; ++q) xn[t][q] = Xv(16 * ct + lc, 16 * (J + 1) + lr + 4 * q);
             }
+            const double* im = imgJ(J);
 #pragma unroll
             for (int K = 0; K < J; ++K) {
 #pragma unroll
                 for (int kc = 0; kc < 4; ++kc) {
-                    const double av = img[(16 * K + 4 * kc + lr) * C2S + lc];
+                    const double av = im[(16 * K + 4 * kc + lr) * C2S + lc];
                     if (K & 1) a1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, yk[t][K][kc], a1, 0, 0, 0);
                     else a0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, yk[t][K][kc], a0, 0, 0, 0);
                 }
@@ -281,7 +293,7 @@ __global__ void __launch_bounds__(64 * NW) k_kal_c2(DevState<T> st, UpdWs<T> ws)
                 y = __builtin_amdgcn_mfma_f64_16x16x4f64(LI[J * 256 + (4 * kc + lr) * 16 + lc], a0[kc], y, 0, 0, 0);
             yk[t][J] = y;
         }
-        __syncthreads();
+        if (!C2_DB) __syncthreads();
     }
 #pragma unroll
     for (int t = 0; t < CT; ++t) {
@@ -1188,8 +1200,9 @@ static void launch_c1(hipStream_t s, const DevState<T>& st, const UpdWs<T>& ws, 
 }
 template <typename T, int NW, int CT, int NTM>
 static void launch_c2(hipStream_t s, const DevState<T>& st, const UpdWs<T>& ws) {
+    // two staging buffers (C2_DB); the first also holds the diagonal-block scratch
     constexpr int IMG = 16 * NTM * C2S > NW * 272 ? 16 * NTM * C2S : NW * 272;
-    const size_t lds = (NTM * 256 + IMG) * sizeof(double);
+    const size_t lds = (NTM * 256 + (C2_DB ? 16 * NTM * C2S : 0) + IMG) * sizeof(double);
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)k_kal_c2<T, NW, CT, NTM>, hipFuncAttributeMaxDynamicSharedMemorySize,
