@@ -1003,9 +1003,6 @@ __device__ __forceinline__ bool mk_factor(const DevState<T>& st, const UpdWs<T>&
 #pragma unroll
         for (int q = 0; q < 4; ++q)
             acc[j][q] = brow[j] >= 0 ? load(16 * brow[j] + lr + 4 * q, 16 * bcol[j] + lc) : 0.0;
-#ifdef MSCKF_MK_SB
-    __builtin_amdgcn_sched_barrier(0);
-#endif
     const double oh[4] = {lr == 0 ? 1.0 : 0.0, lr == 1 ? 1.0 : 0.0, lr == 2 ? 1.0 : 0.0, lr == 3 ? 1.0 : 0.0};
     for (int s = 0; s < nsteps; ++s) {
         const int KB = s >> 2, sc = s & 3, p0 = 4 * s;
@@ -1079,9 +1076,6 @@ __device__ __forceinline__ bool mk_factor(const DevState<T>& st, const UpdWs<T>&
             const double av = -(xr[0] * w0 + xr[1] * w1 + xr[2] * w2 + xr[3] * u3);
             const double bv = pan[(16 * bcol[j] + lc) * MK_PS + lr];
             acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[j], 0, 0, 0);
-#ifdef MSCKF_MK_SB
-            __builtin_amdgcn_sched_barrier(0);   // one slot's operands in flight
-#endif
         }
     }
     if (STAGE == 0) {   // S_ii: the Schur complement left in rows / columns >= Cp (lower part)
