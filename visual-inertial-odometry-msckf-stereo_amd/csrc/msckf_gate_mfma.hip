@@ -140,6 +140,8 @@ static_assert(gm_class_exact(), "gating size classes must match the MFMA block c
 // through the multi-pass Y phase): the f64 classes.  (f32 NB = 5 / 6 streamed at
 // four waves per SIMD measured no faster -- 2.68 ms -- or slower with NB = 6's
 // spill -- 2.92 ms -- than the wide version at three.)
+// (round 4 again: fp32 NB = 5 streamed at four waves per SIMD, 123 VGPRs, no
+// spill, measured 2.32 ms against 2.19-2.21 -- profiles/r04/ab_gate_st5_*)
 __host__ __device__ constexpr bool gm_stream(int NB, int ts) { return ts == 8; }
 
 template <typename T, int NB, bool STREAM = gm_stream(NB, sizeof(T))>
