@@ -693,8 +693,17 @@ __global__ void __launch_bounds__(64 * NW) k_kal_b(DevState<T> st, Params<T> prm
         if (ph == 1 && tid < 16) bb[buf * 16 + tid] = rb;
     };
     // ---- phase 1: G = A Lc ----
+    // Lc is lower triangular, so chunk k0 only reaches the tile columns
+    // tc <= k0 / 16: wave (wr, wc) owns the rows BR wr .. BR wr + BR - 1 and the
+    // columns wc, wc + WC, wc + 2 WC, ... (interleaved, not a contiguous range),
+    // so every chunk's active columns are spread over all the waves instead of
+    // loading the first column group alone (one barrier per chunk)
+#ifndef KB_INTERLEAVE
+#define KB_INTERLEAVE 1
+#endif
     {
-        const int tr0 = BR * (wv / WC), tc0 = BC * (wv % WC);
+        const int tr0 = BR * (wv / WC), wc = wv % WC;
+        auto tcol = [&](int y) { return KB_INTERLEAVE ? wc + WC * y : BC * wc + y; };
         v4d acc[BR][BC];
 #pragma unroll
         for (int x = 0; x < BR; ++x)
@@ -716,14 +725,14 @@ __global__ void __launch_bounds__(64 * NW) k_kal_b(DevState<T> st, Params<T> prm
 #pragma unroll
                 for (int x = 0; x < BR; ++x) av[x] = tr0 + x < nT ? i0[kr + 16 * (tr0 + x) + lc] : 0.0;
 #pragma unroll
-                for (int y = 0; y < BC; ++y) bv[y] = tc0 + y < nT ? i1[kr + 16 * (tc0 + y) + lc] : 0.0;
+                for (int y = 0; y < BC; ++y) bv[y] = tcol(y) < nT ? i1[kr + 16 * tcol(y) + lc] : 0.0;
 #pragma unroll
                 for (int x = 0; x < BR; ++x) {
                     if (tr0 + x >= nT) continue;
 #pragma unroll
                     for (int y = 0; y < BC; ++y) {
                         // Lc[k][j] = 0 for j > k: column tile tc needs k >= 16 tc
-                        if (tc0 + y >= nT || k0 + 15 < 16 * (tc0 + y)) continue;
+                        if (tcol(y) >= nT || k0 + 15 < 16 * tcol(y)) continue;
                         acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[x], bv[y], acc[x][y], 0, 0, 0);
                     }
                 }
@@ -737,7 +746,7 @@ __global__ void __launch_bounds__(64 * NW) k_kal_b(DevState<T> st, Params<T> prm
             for (int y = 0; y < BC; ++y)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const int i = 16 * (tr0 + x) + lr + 4 * r, j = 16 * (tc0 + y) + lc;
+                    const int i = 16 * (tr0 + x) + lr + 4 * r, j = 16 * tcol(y) + lc;
                     if (i < C && j < C) G[(size_t)i * ld + j] = acc[x][y][r];
                 }
         __syncthreads();   // G visible to the whole workgroup before phase 2 streams it
