@@ -5,7 +5,7 @@ SRC      := $(PKG)/csrc
 LIB      := $(PKG)/libmsckf_hip.so
 HIPCC    ?= /opt/rocm/bin/hipcc
 ARCH     ?= gfx950
-HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-result -Iinclude -fno-slp-vectorize
+HIPFLAGS := --offload-arch=$(ARCH) --offload-compress -O3 -fPIC -std=c++17 -Wall -Wno-unused-result -Iinclude -fno-slp-vectorize
 OBJS     := $(SRC)/msckf_kernels.o $(SRC)/msckf_kalman.o $(SRC)/msckf_gate_mfma.o $(SRC)/msckf_api.o $(SRC)/msckf_frontend.o \
             $(SRC)/msckf_rccl.o
 HDRS     := $(SRC)/msckf_common.h $(SRC)/msckf_launch.h $(SRC)/msckf_rchol.h include/msckf_hip.h include/msckf_frontend.h \

@@ -158,6 +158,7 @@ struct msckf_ctx {
     // state
     DBuf<unsigned char> P, imu, cams, P_snap, imu_snap, cams_snap;
     DBuf<int> ncams, ncams_snap;
+    DBuf<int> ident;   // [0, B): a contiguous filter list needs no upload (upload_ints)
     // update workspace
     DBuf<unsigned char> Hthin, dx, Lc, Vi, Sii, G, Tm, W, Wk;
     DBuf<int> info, afail;
@@ -676,6 +677,12 @@ int do_create(msckf_ctx* c) {
     HIPC(c->imu.ensure(B * IMU_STRIDE * ts));
     HIPC(c->cams.ensure(B * c->Nmax * CAM_STRIDE * ts));
     HIPC(c->ncams.ensure(B));
+    {
+        std::vector<int> id(B);
+        for (size_t b = 0; b < B; ++b) id[b] = (int)b;
+        HIPC(c->ident.ensure(B));
+        HIPC(hipMemcpy(c->ident.p, id.data(), B * sizeof(int), hipMemcpyHostToDevice));
+    }
     HIPC(c->Hthin.ensure(B * c->Cmax * (c->Cmax + 1) * sizeof(KT)));
     HIPC(c->dx.ensure(B * (c->Dmax + c->Cmax) * sizeof(KT)));
     HIPC(c->info.ensure(4 * B));
@@ -783,6 +790,15 @@ int check_list(msckf_ctx* c, int nfilt, const int32_t* filters) {
 
 // uploads int lists to iscratch back to back; returns device pointers
 int upload_ints(msckf_ctx* c, std::initializer_list<const std::vector<int>*> lists, std::vector<const int*>& out) {
+    if (lists.size() == 1) {   // a run of consecutive slots (the single-filter path: [0]) is a slice of ident
+        const std::vector<int>& l = **lists.begin();
+        bool run = !l.empty() && l[0] >= 0 && l.back() < c->B;
+        for (size_t i = 1; run && i < l.size(); ++i) run = l[i] == l[i - 1] + 1;
+        if (run) {
+            out.assign(1, c->ident.p + l[0]);
+            return 0;
+        }
+    }
     size_t tot = 0;
     for (auto* l : lists) tot += l->size();
     HIPC(c->iscratch.ensure(tot + 1));
@@ -1083,7 +1099,7 @@ int msckf_destroy(msckf_ctx_t* c) {
     for (auto* b : {&c->P, &c->imu, &c->cams, &c->P_snap, &c->imu_snap, &c->cams_snap, &c->Hthin, &c->Lc, &c->Vi, &c->Sii, &c->G, &c->Tm, &c->W, &c->Wk,
                     &c->dx, &c->batch, &c->obs_ws, &c->obs_ht, &c->obs_g, &c->fqr, &c->tau, &c->ysq, &c->scratch})
         b->release();
-    for (auto* b : {&c->ncams, &c->ncams_snap, &c->info, &c->afail, &c->row_off, &c->iscratch})
+    for (auto* b : {&c->ncams, &c->ncams_snap, &c->ident, &c->info, &c->afail, &c->row_off, &c->iscratch})
         b->release();
     c->up.release();
     c->down.release();
