@@ -111,3 +111,38 @@ def test_readback_equals_separate_reads():
         assert rows == int(rows2[0]) and rows > 0
     finally:
         ms.close()
+
+
+@pytest.mark.parametrize("B", [4, 600])
+def test_readback_gather_and_copy_paths(B):
+    """msckf_readback moves a sync point's arrays to the host either with one
+    gather kernel that stores into the pinned buffer (<= 8 arrays and <= 1 MiB:
+    B = 4) or with one runtime copy per array (B = 600: the cam records of the
+    context alone are ~3 MB).  Both must return exactly what set_state stored
+    (fp64 context: bit-exact) and the listed filters' covariance diagonals, for
+    a scrambled filter list."""
+    from msckf_amd import FilterConfig
+    from msckf_amd._lib import CAM_LEN, IMU_LEN, Context
+    rng = np.random.default_rng(B)
+    N = 32
+    ctx = Context(FilterConfig(), n_filters=B, n_cam_capacity=N, dtype=np.float64)
+    try:
+        imus, camss, diags = [], [], []
+        for f in range(B):
+            n = int(rng.integers(2, N + 1))
+            D = 21 + 6 * n
+            imu = rng.standard_normal(IMU_LEN)
+            cams = rng.standard_normal((n, CAM_LEN))
+            P = np.diag(rng.uniform(0.5, 2.0, D)) + 1e-3 * np.ones((D, D))
+            ctx.set_state(f, imu, cams, P)
+            imus.append(imu)
+            camss.append(cams)
+            diags.append(np.diag(P).copy())
+        filters = rng.permutation(B)[:min(B, 64)]
+        imu_rb, cl, cv = ctx.readback(filters, cov=(3, 10))
+        for w, f in enumerate(filters):
+            np.testing.assert_array_equal(imu_rb[w], imus[f])
+            np.testing.assert_array_equal(cl[w], camss[f])
+            np.testing.assert_array_equal(cv[w], diags[f][3:13])
+    finally:
+        ctx.close()
