@@ -58,6 +58,9 @@ def parse():
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "fp64"])
     ap.add_argument("--unique", type=int, default=32, help="distinct synthetic problems tiled over the batch")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-baseline sample")
+    ap.add_argument("--rccl-timeout", type=float, default=1800.0,
+                    help="deadline (s) of every replica collective once RCCL is up (rank 0 runs the accuracy / "
+                         "ATE legs while the others wait in a barrier)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-fp64", action="store_true", help="skip the fp64-context leg")
     ap.add_argument("--no-ate", action="store_true", help="skip the ATE replay leg")
@@ -459,7 +462,7 @@ def main():
         cpu, refs = cpu_baseline(args, probs[:N_CHECK])
 
     ctx, feat_off = build_batch(args, probs, dtype, grp.local_rank)
-    transport = grp.attach_rccl(ctx.device_info()[0])   # barriers / max / gathers over RCCL from here on
+    transport = grp.attach_rccl(ctx.device_info()[0], collective_timeout_s=args.rccl_timeout)   # barriers / max / gathers over RCCL from here on
     devs = gather_devices(grp, ctx.device_info())
     el, times, timed = timed_update(ctx, args, grp)
     value = replicas.whole_job_rate(args.batch, grp.world, args.steps, el)

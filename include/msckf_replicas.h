@@ -43,8 +43,14 @@ int msckf_rccl_init(const uint8_t* id, int nranks, int rank, int hip_device, dou
 int msckf_rccl_allreduce(msckf_rccl_t* c, double* v, int n, int op);
 /* All-gather of nbytes per rank: all_out receives nranks * nbytes, rank order. */
 int msckf_rccl_allgather(msckf_rccl_t* c, const void* mine, int nbytes, void* all_out);
+/* Deadline (seconds) of every later wait on this communicator: collectives
+ * and the teardown.  A launcher whose ranks do unequal work between two
+ * collectives (rank 0's accuracy / ATE legs) sets it generously. */
+int msckf_rccl_set_timeout(msckf_rccl_t* c, double timeout_s);
 /* ncclCommCount (ranks in the communicator) and the communicator's rank. */
 int msckf_rccl_count(const msckf_rccl_t* c, int* count_out, int* rank_out);
+/* ncclCommFinalize, polled to completion, then ncclCommDestroy; a teardown
+ * that fails or outlives the deadline is aborted (returns -4). */
 int msckf_rccl_destroy(msckf_rccl_t* c);
 const char* msckf_rccl_last_error(void);
 

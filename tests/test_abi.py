@@ -52,7 +52,7 @@ def test_replica_transport_exports_and_binding():
     same library and typed one to one by the binding; librccl itself is opened
     only when a communicator is made (dlopen), so loading needs no RCCL."""
     syms = header_symbols("msckf_replicas.h", "msckf_rccl_")
-    assert sorted(_lib.REPLICA_EXPORTED) == syms and len(syms) == 7
+    assert sorted(_lib.REPLICA_EXPORTED) == syms and len(syms) == 8
     if not os.path.exists(_lib.LIB_PATH):
         pytest.skip("libmsckf_hip.so not built")
     lib = ctypes.CDLL(_lib.LIB_PATH)

@@ -380,20 +380,23 @@ def test_batched_fp32_80x1000_vs_oracle():
     check_fp32_batch(problems, 80)
 
 
-@pytest.mark.parametrize("N,F,B,cap", [(30, 200, 2, 30), (40, 150, 2, None), (82, 50, 1, None)])
+@pytest.mark.parametrize("N,F,B,cap", [(30, 200, 2, 30), (40, 150, 2, None), (82, 50, 1, None), (100, 70, 1, None)])
 def test_gate_fp32_gamma_vs_oracle(N, F, B, cap):
     """fp32 gating on MFMA tiles against the oracle's fp64 gamma
     (msckf.py:606-614).  N = 30 (cam capacity 30, the bench's workload);
     N = 40: every one-wave size class (1..8 16-row blocks,
     single- and multi-pass Y staging); N = 82: also the four-wave workgroup
-    kernel for 40 < M <= 82 (up to 16 blocks, Y staged in passes).  Tolerance:
+    kernel for 40 < M <= 82 (up to 16 blocks, Y staged in passes); N = 100:
+    also the class beyond 82 observations (the workgroup LDS kernel k_gate_lds
+    / its global-memory variant k_gate, fed by k_feature's compact QR
+    factors), up to the longest track the chi2 table gates.  Tolerance:
     fp32 with the saddle point's conditioning (~1e3) -- median relative error
     <= 1e-4, 99th percentile <= 1e-3; decisions: at most 1 % of the features
     differ, and only where the oracle's gamma is within 5 % of the threshold."""
     from msckf_amd import chi2_threshold
     problems = [synth.make_update_problem(N, F, seed=300 + b) for b in range(B)]
     ctx, ds, feat_off, acc, gam, pw, valid, rows = _batched(problems, np.float32, cap=cap)
-    errs = []
+    errs, nlong = [], 0
     for b, d in enumerate(ds):
         st, acc_o, tri_p, tri_ok, gam_o = oracle_update(d)
         sl = slice(feat_off[b], feat_off[b + 1])
@@ -401,13 +404,17 @@ def test_gate_fp32_gamma_vs_oracle(N, F, B, cap):
         g, go = gam[sl][ok], gam_o[ok]
         assert np.isfinite(g).all()
         errs.append(np.abs(g - go) / np.maximum(np.abs(go), 1e-6))
+        nlong += int((problems[b].track_lengths()[ok] > 82).sum())
         thr = np.array([chi2_threshold(m - 1) for m in problems[b].track_lengths()])[ok]
         flip = acc[sl][ok].astype(bool) != acc_o[ok].astype(bool)
         assert flip.mean() <= 0.01, flip.mean()
         assert (np.abs(go[flip] / thr[flip] - 1) < 0.05).all()
     e = np.concatenate(errs)
     assert e.size > 40
-    print("fp32 gamma rel err: median %.2e p99 %.2e max %.2e" % (np.median(e), np.quantile(e, 0.99), e.max()))
+    if N > 82:
+        assert nlong >= 8, nlong   # the M > 82 class is really exercised
+    print("fp32 gamma rel err: median %.2e p99 %.2e max %.2e (%d tracks with M > 82)"
+          % (np.median(e), np.quantile(e, 0.99), e.max(), nlong))
     assert np.median(e) < 1e-4, np.median(e)
     assert np.quantile(e, 0.99) < 1e-3, np.quantile(e, 0.99)
 
@@ -656,6 +663,9 @@ def test_sequence_s4_degenerate():
     k0 = next((k for k in range(len(ref)) if dev(k) > 1e-6 or abs(rec[k, 29] - ref[k, 29]) > 1e-6 * ref[k, 29]),
               len(ref))
     assert k0 < len(ref), "s4 stays within 1e-6: it should then pass test_sequence_golden's bounds"
+    # the departure frame is pinned: frames 0-2 carry no degenerate accepted
+    # feature and must stay on the reference (an earlier departure is a regression)
+    assert k0 >= 3, "s4 leaves the 1e-6 band at frame %d, before the degenerate frame 3" % k0
     gl, ref_gl = [tuple(x) for x in flt.gate_log], [tuple(x) for x in g["gates"]]
     assert [x for x in gl if x[0] < k0] == [x for x in ref_gl if x[0] < k0]
     assert [tuple(x) for x in flt.shape_log if x[0] < k0] == [tuple(x) for x in g["shapes"] if x[0] < k0]

@@ -22,8 +22,12 @@ def test_rccl_world1_collectives():
         assert comm.allreduce(2.5, "sum") == 2.5
         assert comm.allreduce(-7.0, "max") == -7.0
         assert comm.allgather_bytes(b"abc\x00xyz") == [b"abc\x00xyz"]
+        comm.set_timeout(5.0)
+        assert comm.allreduce(1.0, "sum") == 1.0
+        with pytest.raises(RuntimeError):
+            comm.set_timeout(0.0)
     finally:
-        comm.close()
+        comm.close()   # finalize polled to completion, then destroy (raises if the teardown was aborted)
         ctx.close()
 
 
@@ -31,8 +35,9 @@ def test_replica_group_over_rccl():
     ctx = Context(FilterConfig(), n_filters=1, n_cam_capacity=4)
     grp = replicas.ReplicaGroup(rank=0, world=1, local_rank=0)
     try:
-        tr = grp.attach_rccl(ctx.device_info()[0])
-        assert tr == {"transport": "rccl", "rccl_comm_count": [1], "rccl_ranks": [0]}, tr
+        tr = grp.attach_rccl(ctx.device_info()[0], collective_timeout_s=120.0)
+        assert tr == {"transport": "rccl", "rccl_comm_count": [1], "rccl_ranks": [0],
+                      "collective_timeout_s": 120.0}, tr
         grp.barrier()
         assert grp.max_over_ranks(3.25) == 3.25
         assert grp.sum_over_ranks(1.5) == 1.5

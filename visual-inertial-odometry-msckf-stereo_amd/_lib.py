@@ -103,6 +103,7 @@ REPLICA_SIGS = {
     "msckf_rccl_init": (C.c_int, [_U8, C.c_int, C.c_int, C.c_int, C.c_double, C.POINTER(_P)]),
     "msckf_rccl_allreduce": (C.c_int, [_P, _D, C.c_int, C.c_int]),
     "msckf_rccl_allgather": (C.c_int, [_P, C.c_void_p, C.c_int, C.c_void_p]),
+    "msckf_rccl_set_timeout": (C.c_int, [_P, C.c_double]),
     "msckf_rccl_count": (C.c_int, [_P, _I, _I]),
     "msckf_rccl_destroy": (C.c_int, [_P]),
     "msckf_rccl_last_error": (C.c_char_p, []),

@@ -552,11 +552,7 @@ int load_features(msckf_ctx* c, int nf, const int32_t* feat_off, int single_filt
     }
     // Gram records only for the record-reading assembly (windows > 32 cams, or
     // per-filter tables too large for the fused kernel's LDS)
-#ifndef MSCKF_INFO_RECORDS
     c->gram = !info_fused_fits(c->Nmax, c->max_nf);
-#else
-    c->gram = true;   // experiment builds: force the record path
-#endif
     // (allocated in either case: k_feature writes the records of ill-conditioned
     // features for the fused assembly too -- FQR_FLAG)
     HIPC(c->obs_g.ensure(((size_t)nobs + 1) * OBG_STRIDE * sizeof(double)));
@@ -573,13 +569,11 @@ int run_update_chain(msckf_ctx* c, int row_cap, bool triangulate) {
     UpdWs<T> ws = upd_ws<T>(c);
     // stage A (register-tile windows) under the Jacobians and gating
     const bool early_a = kalman_chol_supported(c->Cmax);
-#ifndef MSCKF_A_FORK_EARLY
     if (triangulate) {
         c->timer.begin(s, "triangulate");
         launch_triangulate<T>(s, st, prm, fb, c->sc);
         c->timer.end(s);
     }
-#endif
     // Once stage A is on the side stream, every exit path joins it: an early
     // return must not leave k_kal_a reading P while a later call (restore,
     // set_state) on the main stream overwrites it.
@@ -597,13 +591,6 @@ int run_update_chain(msckf_ctx* c, int row_cap, bool triangulate) {
         launch_kalman_a_reg<T>(c->side, st, ws, &c->timer);
         HIPC(hipEventRecord(c->ev_join, c->side));
     }
-#ifdef MSCKF_A_FORK_EARLY
-    if (triangulate) {
-        c->timer.begin(s, "triangulate");
-        launch_triangulate<T>(s, st, prm, fb, c->sc);
-        c->timer.end(s);
-    }
-#endif
     c->timer.begin(s, "feature_jacobian");
     launch_feature<T>(s, st, prm, fb, c->sc);
     c->timer.end(s);

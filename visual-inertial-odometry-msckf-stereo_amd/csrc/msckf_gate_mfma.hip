@@ -109,9 +109,6 @@ struct GmPairTab {
 };
 static_assert(gm_rowoff(3 * GM_MAXM) < 65536, "pair table offsets are 16-bit");
 __device__ constexpr GmPairTab g_gm_pairs{};
-#ifndef GATE_BIF_BIG
-#define GATE_BIF_BIG 3
-#endif
 __host__ __device__ constexpr int bidx(int rb, int cb) { return rb * (rb + 1) / 2 + cb; }
 // The one-wave size classes (GateClasses::LIM) are exactly the 16-row block
 // counts: every feature of class c fills nb = c + 1 blocks, so the kernel of a
@@ -486,7 +483,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_wav
     for (int u = 0; u < 6; ++u) Prow[u] = P + u * ldp;
     // pair blocks per lane in flight: the Y phase's VGPRs are free up to the
     // elimination's peak once the accumulators outgrow them (NB >= 5)
-    constexpr int BIF = (MP || sizeof(T) == 8) ? 1 : (NB >= 5 ? GATE_BIF_BIG : 2);
+    constexpr int BIF = (MP || sizeof(T) == 8) ? 1 : (NB >= 5 ? 3 : 2);
     auto npairs = [&](int lo, int hi) { return hi < lo ? 0 : (hi + 1) * (hi + 2) / 2 - lo * (lo + 1) / 2; };
     for (int R0 = 0; R0 < nb;) {
         const int alo = (16 * R0) / 3;
@@ -929,12 +926,7 @@ __global__ void __launch_bounds__(256) k_gate_mfma_wg(DevState<float> st, Params
 template <typename T, int NB, bool MP>
 void launch_cfg(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const FeatBatch<T>& fb,
                 const int* list, int cnt, int Mmax, int capf, int wpb, size_t lds) {
-    static size_t attr = 64 * 1024;
-    if (lds > attr) {
-        (void)hipFuncSetAttribute((const void*)k_gate_mfma<T, NB, MP>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)lds);
-        attr = lds;
-    }
+    lds_limit((const void*)k_gate_mfma<T, NB, MP>, lds);
     hipLaunchKernelGGL((k_gate_mfma<T, NB, MP>), dim3((cnt + wpb - 1) / wpb), dim3(64 * wpb), lds, s, st, prm, fb,
                        list, cnt, Mmax, capf);
 }
@@ -953,10 +945,7 @@ void launch_nb(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const
     // measured 2.47 ms against 2.52 ms for 36 -- profiles/r03/ab_gate_kb/; fp64
     // keeps 72, its two waves per SIMD already fill the LDS)
     // (round 4: the staging is the dense lower matrix, capacities in elements)
-#ifndef GATE_SINGLE_KB
-#define GATE_SINGLE_KB 44
-#endif
-    constexpr int single_kb = sizeof(T) == 4 ? GATE_SINGLE_KB : 72;
+    constexpr int single_kb = sizeof(T) == 4 ? 44 : 72;
     constexpr int RS = GM<T>::RS;
     const int full = gm_dense(0, Mmax - 1);
     int cmin = 0;   // one block row per pass at least
@@ -997,11 +986,7 @@ void launch_gate_mfma_wg(hipStream_t s, const DevState<float>& st, const Params<
     if (capb > nbk) capb = nbk;
     if (capb < 6 * maxM) capb = 6 * maxM;   // one block row (up to six observation rows) per pass at least
     const size_t lds = (size_t)gw_floats(maxM, capb) * sizeof(float);
-    static size_t attr = 64 * 1024;
-    if (lds > attr) {
-        (void)hipFuncSetAttribute((const void*)k_gate_mfma_wg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        attr = lds;
-    }
+    lds_limit((const void*)k_gate_mfma_wg, lds);
     hipLaunchKernelGGL(k_gate_mfma_wg, dim3(cnt), dim3(256), lds, s, st, prm, fb, list, maxM, capb);
 }
 

@@ -233,16 +233,12 @@ __global__ void __launch_bounds__(64 * NW) k_kal_c2(DevState<T> st, UpdWs<T> ws)
             pf[q] = e < 16 * w ? -Lv(16 * J + i, col) : 0.0;
         }
     };
-    // (C2_DB: block row J staged in buffer J & 1 -- the closing barrier of each
-    // step is then not needed, a later step's put never overwrites a buffer
-    // another wave may still read.  Measured equal to two barriers per step,
-    // 1.184-1.187 vs 1.187-1.188 ms; four accumulator chains instead of two:
-    // 1.42 ms, profiles/r04/ab_c2_*)
-#ifndef C2_DB
-#define C2_DB 1
-#endif
+    // block row J is staged in buffer J & 1, so a step needs no closing
+    // barrier: a later step's put never overwrites a buffer another wave may
+    // still read (measured equal to two barriers per step; four accumulator
+    // chains instead of two: 1.42 vs 1.19 ms, profiles/r04/ab_c2_*)
     constexpr int IMGB = 16 * NTM * C2S;
-    auto imgJ = [&](int J) { return C2_DB ? img + (J & 1) * IMGB : img; };
+    auto imgJ = [&](int J) { return img + (J & 1) * IMGB; };
     auto put = [&](int J) {
         const int w = 16 * J;
         double* im = imgJ(J);
@@ -293,7 +289,6 @@ __global__ void __launch_bounds__(64 * NW) k_kal_c2(DevState<T> st, UpdWs<T> ws)
                 y = __builtin_amdgcn_mfma_f64_16x16x4f64(LI[J * 256 + (4 * kc + lr) * 16 + lc], a0[kc], y, 0, 0, 0);
             yk[t][J] = y;
         }
-        if (!C2_DB) __syncthreads();
     }
 #pragma unroll
     for (int t = 0; t < CT; ++t) {
@@ -698,12 +693,9 @@ __global__ void __launch_bounds__(64 * NW) k_kal_b(DevState<T> st, Params<T> prm
     // columns wc, wc + WC, wc + 2 WC, ... (interleaved, not a contiguous range),
     // so every chunk's active columns are spread over all the waves instead of
     // loading the first column group alone (one barrier per chunk)
-#ifndef KB_INTERLEAVE
-#define KB_INTERLEAVE 1
-#endif
     {
         const int tr0 = BR * (wv / WC), wc = wv % WC;
-        auto tcol = [&](int y) { return KB_INTERLEAVE ? wc + WC * y : BC * wc + y; };
+        auto tcol = [&](int y) { return wc + WC * y; };
         v4d acc[BR][BC];
 #pragma unroll
         for (int x = 0; x < BR; ++x)
@@ -1188,12 +1180,7 @@ bool kalman_chol_supported(int Cmax) { return ((Cmax + 15) & ~15) <= 16 * 12; }
 
 template <typename T, int NW, int TPW>
 static void launch_e1(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const UpdWs<T>& ws, size_t lds) {
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_kal_e1<T, NW, TPW>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
-        attr = true;
-    }
+    lds_limit((const void*)k_kal_e1<T, NW, TPW>, 160 * 1024);
     hipLaunchKernelGGL((k_kal_e1<T, NW, TPW>), dim3(st.B), dim3(64 * NW), lds, s, st, prm, ws);
 }
 
@@ -1203,45 +1190,26 @@ static void launch_c1(hipStream_t s, const DevState<T>& st, const UpdWs<T>& ws, 
 }
 template <typename T, int NW, int CT, int NTM>
 static void launch_c2(hipStream_t s, const DevState<T>& st, const UpdWs<T>& ws) {
-    // two staging buffers (C2_DB); the first also holds the diagonal-block scratch
+    // two staging buffers; the first also holds the diagonal-block scratch
     constexpr int IMG = 16 * NTM * C2S > NW * 272 ? 16 * NTM * C2S : NW * 272;
-    const size_t lds = (NTM * 256 + (C2_DB ? 16 * NTM * C2S : 0) + IMG) * sizeof(double);
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_kal_c2<T, NW, CT, NTM>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
-        attr = true;
-    }
+    const size_t lds = (NTM * 256 + 16 * NTM * C2S + IMG) * sizeof(double);
+    lds_limit((const void*)k_kal_c2<T, NW, CT, NTM>, 160 * 1024);
     hipLaunchKernelGGL((k_kal_c2<T, NW, CT, NTM>), dim3(st.B), dim3(64 * NW), lds, s, st, ws);
 }
 
 template <typename T, int NW, int WR, int WC, int NTM>
 static void launch_b(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const UpdWs<T>& ws, size_t lds) {
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_kal_b<T, NW, WR, WC, NTM>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
-        attr = true;
-    }
+    lds_limit((const void*)k_kal_b<T, NW, WR, WC, NTM>, 160 * 1024);
     hipLaunchKernelGGL((k_kal_b<T, NW, WR, WC, NTM>), dim3(st.B), dim3(64 * NW), lds, s, st, prm, ws);
 }
 
 // k_kal_mchol launches: NBR = block rows (exact for the bench window, 12 / 13),
-// NW waves per filter
-#ifndef MSCKF_MK_NW
-#define MSCKF_MK_NW 4
-#endif
+// four waves per filter (8 / 16 measured slower, §5.7)
 template <typename T, int STAGE, int NBR>
 static void launch_mk_nbr(hipStream_t s, const DevState<T>& st, const UpdWs<T>& ws) {
-    constexpr int NW = NBR <= 6 ? 4 : MSCKF_MK_NW;
+    constexpr int NW = 4;
     const size_t lds = mk_lds_doubles(NBR) * sizeof(double);
-    // stage A co-runs with k_feature / the gate on the side stream: a grid of
-    // MSCKF_A_GRID workgroups walking the filters leaves them CU room
-#ifndef MSCKF_A_GRID
-#define MSCKF_A_GRID 0
-#endif
-    const int grid = (STAGE == 0 && MSCKF_A_GRID > 0 && st.B > MSCKF_A_GRID) ? MSCKF_A_GRID : st.B;
-    hipLaunchKernelGGL((k_kal_mchol<T, NW, NBR, STAGE>), dim3(grid), dim3(64 * NW), lds, s, st, ws);
+    hipLaunchKernelGGL((k_kal_mchol<T, NW, NBR, STAGE>), dim3(st.B), dim3(64 * NW), lds, s, st, ws);
     // stage A near-singular P_cc: shifted retries of the failed filters only
     // (64 workgroups walk the filter list; none do any work on a healthy batch)
     if constexpr (STAGE == 0)
@@ -1261,21 +1229,15 @@ static void launch_mk(hipStream_t s, const DevState<T>& st, const UpdWs<T>& ws, 
 // (throughput: two filters per CU, VALU-light); a handful of filters (the
 // drop-in per-frame path, B = 1) keeps the register tiles, whose 4-pivot
 // steps have the shorter latency (B = 1, 20 cams, fp64: A 57 vs 68 us).
-#ifndef MSCKF_MK_MIN_B
-#define MSCKF_MK_MIN_B 64
-#endif
+constexpr int MK_MIN_B = 64;
 // MSCKF_KALMAN_CHOL=mfma / tiles (environment, read per launch) forces one
 // path -- the parity tests run both on the same inputs.
 template <typename T> static bool use_mk(const DevState<T>& st) {
-#ifdef MSCKF_KAL_RCHOL
-    return false;
-#else
     if (const char* e = getenv("MSCKF_KALMAN_CHOL")) {
         if (e[0] == 'm') return true;
         if (e[0] == 't') return false;
     }
-    return st.B >= MSCKF_MK_MIN_B;
-#endif
+    return st.B >= MK_MIN_B;
 }
 
 template <typename T>

@@ -2997,11 +2997,7 @@ void launch_propagate(hipStream_t s, const DevState<T>& st, const Params<T>& prm
     if (nfilt <= 0) return;
     constexpr int PKC = prop_pkc<T>();
     const size_t lds = (size_t)prop_lds<T>(PKC) * sizeof(T);
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_propagate<T, PKC>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        attr = true;
-    }
+    lds_limit((const void*)k_propagate<T, PKC>, 160 * 1024);
     hipLaunchKernelGGL((k_propagate<T, PKC>), dim3(nfilt), dim3(64), lds, s, st, prm, nfilt, filters, smp_off,
                        samples);
 }
@@ -3084,12 +3080,7 @@ size_t gate_lds_bytes(int maxM) {
 template <typename T, int TPL, bool MP>
 static void launch_gate_wave_cfg(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const FeatBatch<T>& fb,
                                  const int* list, int cnt, int Mmax, int capb, int wpb, size_t lds) {
-    static size_t attr = 64 * 1024;
-    if (lds > attr) {
-        (void)hipFuncSetAttribute((const void*)k_gate_wave<T, TPL, MP>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)lds);
-        attr = lds;
-    }
+    lds_limit((const void*)k_gate_wave<T, TPL, MP>, lds);
     hipLaunchKernelGGL((k_gate_wave<T, TPL, MP>), dim3((cnt + wpb - 1) / wpb), dim3(64 * wpb), lds, s, st, prm, fb,
                        list, cnt, Mmax, capb);
 }
@@ -3132,11 +3123,7 @@ template <typename T>
 void launch_gate(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const FeatBatch<T>& fb,
                  const GateClasses& gc) {
     if (fb.nf == 0) return;
-    static bool attr_set = false;
-    if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)k_gate_lds<T>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        attr_set = true;
-    }
+    lds_limit((const void*)k_gate_lds<T>, 160 * 1024);
     for (int c = 0; c < GateClasses::NC; ++c) {
         const int cnt = gc.off[c + 1] - gc.off[c];
         if (cnt == 0) continue;
@@ -3156,12 +3143,10 @@ void launch_gate(hipStream_t s, const DevState<T>& st, const Params<T>& prm, con
             const int nrow = gate_nt(maxM), tiles = nrow * (nrow + 1) / 2;
             const size_t lds = gate_big_lds_bytes(maxM);
             if (tiles <= 256 * 4) {
-                static bool a1 = false;
-                if (!a1) { (void)hipFuncSetAttribute((const void*)k_gate_big<T, 256, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); a1 = true; }
+                lds_limit((const void*)k_gate_big<T, 256, 4>, 160 * 1024);
                 hipLaunchKernelGGL((k_gate_big<T, 256, 4>), dim3(cnt), dim3(256), lds, s, st, prm, fb, list);
             } else {
-                static bool a2 = false;
-                if (!a2) { (void)hipFuncSetAttribute((const void*)k_gate_big<T, 512, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024); a2 = true; }
+                lds_limit((const void*)k_gate_big<T, 512, 4>, 160 * 1024);
                 hipLaunchKernelGGL((k_gate_big<T, 512, 4>), dim3(cnt), dim3(512), lds, s, st, prm, fb, list);
             }
             continue;
@@ -3208,11 +3193,7 @@ static void launch_info_cfg(hipStream_t s, const DevState<T>& st, const FeatBatc
     const size_t lds = fbn * per + 8 + (pre ? meta : 0);
     const int TS = (st.Nmax + 7) / 8, ntl = TS * (TS + 1) / 2;
     const int parts = (ntl + (NT / 64) - 1) / (NT / 64);
-    static size_t attr = 64 * 1024;   // dynamic LDS granted so far (default 64 KB)
-    if (lds > attr) {
-        (void)hipFuncSetAttribute((const void*)k_info<T, 1, NT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        attr = lds;
-    }
+    lds_limit((const void*)k_info<T, 1, NT>, lds);
     hipLaunchKernelGGL((k_info<T, 1, NT>), dim3(st.B, parts), dim3(NT), lds, s, st, fb, ws, fbn, pre ? maxnf : 0,
                        pre ? maxobs : 0);
 }
@@ -3225,23 +3206,14 @@ void launch_compress(hipStream_t s, const DevState<T>& st, const Params<T>& prm,
     // windows up to 32 cams, no Gram records: the fused assembly (k_info_fused)
     if (!fb.gram) {
         const size_t lds = info_fused_lds(maxnf);
-        static size_t attr = 64 * 1024;
-        if (lds > attr) {
-            (void)hipFuncSetAttribute((const void*)k_info_fused<T, IF_NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)lds);
-            attr = lds;
-        }
+        lds_limit((const void*)k_info_fused<T, IF_NW>, lds);
         hipLaunchKernelGGL((k_info_fused<T, IF_NW>), dim3(st.B), dim3(64 * IF_NW), lds, s, st, prm, fb, ws, maxnf);
         return;
     }
     // windows up to 32 cams: fp64 MFMA tiles (k_info_mfma)
     const size_t lds_m = info_mfma_lds(maxnf, maxobs);
     if (st.Nmax <= 32 && maxobs > 0 && lds_m <= 160 * 1024) {
-        static size_t attr = 64 * 1024;
-        if (lds_m > attr) {
-            (void)hipFuncSetAttribute((const void*)k_info_mfma<T>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_m);
-            attr = lds_m;
-        }
+        lds_limit((const void*)k_info_mfma<T>, lds_m);
         hipLaunchKernelGGL((k_info_mfma<T>), dim3(st.B), dim3(64 * IM_NW), lds_m, s, st, fb, ws, maxnf, maxobs);
         return;
     }

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <mutex>
 #include <string>
 #include <utility>
 #include <vector>
@@ -9,6 +10,29 @@
 #include "msckf_common.h"
 
 namespace msckf {
+
+// Raise a kernel's dynamic-LDS limit to at least `bytes` on the current
+// device.  hipFuncSetAttribute is per device, so the grant is remembered per
+// (kernel, device) -- a process-wide flag would skip a context on a second
+// device -- and under a lock (contexts may launch from several threads).
+inline void lds_limit(const void* fn, size_t bytes) {
+    if (bytes <= 64 * 1024) return;   // the default grant
+    struct Grant { const void* fn; int dev; size_t bytes; };
+    static std::mutex mu;
+    static std::vector<Grant> grants;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> g(mu);
+    for (auto& e : grants)
+        if (e.fn == fn && e.dev == dev) {
+            if (e.bytes >= bytes) return;
+            (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+            e.bytes = bytes;
+            return;
+        }
+    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    grants.push_back({fn, dev, bytes});
+}
 
 // Accumulates device time per kernel name from HIP events recorded on the
 // launch stream (so the measurement sees exactly the stream the kernel runs on).

@@ -42,6 +42,7 @@ struct RcclApi {
     ncclResult_t (*commGetAsyncError)(ncclComm_t, ncclResult_t*) = nullptr;
     ncclResult_t (*commAbort)(ncclComm_t) = nullptr;
     ncclResult_t (*commDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*commFinalize)(ncclComm_t) = nullptr;   // optional (older RCCL lacks it)
     ncclResult_t (*commCount)(const ncclComm_t, int*) = nullptr;
     ncclResult_t (*allReduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t) = nullptr;
     ncclResult_t (*allGather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
@@ -74,6 +75,7 @@ bool load_rccl() {
                sym(g_api.allReduce, "ncclAllReduce") && sym(g_api.allGather, "ncclAllGather") &&
                sym(g_api.errorString, "ncclGetErrorString");
     if (!g_api.ok) g_api.why = "librccl lacks a required symbol";
+    (void)sym(g_api.commFinalize, "ncclCommFinalize");
     return g_api.ok;
 }
 
@@ -245,14 +247,53 @@ int msckf_rccl_count(const msckf_rccl_t* c, int* count_out, int* rank_out) {
     return 0;
 }
 
+int msckf_rccl_set_timeout(msckf_rccl_t* c, double timeout_s) {
+    if (!c) RFAIL(-1, "no communicator");
+    if (!(timeout_s > 0)) RFAIL(-1, "timeout %g s", timeout_s);
+    c->timeout_s = timeout_s;
+    return 0;
+}
+
 int msckf_rccl_destroy(msckf_rccl_t* c) {
     if (!c) return 0;
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    if (c->comm) g_api.commDestroy(c->comm);
+    int rc = 0;
+    if (c->comm) {
+        // A non-blocking communicator finishes its teardown asynchronously:
+        // finalize it and poll until its outstanding operations are done
+        // before destroying it and freeing the buffers they may still touch;
+        // a teardown that errors or outlives the deadline is aborted instead.
+        bool clean = false;
+        if (g_api.commFinalize) {
+            ncclResult_t r = g_api.commFinalize(c->comm);
+            if (r == ncclSuccess || r == ncclInProgress) {
+                const auto t0 = Clock::now();
+                for (;;) {
+                    ncclResult_t st = ncclSuccess;
+                    if (g_api.commGetAsyncError(c->comm, &st) != ncclSuccess) break;
+                    if (st == ncclSuccess) { clean = true; break; }
+                    if (st != ncclInProgress) break;
+                    if (std::chrono::duration<double>(Clock::now() - t0).count() > c->timeout_s) break;
+                    std::this_thread::sleep_for(std::chrono::microseconds(50));
+                }
+            }
+        } else {
+            ncclResult_t st = ncclSuccess;   // no finalize: destroy only a quiescent communicator
+            clean = g_api.commGetAsyncError(c->comm, &st) == ncclSuccess && st == ncclSuccess;
+        }
+        if (clean) {
+            (void)g_api.commDestroy(c->comm);
+        } else {
+            (void)g_api.commAbort(c->comm);
+            r_err = "communicator teardown did not complete: aborted";
+            rc = -4;
+        }
+        c->comm = nullptr;
+    }
     if (c->dbuf) (void)hipFree(c->dbuf);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
-    return 0;
+    return rc;
 }
 
 }  // extern "C"

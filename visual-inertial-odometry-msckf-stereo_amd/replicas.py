@@ -154,6 +154,9 @@ class RcclComm:
         raw = dst.raw
         return [raw[k * n:(k + 1) * n] for k in range(self.world)]
 
+    def set_timeout(self, seconds: float):
+        self._check(self._L.msckf_rccl_set_timeout(self._h, float(seconds)), "msckf_rccl_set_timeout")
+
     def count(self):
         C = self._C
         n, r = C.c_int32(), C.c_int32()
@@ -162,8 +165,8 @@ class RcclComm:
 
     def close(self):
         if self._h is not None:
-            self._L.msckf_rccl_destroy(self._h)
-            self._h = None
+            h, self._h = self._h, None
+            self._check(self._L.msckf_rccl_destroy(h), "msckf_rccl_destroy")
 
 
 @dataclass
@@ -190,18 +193,32 @@ class ReplicaGroup:
         _send(self._sock, {"op": "gather", "v": obj})
         return list(self._lines.read()["v"])
 
+    def _rccl_do(self, what, fn, *a):
+        # A collective that fails after the communicator came up ends the job
+        # with the transport named: the ranks cannot agree to fall back to the
+        # hub without a working collective, and a half-finished timed region
+        # must not print a line.
+        try:
+            return fn(*a)
+        except RuntimeError as e:
+            raise RuntimeError("replica %s over rccl failed on rank %d of %d: %s"
+                               % (what, self.rank, self.world, e)) from e
+
     def _call(self, op, v=0.0):
         if self._rccl is not None:
-            return self._rccl.allreduce(v, "max" if op == "max" else "sum")
+            return self._rccl_do(op, self._rccl.allreduce, v, "max" if op == "max" else "sum")
         return self._hub_call(op, v)
 
-    def attach_rccl(self, device: int, timeout_s: float = 60.0) -> dict:
+    def attach_rccl(self, device: int, timeout_s: float = 60.0, collective_timeout_s: float = 1800.0) -> dict:
         """Brings up RCCL on ``device`` for this group's collectives (the
         north star's multi-GPU transport).  Rank 0 makes the unique id and
         hands it out over the hub; every rank then reports over the hub
         whether its communicator came up, and unless all did, all of them stay
-        on the hub.  Returns the transport record for the bench line: the
-        transport used and each rank's ncclCommCount (or the reason)."""
+        on the hub.  ``timeout_s`` bounds the bring-up; ``collective_timeout_s``
+        every later collective (generous: the ranks wait in a barrier while
+        rank 0 runs its accuracy and ATE legs).  Returns the transport record
+        for the bench line: the transport used and each rank's ncclCommCount
+        (or the reason)."""
         uid, err = None, None
         if self.rank == 0:
             try:
@@ -222,12 +239,18 @@ class ReplicaGroup:
                 comm.close()
             self.transport = "tcp-hub (rccl unavailable: %s)" % next(e for e in errs if e)
             return {"transport": self.transport}
+        comm.set_timeout(collective_timeout_s)
         self._rccl = comm
         self.transport = "rccl"
         counts = [json.loads(b.rstrip(b"\0").decode()) for b in
-                  self._rccl.allgather_bytes(json.dumps(list(comm.count())).encode().ljust(32, b"\0"))]
-        return {"transport": "rccl", "rccl_comm_count": [c[0] for c in counts],
-                "rccl_ranks": [c[1] for c in counts]}
+                  self._rccl_do("gather", self._rccl.allgather_bytes,
+                                json.dumps(list(comm.count())).encode().ljust(32, b"\0"))]
+        rec = {"transport": "rccl", "rccl_comm_count": [c[0] for c in counts],
+               "rccl_ranks": [c[1] for c in counts], "collective_timeout_s": collective_timeout_s}
+        if self.world > 1:
+            rec["note"] = ("world > 1 over RCCL runs only in the driver's multi-GPU bench; "
+                           "this repo's own tests cover world 1 on the GPU and world 2 over the hub")
+        return rec
 
     def barrier(self):
         self._call("barrier")
@@ -245,8 +268,9 @@ class ReplicaGroup:
         data only: e.g. the device each replica ran on)."""
         if self._rccl is not None:
             b = json.dumps(obj).encode()
-            n = int(self._rccl.allreduce(len(b), "max"))
-            return [json.loads(x.rstrip(b"\0").decode()) for x in self._rccl.allgather_bytes(b.ljust(n, b"\0"))]
+            n = int(self._rccl_do("gather", self._rccl.allreduce, len(b), "max"))
+            return [json.loads(x.rstrip(b"\0").decode())
+                    for x in self._rccl_do("gather", self._rccl.allgather_bytes, b.ljust(n, b"\0"))]
         return self._hub_gather(obj)
 
     def close(self):
