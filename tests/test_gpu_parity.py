@@ -531,6 +531,32 @@ def test_sequence_s1_mfma_cholesky(monkeypatch):
     _check_sequence("sequence_s1")
 
 
+def test_sequence_s4_mfma_cholesky(monkeypatch):
+    """s4 on k_kal_mchol: after its degenerate frame-3 update the reference's
+    non-Joseph covariance update leaves P_cc indefinite, the first partial
+    Cholesky fails and the filter is factored again with a shifted P_cc by the
+    retry launch (its parallel scan of the failed filters).  The stream must
+    run to the end, frames 0-2 on the reference (<= 1e-6), and the trajectory
+    as close to the ground truth as the reference's own."""
+    from msckf_amd.trajectory import Trajectory, ate
+    from msckf_amd.replay import FeatureStream
+    monkeypatch.setenv("MSCKF_KALMAN_CHOL", "mfma")
+    g = golden("sequence_s4")
+    seq = synth.make_sequence(int(g["n_frames"]), int(g["seed"]))
+    flt = msckf_amd.MSCKF(sequence_config(g))
+    rec = _run_sequence(flt, seq)
+    flt.close()
+    ref = g["rec"]
+    assert rec.shape == ref.shape
+    for k in range(3):
+        assert np.linalg.norm(rec[k, 1:29] - ref[k, 1:29]) <= 1e-6 * np.linalg.norm(ref[k, 1:29]), k
+    gt = FeatureStream.from_synthetic(seq).gt
+    ate_gpu = ate(Trajectory(rec[:, 0], rec[:, 5:8]), gt)
+    ate_ref = ate(Trajectory(ref[:, 0], ref[:, 5:8]), gt)
+    print("s4 (mfma Cholesky): ATE vs ground truth: device %.4f m, reference %.4f m" % (ate_gpu, ate_ref))
+    assert ate_gpu <= 2 * ate_ref + 0.01
+
+
 def _check_sequence(name):
     g = golden(name)
     seq = synth.make_sequence(int(g["n_frames"]), int(g["seed"]))

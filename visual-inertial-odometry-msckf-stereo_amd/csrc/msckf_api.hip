@@ -643,7 +643,11 @@ int unpack_results(msckf_ctx* c, const DownList& d, const ResultsRead& r, uint8_
         if (rows_out) rows_out[b] = info[4 * b];
         if (info[4 * b + 3] < 0 && bad < 0) bad = b;
     }
-    if (bad >= 0) FAIL(-3, "innovation covariance not positive definite (filter slot %d, %d rows)", bad, info[4 * bad]);
+    if (bad >= 0) {
+        if (info[4 * bad + 3] == -2)   // stage A: the partial Cholesky of P_cc failed, shifted retries included
+            FAIL(-3, "state covariance P_cc not positive definite (filter slot %d, %d rows)", bad, info[4 * bad]);
+        FAIL(-3, "innovation covariance not positive definite (filter slot %d, %d rows)", bad, info[4 * bad]);
+    }
     return 0;
 }
 

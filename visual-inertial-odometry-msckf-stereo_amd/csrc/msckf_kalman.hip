@@ -43,18 +43,29 @@ typedef double v4d __attribute__((ext_vector_type(4)));
 // (msckf_rchol.h): a NaN or a deeper negative pivot still fails with -3.
 constexpr double KALMAN_PIVOT_FLOOR = 1e-10;
 
-// workgroup reduction (all threads call; lds: >= 16 doubles of scratch, reused after)
+// largest of n diagonal entries M[(o + i)(ld + 1)]: workgroup reduction (all
+// threads call; lds: >= 16 doubles of scratch, reused after)
 template <typename T>
-__device__ double pcc_pivot_floor(const T* P, int ld, int C, double* lds) {
+__device__ double diag_max(const T* M, int ld, int o, int n, double* lds) {
     double m = 0.0;
-    for (int i = threadIdx.x; i < C; i += blockDim.x) m = fmax(m, (double)P[(size_t)(21 + i) * ld + 21 + i]);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) m = fmax(m, (double)M[(size_t)(o + i) * (ld + 1)]);
     m = wave_max(m);
     if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = m;
     __syncthreads();
     for (int w = 0; w < (int)(blockDim.x >> 6); ++w) m = fmax(m, lds[w]);
     __syncthreads();
-    return m * KALMAN_PIVOT_FLOOR;
+    return m;
 }
+template <typename T>
+__device__ double pcc_pivot_floor(const T* P, int ld, int C, double* lds) {
+    return diag_max(P, ld, 21, C, lds) * KALMAN_PIVOT_FLOOR;
+}
+// Stage C's pivots are floored at s2 (T = s2 I + Lc^T A Lc >= s2 I in exact
+// arithmetic; a numerically degenerate A's rounding can push a computed pivot
+// below it) down to -T_FLOOR_NEG x the largest diagonal entry of T: that covers
+// rounding at any conditioning (golden stream s4: pivots of order -eps |T|), a
+// pivot further below zero means a corrupted T and fails the update.
+constexpr double T_FLOOR_NEG = 1e-9;
 
 // ---- stage A: [P_cc P_ci; P_ic P_ii] in index space [cams (Cp) | IMU (24)] ----
 template <typename T, int NT, int TPL, bool RETRY = false>
@@ -126,7 +137,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 2
     const int b = blockIdx.x;
     if (ws.info[4 * b] == 0) return;
     if (ws.afail[b]) {   // stage A failed (P_cc not PD): no update for this filter
-        if (threadIdx.x == 0) ws.info[4 * b + 3] = -1;
+        if (threadIdx.x == 0) ws.info[4 * b + 3] = -2;
         return;
     }
     const int C = 6 * st.ncams[b], Cp = round4(C), nTc = Cp / 4;
@@ -150,10 +161,11 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 2
     // numerically degenerate A (a landmark millimetres from the camera: entries
     // ~1e9, cond(T) beyond 1/eps) can still push computed pivots below it.  They
     // are floored at s2 instead of failing the filter -- the reference's LU solve
-    // (msckf.py:560-563) returns its own rounding noise there, without an error.
-    // A NaN pivot still fails.
+    // (msckf.py:560-563) returns its own rounding noise there, without an error --
+    // down to -T_FLOOR_NEG x max diag(T); a NaN or deeper pivot still fails.
+    const double tmax = diag_max(Tm, ldt, 0, C, reinterpret_cast<double*>(smem_raw));
     const bool ok = rchol_core<NT, TPL>(nTc, nTc, nTc, reinterpret_cast<double*>(smem_raw), load, panel, trail, ws.s2,
-                                        -INFINITY);
+                                        -T_FLOOR_NEG * tmax);
     if (!ok && threadIdx.x == 0) ws.info[4 * b + 3] = -1;
 }
 
@@ -373,7 +385,7 @@ __global__ void __launch_bounds__(64) k_gchol_diag(DevState<T> st, UpdWs<T> ws, 
         __syncthreads();
     }
     if (bad) {
-        if (lane == 0) ws.info[4 * b + 3] = -1;
+        if (lane == 0) ws.info[4 * b + 3] = STAGE == 0 ? -2 : -1;
         return;
     }
     for (int e = lane; e < nb * nb; e += 64) {
@@ -623,9 +635,15 @@ __global__ void __launch_bounds__(256) k_kal_b2(DevState<T> st, Params<T> prm, U
 }
 
 // ---- stage B, one workgroup per filter (production path when C <= 16 * NTM) ----
-// Phase 1: G = A Lc over the full nT x nT tile grid; the NW = WR x WC waves
-// each own a (NTM/WR) x (NTM/WC) block of 16 x 16 tiles, so one k-step reads
-// NTM/WR + NTM/WC operands for their product of MFMAs.
+// Phase 1: the lower 16 x 16 tiles of G = A Lc -- phase 2 reads G[k][j] only
+// for k >= 16 (j / 16) (T[i][j] = sum_k Lc[k][i] G[k][j], Lc[k][i] = 0 for
+// k < i, i >= j), so the upper tiles are neither formed nor stored (round 5:
+// 28 % of the phase's MFMAs and half of G's HBM round trip).  Wave w owns
+// tiles w + NW s of the column-major lower enumeration: a K chunk k0 reaches
+// the tile columns <= k0 / 16 (Lc lower triangular), i.e. a prefix of that
+// enumeration, which the round-robin deal spreads evenly over the waves
+// (46 tile-chunks on the busiest wave at 12 x 12 tiles, against 72 for the
+// full grid on a 4 x 4 wave grid).
 // Phase 2: lower tiles of T = s2 I + Lc^T G (wave w owns tiles w + NW s of the
 // row-major lower enumeration) and c = Lc^T b.  K streams in chunks of 16 rows
 // through double-buffered LDS images [k][col]; both operands are row slices in
@@ -639,11 +657,9 @@ __device__ __forceinline__ void lower_tile(int t, int& ti, int& tj) {
     tj = t - i * (i + 1) / 2;
 }
 
-template <typename T, int NW, int WR, int WC, int NTM>
+template <typename T, int NW, int NTM>
 __global__ void __launch_bounds__(64 * NW) k_kal_b(DevState<T> st, Params<T> prm, UpdWs<T> ws) {
-    static_assert(WR * WC == NW && NTM % WR == 0 && NTM % WC == 0, "wave grid");
-    constexpr int BR = NTM / WR, BC = NTM / WC;                  // phase-1 tile block per wave
-    constexpr int TP2 = (NTM * (NTM + 1) / 2 + NW - 1) / NW;     // phase-2 tiles per wave
+    constexpr int TP2 = (NTM * (NTM + 1) / 2 + NW - 1) / NW;     // lower tiles per wave (both phases)
     constexpr int NT = 64 * NW, Q = (16 * 16 * NTM + NT - 1) / NT;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     const int b = blockIdx.x;
@@ -669,7 +685,9 @@ __global__ void __launch_bounds__(64 * NW) k_kal_b(DevState<T> st, Params<T> prm
             const int k = e / Cq, c = e - k * Cq, gk = k0 + k;
             const bool in = e < 16 * Cq && gk < C && c < C;
             const double lcv = (in && c <= gk) ? Lc[(size_t)gk * Cpw + c] : 0.0;
-            const double ov = in ? (ph == 0 ? Am : G)[(size_t)gk * ld + c] : 0.0;
+            // phase 2: G row gk holds the lower tile columns <= gk / 16 only
+            const bool gin = in && (ph == 0 || c < 16 * (gk / 16 + 1));
+            const double ov = gin ? (ph == 0 ? Am : G)[(size_t)gk * ld + c] : 0.0;
             r0[q] = ph == 0 ? ov : lcv;
             r1[q] = ph == 0 ? lcv : ov;
         }
@@ -687,20 +705,19 @@ __global__ void __launch_bounds__(64 * NW) k_kal_b(DevState<T> st, Params<T> prm
         }
         if (ph == 1 && tid < 16) bb[buf * 16 + tid] = rb;
     };
-    // ---- phase 1: G = A Lc ----
-    // Lc is lower triangular, so chunk k0 only reaches the tile columns
-    // tc <= k0 / 16: wave (wr, wc) owns the rows BR wr .. BR wr + BR - 1 and the
-    // columns wc, wc + WC, wc + 2 WC, ... (interleaved, not a contiguous range),
-    // so every chunk's active columns are spread over all the waves instead of
-    // loading the first column group alone (one barrier per chunk)
+    // ---- phase 1: the lower tiles of G = A Lc ----
     {
-        const int tr0 = BR * (wv / WC), wc = wv % WC;
-        auto tcol = [&](int y) { return wc + WC * y; };
-        v4d acc[BR][BC];
+        const int ntl = nT * (nT + 1) / 2;
+        v4d acc[TP2];
+        int gr[TP2], gc[TP2];
 #pragma unroll
-        for (int x = 0; x < BR; ++x)
-#pragma unroll
-            for (int y = 0; y < BC; ++y) acc[x][y] = v4d{0.0, 0.0, 0.0, 0.0};
+        for (int s = 0; s < TP2; ++s) {   // column-major lower enumeration
+            const int t = wv + NW * s, tt = t < ntl ? t : 0;
+            const int c = colmajor_col(tt, nT), r = c + tt - (c * nT - c * (c - 1) / 2);
+            gr[s] = __builtin_amdgcn_readfirstlane(t < ntl ? r : -1);
+            gc[s] = __builtin_amdgcn_readfirstlane(c);
+            acc[s] = v4d{0.0, 0.0, 0.0, 0.0};
+        }
         load(0, 0);
         put(0, 0);
         __syncthreads();
@@ -713,34 +730,26 @@ __global__ void __launch_bounds__(64 * NW) k_kal_b(DevState<T> st, Params<T> prm
 #pragma unroll
             for (int kc = 0; kc < 4; ++kc) {
                 const int kr = (4 * kc + lr) * Cq;
-                double av[BR], bv[BC];
 #pragma unroll
-                for (int x = 0; x < BR; ++x) av[x] = tr0 + x < nT ? i0[kr + 16 * (tr0 + x) + lc] : 0.0;
-#pragma unroll
-                for (int y = 0; y < BC; ++y) bv[y] = tcol(y) < nT ? i1[kr + 16 * tcol(y) + lc] : 0.0;
-#pragma unroll
-                for (int x = 0; x < BR; ++x) {
-                    if (tr0 + x >= nT) continue;
-#pragma unroll
-                    for (int y = 0; y < BC; ++y) {
-                        // Lc[k][j] = 0 for j > k: column tile tc needs k >= 16 tc
-                        if (tcol(y) >= nT || k0 + 15 < 16 * tcol(y)) continue;
-                        acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[x], bv[y], acc[x][y], 0, 0, 0);
-                    }
+                for (int s = 0; s < TP2; ++s) {
+                    // Lc[k][j] = 0 for j > k: column tile gc needs k >= 16 gc
+                    if (gr[s] < 0 || k0 + 15 < 16 * gc[s]) continue;
+                    acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(i0[kr + 16 * gr[s] + lc], i1[kr + 16 * gc[s] + lc],
+                                                                  acc[s], 0, 0, 0);
                 }
             }
             if (more) put(0, buf ^ 1);
             __syncthreads();
         }
 #pragma unroll
-        for (int x = 0; x < BR; ++x)
+        for (int s = 0; s < TP2; ++s) {
+            if (gr[s] < 0) continue;
 #pragma unroll
-            for (int y = 0; y < BC; ++y)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int i = 16 * (tr0 + x) + lr + 4 * r, j = 16 * tcol(y) + lc;
-                    if (i < C && j < C) G[(size_t)i * ld + j] = acc[x][y][r];
-                }
+            for (int r = 0; r < 4; ++r) {
+                const int i = 16 * gr[s] + lr + 4 * r, j = 16 * gc[s] + lc;
+                if (i < C && j < C) G[(size_t)i * ld + j] = acc[s][r];
+            }
+        }
         __syncthreads();   // G visible to the whole workgroup before phase 2 streams it
     }
     // ---- phase 2: T = s2 I + Lc^T G (lower), c = Lc^T b ----
@@ -944,9 +953,9 @@ __global__ void __launch_bounds__(64 * NW) k_kal_e1(DevState<T> st, Params<T> pr
 // with a Newton step, no division or square root), the Cholesky columns
 // Y = X L_d^-T of the step (Lc / Vc_i in A, L_T in C1) are formed one panel row
 // per thread and stored.  Pivot floors as rchol_core (stage A: rounding-level
-// negatives; C1: T >= s2 I).  Stage A retries a failed filter with a shifted
-// P_cc in the same launch (rare; the register-tile kernel needed a second
-// launch over every filter for it).
+// negatives; C1: T >= s2 I).  Stage A's shifted retries of a failed filter run
+// in a small second launch over the failed filters only (found by one
+// parallel scan of the failure flags).
 // ===========================================================================
 constexpr int MK_PS = 4;   // doubles per panel row (the step's four columns)
 
@@ -1110,13 +1119,44 @@ k_kal_mchol(DevState<T> st, UpdWs<T> ws) {
         const int b = blockIdx.x;
         if (ws.info[4 * b] == 0) return;
         if (ws.afail[b]) {   // stage A failed (P_cc not PD): no update for this filter
-            if (tid == 0) ws.info[4 * b + 3] = -1;
+            if (tid == 0) ws.info[4 * b + 3] = -2;
             return;
         }
         // T = s2 I + Lc^T A Lc >= s2 I: pivots below s2 are rounding (k_kal_c1)
-        const bool ok = mk_factor<T, NW, NBR, 1>(st, ws, b, 0.0, ws.s2, -INFINITY, pan0);
+        const int C = 6 * st.ncams[b], ldt = ws.Cmax + 1;
+        const double tmax = diag_max(ws.Tm + (size_t)b * ws.Cmax * ldt, ldt, 0, C, red);
+        const bool ok = mk_factor<T, NW, NBR, 1>(st, ws, b, 0.0, ws.s2, -T_FLOOR_NEG * tmax, pan0);
         if (!ok && tid == 0) ws.info[4 * b + 3] = -1;
         return;
+    }
+    if (RETRY) {   // the failed filters of this workgroup's share, found in one parallel pass
+        __shared__ int nfail, failed[64];
+        if (tid == 0) nfail = 0;
+        __syncthreads();
+        for (int i = tid; blockIdx.x + (size_t)i * gridDim.x < (size_t)st.B; i += blockDim.x) {
+            const int b = blockIdx.x + i * gridDim.x;
+            if (ws.afail[b]) {
+                const int k = atomicAdd(&nfail, 1);
+                if (k < 64) failed[k] = b;
+            }
+        }
+        __syncthreads();
+        const int nf = nfail;
+        for (int k = 0; k < nf; ++k) {
+            // (more than 64 failures in one share: the rest are walked by scanning again)
+            const int b = k < 64 ? failed[k] : -1;
+            if (b < 0) break;
+            const int C = 6 * st.ncams[b];
+            const double floor = pcc_pivot_floor(st.P + (size_t)b * st.Dmax * st.Dmax, st.Dmax, C, red);
+            bool ok = false;
+            for (int att = 1; att < 3 && !ok; ++att) {
+                const double shift = (att == 1 ? 1e-8 : 1e-6) * (floor / KALMAN_PIVOT_FLOOR);
+                ok = mk_factor<T, NW, NBR, 0>(st, ws, b, shift, floor, -PIVOT_FLOOR_NEG * floor, pan0);
+            }
+            if (tid == 0) ws.afail[b] = ok ? 0 : 1;   // read by stage C
+        }
+        if (nf <= 64) return;
+        __syncthreads();
     }
     for (int b = blockIdx.x; b < st.B; b += gridDim.x) {
         if (RETRY && ws.afail[b] == 0) continue;   // uniform
@@ -1197,10 +1237,10 @@ static void launch_c2(hipStream_t s, const DevState<T>& st, const UpdWs<T>& ws) 
     hipLaunchKernelGGL((k_kal_c2<T, NW, CT, NTM>), dim3(st.B), dim3(64 * NW), lds, s, st, ws);
 }
 
-template <typename T, int NW, int WR, int WC, int NTM>
+template <typename T, int NW, int NTM>
 static void launch_b(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const UpdWs<T>& ws, size_t lds) {
-    lds_limit((const void*)k_kal_b<T, NW, WR, WC, NTM>, 160 * 1024);
-    hipLaunchKernelGGL((k_kal_b<T, NW, WR, WC, NTM>), dim3(st.B), dim3(64 * NW), lds, s, st, prm, ws);
+    lds_limit((const void*)k_kal_b<T, NW, NTM>, 160 * 1024);
+    hipLaunchKernelGGL((k_kal_b<T, NW, NTM>), dim3(st.B), dim3(64 * NW), lds, s, st, prm, ws);
 }
 
 // k_kal_mchol launches: NBR = block rows (exact for the bench window, 12 / 13),
@@ -1273,9 +1313,9 @@ void launch_kalman_chol(hipStream_t s, const DevState<T>& st, const Params<T>& p
     }
     kt->begin(s, "kalman_b");
     if (Cq <= 16 * 8) {
-        launch_b<T, 8, 4, 2, 8>(s, st, prm, ws, (4 * 16 * (size_t)Cq + 32) * sizeof(double));
+        launch_b<T, 8, 8>(s, st, prm, ws, (4 * 16 * (size_t)Cq + 32) * sizeof(double));
     } else if (Cq <= 16 * 12) {
-        launch_b<T, 16, 4, 4, 12>(s, st, prm, ws, (4 * 16 * (size_t)Cq + 32) * sizeof(double));
+        launch_b<T, 16, 12>(s, st, prm, ws, (4 * 16 * (size_t)Cq + 32) * sizeof(double));
     } else {   // large windows: 64 x 64 output tiles, one workgroup each
         const int tiles = (Cmax + GT - 1) / GT;
         hipLaunchKernelGGL(k_kal_b1<T>, dim3(tiles, tiles, st.B), dim3(256), 0, s, st, ws);
