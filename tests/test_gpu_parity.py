@@ -419,12 +419,14 @@ def test_gate_fp32_gamma_vs_oracle(N, F, B, cap):
     assert np.quantile(e, 0.99) < 1e-3, np.quantile(e, 0.99)
 
 
-@pytest.mark.parametrize("N,F,B,nmin", [(40, 150, 2, 200), (82, 50, 1, 40)])
+@pytest.mark.parametrize("N,F,B,nmin", [(40, 150, 2, 200), (50, 120, 1, 60), (82, 50, 1, 40)])
 def test_gate_fp64_gamma_vs_oracle(N, F, B, nmin):
     """fp64 gating against the oracle's gamma (msckf.py:606-614), relative
     1e-9: the one-wave fp64 MFMA kernel (v_mfma_f64_16x16x4_f64, its own
-    accumulator row layout) for every class up to 6 blocks (M <= 30, single- and
-    multi-pass Y staging), k_gate_wave for 31 <= M <= 40; decisions identical."""
+    accumulator row layout) for every class up to 7 blocks (M <= 36, single- and
+    multi-pass Y staging), k_gate_wave for 37 <= M <= 40, k_gate_big
+    (workgroup register tiles) for 41 <= M <= 82 (N = 50: classes up to 50
+    observations, the 50x400 bench shape); decisions identical."""
     problems = [synth.make_update_problem(N, F, seed=700 + b) for b in range(B)]
     ctx, ds, feat_off, acc, gam, pw, valid, rows = _batched(problems, np.float64)
     n = 0

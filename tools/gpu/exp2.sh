@@ -1,8 +1,9 @@
 # A/B with repeats: base and each experiment build alternated R times (noise estimate).
 #   bash tools/gpu/exp2.sh r03x 2 seg1 wpb1 ...
+#   BENCH_ARGS="--N 50 --F 400 --dtype fp64 ..." bash tools/gpu/exp2.sh ...   (other workloads)
 set -o pipefail
 OUT=gpurun_out/${1:-exp}; R=${2:-2}; shift 2; mkdir -p $OUT
-ARGS="--no-cpu --no-ate --no-prop --no-fp64"
+ARGS=${BENCH_ARGS:-"--no-cpu --no-ate --no-prop --no-fp64"}
 for r in $(seq 1 $R); do
   timeout -k 10 300 python -u bench.py $ARGS > $OUT/base_$r.json 2> $OUT/base_$r.err || { tail -20 $OUT/base_$r.err; exit 1; }
   for e in "$@"; do

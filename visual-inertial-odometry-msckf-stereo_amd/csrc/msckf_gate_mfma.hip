@@ -359,9 +359,10 @@ __device__ __forceinline__ void gm_assemble(typename GM<T>::V4 (&acc)[NB * (NB +
 
 // waves per SIMD the accumulators (4 NB (NB + 1) / 2 registers) leave room for
 // (single-pass Y staging keeps two or three pair blocks in flight: one wave less)
-// (fp64: 8 NB (NB + 1) / 2 accumulator registers)
+// (fp64: 8 NB (NB + 1) / 2 accumulator registers; NB = 7 at one wave per SIMD,
+// with the accumulators spread over the AGPRs)
 __host__ __device__ constexpr int gm_waves(int NB, bool MP, int ts = 4) {
-    return ts == 8 ? (NB <= 3 ? 3 : 2)
+    return ts == 8 ? (NB <= 3 ? 3 : (NB <= 6 ? 2 : 1))
                    : ((NB <= 2 && MP) ? 5 : (NB <= 4 ? 4 : (NB <= 6 ? 3 : 2)));
 }
 
@@ -972,10 +973,16 @@ void launch_nb(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const
 
 }  // namespace
 
-// fp64 up to NB = 6 (M <= 30): beyond it the accumulators spill (k_gate_wave then)
-bool gate_mfma_fits(int maxM, int ts) { return maxM >= 1 && gm_nb(maxM) <= (ts == 8 ? 6 : 8); }
+// fp64 up to NB = 7 (M <= 36) at one wave per SIMD, the accumulators in AGPRs
+// (round 5: 31 <= M <= 36 off k_gate_wave, 50x400 fp64 gate 60.4 -> 56.0 ms,
+// profiles/r05/ab_gate_fp64_nb7/); NB = 8 would spill
+bool gate_mfma_fits(int maxM, int ts) { return maxM >= 1 && gm_nb(maxM) <= (ts == 8 ? 7 : 8); }
 bool gate_mfma_wg_fits(int maxM) { return maxM >= 1 && gm_nb(maxM) <= GW_NB; }
 
+// (round 5 ran the same elimination on fp64 MFMA for 41 <= M <= 62, three
+// block rows per wave: 256 VGPRs + 192 AGPRs, one workgroup per CU, parity
+// green but the 50x400 fp64 gate 55.9 -> 61.5 ms against k_gate_big's register
+// tiles at two workgroups per CU -- profiles/r05/exp_gate_mfma_wg64/)
 void launch_gate_mfma_wg(hipStream_t s, const DevState<float>& st, const Params<float>& prm,
                          const FeatBatch<float>& fb, const int* list, int cnt, int maxM) {
     if (cnt <= 0) return;
@@ -1001,11 +1008,9 @@ void launch_gate_mfma(hipStream_t s, const DevState<T>& st, const Params<T>& prm
         case 4: launch_nb<T, 4>(s, st, prm, fb, list, cnt, maxM); break;
         case 5: launch_nb<T, 5>(s, st, prm, fb, list, cnt, maxM); break;
         case 6: launch_nb<T, 6>(s, st, prm, fb, list, cnt, maxM); break;
+        case 7: launch_nb<T, 7>(s, st, prm, fb, list, cnt, maxM); break;
         default:
-            if constexpr (sizeof(T) == 4) {
-                if (gm_nb(maxM) == 7) launch_nb<T, 7>(s, st, prm, fb, list, cnt, maxM);
-                else launch_nb<T, 8>(s, st, prm, fb, list, cnt, maxM);
-            }
+            if constexpr (sizeof(T) == 4) launch_nb<T, 8>(s, st, prm, fb, list, cnt, maxM);
             break;
     }
 }

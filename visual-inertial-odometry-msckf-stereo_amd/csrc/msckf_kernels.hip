@@ -3139,6 +3139,8 @@ void launch_gate(hipStream_t s, const DevState<T>& st, const Params<T>& prm, con
                 continue;
             }
         }
+        // (round 5: fp64 30 < M <= 40 on k_gate_big instead of k_gate_wave measured
+        // slower, gate 60.5 -> 63.4 ms at 50x400, profiles/r05/exp_gate_big_fp64_31_40/)
         if (c == GateClasses::NC - 2) {   // 40 < M <= 82: register tiles, one workgroup per feature
             const int nrow = gate_nt(maxM), tiles = nrow * (nrow + 1) / 2;
             const size_t lds = gate_big_lds_bytes(maxM);

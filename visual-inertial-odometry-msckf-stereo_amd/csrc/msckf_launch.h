@@ -137,7 +137,8 @@ bool gate_mfma_fits(int maxM, int scalar_bytes);
 template <typename T>
 void launch_gate_mfma(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&, const int* list, int cnt,
                       int maxM);
-// fp32 gating of large tracks (40 < M <= 82) on MFMA tiles, one 4-wave workgroup per feature
+// fp32 gating of large tracks (40 < M <= 82) on MFMA tiles, one 4-wave
+// workgroup per feature
 bool gate_mfma_wg_fits(int maxM);
 void launch_gate_mfma_wg(hipStream_t, const DevState<float>&, const Params<float>&, const FeatBatch<float>&,
                          const int* list, int cnt, int maxM);
