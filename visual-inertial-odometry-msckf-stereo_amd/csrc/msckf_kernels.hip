@@ -109,6 +109,26 @@ __device__ __forceinline__ T prop_dot(const T (&x)[21], const T (&y)[N], unsigne
 }
 __device__ __forceinline__ void prop_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
+// Phase timing of k_propagate (probe builds only, `make probe`:
+// -DMSCKF_GATE_PROBE; tools/probes/prop_phases.py reads it): per scalar type,
+// wave-cycle sums (s_memtime) of the start (P11 load, cross-block prefetch),
+// the chunk scalars (A..B4), the per-sample Phi (C1..C3b), the Q term (C4..C5),
+// D1, D2, D3, the end (write-back, cross blocks), and the wave count.
+#ifdef MSCKF_GATE_PROBE
+__device__ unsigned long long g_prop_probe[2][10];
+#define PPROBE_T(v) const unsigned long long v = __builtin_readcyclecounter()
+#define PPROBE_ADD(ph, dt) \
+    do { if (lane == 0) atomicAdd(&g_prop_probe[sizeof(T) == 8][ph], (unsigned long long)(dt)); } while (0)
+extern "C" int msckf_prop_probe_read(unsigned long long* out) {   // [2][10], then reset
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prop_probe), sizeof(g_prop_probe)) != hipSuccess) return -1;
+    static unsigned long long zero[2][10] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_prop_probe), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
+}
+#else
+#define PPROBE_T(v) (void)0
+#define PPROBE_ADD(ph, dt) (void)0
+#endif
+
 template <typename T, int PKC>
 __global__ void __launch_bounds__(64) k_propagate(DevState<T> st, Params<T> prm, int nfilt,
                                                   const int* __restrict__ filters,
@@ -122,6 +142,7 @@ __global__ void __launch_bounds__(64) k_propagate(DevState<T> st, Params<T> prm,
     const int n = smp_off[w + 1] - smp_off[w];
     const T* samples = samples_all + 7 * (size_t)smp_off[w];
     if (n <= 0) return;
+    PPROBE_T(t_start);
     T* Pa = reinterpret_cast<T*>(smem_raw);  // P11 (ping-pong with Pb)
     T* Pb = Pa + MAT;
     T* cTa = Pb + MAT;                       // (Phi_k ... Phi_1)^T (ping-pong with cTb)
@@ -151,12 +172,18 @@ __global__ void __launch_bounds__(64) k_propagate(DevState<T> st, Params<T> prm,
         for (int m = 0; m < 21; ++m) pre[pp][m] = j < D ? P[m * ld + j] : T(0);
     }
     prop_sync();
+    PPROBE_T(t_started);
+    PPROBE_ADD(0, t_started - t_start);
+#ifdef MSCKF_GATE_PROBE
+    unsigned long long t_ph[6] = {0, 0, 0, 0, 0, 0};
+#endif
     // matrix phases: lane (g, c), g = lane / 21 the row inside each 3-row block,
     // c = lane % 21 a column (lane 63 idle)
     const int g = lane / 21, c = lane - 21 * (lane / 21);
     const bool act = lane < 63;
     for (int k0 = 0; k0 < n; k0 += PKC) {
         const int kc = min(PKC, n - k0);
+        PPROBE_T(t_c0);
         // ---- A: one lane per sample ----
         if (lane < kc) {
             T* sk = SK + lane * PROP_SC;
@@ -345,7 +372,11 @@ __global__ void __launch_bounds__(64) k_propagate(DevState<T> st, Params<T> prm,
             s_imu[I_ALIAS] = T(1);
         }
         prop_sync();
+#ifdef MSCKF_GATE_PROBE
+        { PPROBE_T(t_c1); t_ph[0] += t_c1 - t_c0; }
+#endif
         for (int k = 0; k < kc; ++k) {
+            PPROBE_T(t_s0);
             const T* sk = SK + k * PROP_SC;
             const T dt = sk[PK_DT];
             const T* R = sk + PK_R;
@@ -410,6 +441,10 @@ __global__ void __launch_bounds__(64) k_propagate(DevState<T> st, Params<T> prm,
                 }
             }
             prop_sync();
+#ifdef MSCKF_GATE_PROBE
+            PPROBE_T(t_s1);
+            t_ph[1] += t_s1 - t_s0;
+#endif
             // this lane's rows 3 rb + g of Phi (non-zero blocks only): C5, D1 and D2 use them
             T phr[7][21];
 #pragma unroll
@@ -447,6 +482,10 @@ __global__ void __launch_bounds__(64) k_propagate(DevState<T> st, Params<T> prm,
                 }
             }
             prop_sync();
+#ifdef MSCKF_GATE_PROBE
+            PPROBE_T(t_s2);
+            t_ph[2] += t_s2 - t_s1;
+#endif
             // ---- D1: A = Phi P11 (column c), cumulative Phi (row c of its transpose) ----
             if (act) {
                 T prow[21], crow[21];
@@ -461,6 +500,10 @@ __global__ void __launch_bounds__(64) k_propagate(DevState<T> st, Params<T> prm,
                 }
             }
             prop_sync();
+#ifdef MSCKF_GATE_PROBE
+            PPROBE_T(t_s3);
+            t_ph[3] += t_s3 - t_s2;
+#endif
             // ---- D2: A Phi^T + Q dt (row c) ----
             if (act) {
                 T arow[21];
@@ -474,6 +517,10 @@ __global__ void __launch_bounds__(64) k_propagate(DevState<T> st, Params<T> prm,
                 }
             }
             prop_sync();
+#ifdef MSCKF_GATE_PROBE
+            PPROBE_T(t_s4);
+            t_ph[4] += t_s4 - t_s3;
+#endif
             // ---- D3: P11 = (P11' + P11'^T) / 2 (msckf.py:362-363) ----
             if (act) {
 #pragma unroll
@@ -483,10 +530,18 @@ __global__ void __launch_bounds__(64) k_propagate(DevState<T> st, Params<T> prm,
                 }
             }
             prop_sync();
+#ifdef MSCKF_GATE_PROBE
+            PPROBE_T(t_s5);
+            t_ph[5] += t_s5 - t_s4;
+#endif
             T* t = Pa; Pa = Pb; Pb = t;
             t = cTa; cTa = cTb; cTb = t;
         }
     }
+    PPROBE_T(t_end0);
+#ifdef MSCKF_GATE_PROBE
+    for (int q = 0; q < 6; ++q) PPROBE_ADD(1 + q, t_ph[q]);
+#endif
     // write back P11 and the IMU record; the cross blocks with the cumulative Phi
     for (int e = lane; e < 441; e += 64) {
         const int i = e / 21, j = e - 21 * i;
@@ -543,6 +598,10 @@ __global__ void __launch_bounds__(64) k_propagate(DevState<T> st, Params<T> prm,
         }
         prop_sync();
     }
+    PPROBE_T(t_end1);
+    PPROBE_ADD(7, t_end1 - t_end0);
+    PPROBE_ADD(8, t_end1 - t_start);
+    PPROBE_ADD(9, 1);
 }
 
 // ===========================================================================
