@@ -57,10 +57,14 @@ namespace msckf {
 // contiguous rows.  Every dot product runs in the reference order (sum over k
 // ascending).
 // ===========================================================================
+// [w]x[r][c] with a run-time (r, c): one read of w[3 - r - c] and a sign,
+// no branch ([w]x[r][c] = -w[k] for c = r + 1 mod 3, +w[k] for c = r + 2 mod 3)
 template <typename T>
-__device__ __forceinline__ T skew_el(const T* w, int r, int c) {   // [w]x[r][c]
-    return r == c ? T(0)
-                  : (r == 0 ? (c == 1 ? -w[2] : w[1]) : (r == 1 ? (c == 0 ? w[2] : -w[0]) : (c == 0 ? -w[1] : w[0])));
+__device__ __forceinline__ T skew_sel(const T* w, int r, int c) {
+    const int k = r == c ? 0 : 3 - r - c;
+    const T v = w[k];
+    const int d = c - r + 3;
+    return r == c ? T(0) : ((d == 1 || d == 4) ? -v : v);
 }
 
 // LDS row strides of the 21-wide matrices and of Phi G Qc (21 x 12): a lane per
@@ -162,15 +166,11 @@ __global__ void __launch_bounds__(64) k_propagate(DevState<T> st, Params<T> prm,
         Pa[i * RS + j] = P[i * ld + j];
         cTa[i * RS + j] = i == j ? T(1) : T(0);
     }
-    // the cross-block columns, prefetched: their load latency hides behind the samples
+    // the cross-block columns, prefetched (fp32) once the first chunk's samples
+    // are in: vmcnt retires in issue order, so loads issued before the samples'
+    // would hold up the first phase instead of hiding behind the chain
     constexpr int NPRE = sizeof(T) == 4 ? 3 : 0;
     T pre[NPRE > 0 ? NPRE : 1][21];
-#pragma unroll
-    for (int pp = 0; pp < NPRE; ++pp) {
-        const int j = 21 + 64 * pp + lane;
-#pragma unroll
-        for (int m = 0; m < 21; ++m) pre[pp][m] = j < D ? P[m * ld + j] : T(0);
-    }
     prop_sync();
     PPROBE_T(t_started);
     PPROBE_ADD(0, t_started - t_start);
@@ -178,9 +178,12 @@ __global__ void __launch_bounds__(64) k_propagate(DevState<T> st, Params<T> prm,
     unsigned long long t_ph[6] = {0, 0, 0, 0, 0, 0};
 #endif
     // matrix phases: lane (g, c), g = lane / 21 the row inside each 3-row block,
-    // c = lane % 21 a column (lane 63 idle)
-    const int g = lane / 21, c = lane - 21 * (lane / 21);
-    const bool act = lane < 63;
+    // c = lane % 21 a column
+    // lane 63 repeats lane 62's entries (identical values to identical
+    // addresses): no lane is masked off, so no phase branches around its loads
+    const int le = lane < 63 ? lane : 62;
+    const int g = le / 21, c = le - 21 * (le / 21);
+    constexpr bool act = true;
     for (int k0 = 0; k0 < n; k0 += PKC) {
         const int kc = min(PKC, n - k0);
         PPROBE_T(t_c0);
@@ -216,6 +219,14 @@ __global__ void __launch_bounds__(64) k_propagate(DevState<T> st, Params<T> prm,
                     sk[PK_M1 + e] = c1 * (id + Om[e] * dt * T(0.5));
                     sk[PK_M2 + e] = c2 * (id + Om[e] * dt * T(0.25));
                 }
+            }
+        }
+        if (k0 == 0) {
+#pragma unroll
+            for (int pp = 0; pp < NPRE; ++pp) {
+                const int j = 21 + 64 * pp + lane;
+#pragma unroll
+                for (int m = 0; m < 21; ++m) pre[pp][m] = j < D ? P[m * ld + j] : T(0);
             }
         }
         prop_sync();
@@ -386,9 +397,11 @@ __global__ void __launch_bounds__(64) k_propagate(DevState<T> st, Params<T> prm,
                 const int bj = c / 3, cc = c - 3 * (c / 3);
                 const T* wg = sk + PK_W;
                 const T* ac = sk + PK_A;
-                const T f0 = bj == 0 ? -skew_el(wg, g, cc) : (bj == 1 ? (g == cc ? T(-1) : T(0)) : T(0));
-                const T f2 = bj == 0 ? -R[g] * skew_el(ac, 0, cc) + -R[3 + g] * skew_el(ac, 1, cc) + -R[6 + g] * skew_el(ac, 2, cc)
-                                     : (bj == 3 ? -R[3 * cc + g] : T(0));
+                // every operand loaded, then selected: no branch around an LDS read
+                const T f0 = bj == 0 ? -skew_sel(wg, g, cc) : (bj == 1 ? (g == cc ? T(-1) : T(0)) : T(0));
+                const T f2a = -R[g] * skew_sel(ac, 0, cc) + -R[3 + g] * skew_sel(ac, 1, cc) + -R[6 + g] * skew_sel(ac, 2, cc);
+                const T f2b = -R[3 * cc + g];
+                const T f2 = bj == 0 ? f2a : (bj == 3 ? f2b : T(0));
                 const T f4 = (bj == 2 && g == cc) ? T(1) : T(0);
                 fo[0] = f0 * dt;
                 fo[2] = f2 * dt;
