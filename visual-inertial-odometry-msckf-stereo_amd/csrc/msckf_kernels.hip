@@ -111,7 +111,10 @@ __device__ __forceinline__ T prop_dot(const T (&x)[21], const T (&y)[N], unsigne
         }
     return s;
 }
-__device__ __forceinline__ void prop_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// Phase boundary of the one-wave kernel.  One wave's LDS operations execute in
+// issue order, so a lane's read issued after another lane's write sees it: only
+// the compiler must not move LDS accesses across the boundary (no hardware wait).
+__device__ __forceinline__ void prop_sync() { asm volatile("" ::: "memory"); }
 
 // Phase timing of k_propagate (probe builds only, `make probe`:
 // -DMSCKF_GATE_PROBE; tools/probes/prop_phases.py reads it): per scalar type,
