@@ -646,8 +646,8 @@ __global__ void __launch_bounds__(256) k_kal_b2(DevState<T> st, Params<T> prm, U
 // full grid on a 4 x 4 wave grid).
 // Phase 2: lower tiles of T = s2 I + Lc^T G (wave w owns tiles w + NW s of the
 // row-major lower enumeration) and c = Lc^T b.  K streams in chunks of 16 rows
-// through double-buffered LDS images [k][col]; both operands are row slices in
-// memory (A is stored symmetric), so every load is coalesced.  Chunks that
+// through double-buffered LDS images [k][col]; A is read from its stored lower
+// triangle (row or column segments, see load()), Lc and G as row slices.  Chunks that
 // meet only the zero upper triangle of Lc are skipped per tile.
 __device__ __forceinline__ void lower_tile(int t, int& ti, int& tj) {
     int i = (int)((sqrtf(8.0f * (float)t + 1.0f) - 1.0f) * 0.5f);
@@ -672,35 +672,57 @@ __global__ void __launch_bounds__(64 * NW) k_kal_b(DevState<T> st, Params<T> prm
     const KT* Lc = ws.Lc + (size_t)b * Cpw * Cpw;
     KT* G = ws.G + (size_t)b * ws.Cmax * ld;
     KT* Tm = ws.Tm + (size_t)b * ws.Cmax * ld;
-    double* img = reinterpret_cast<double*>(smem_raw);   // [2 buf][2 op][16][Cq], then [2][16] b chunk
-    double* bb = img + 4 * 16 * Cq;
+    // LDS images [2 buf][2 op][16][CqS], then [2][16] b chunk; the row stride
+    // CqS = Cq + 2 keeps the column-gathered writes of phase 1 conflict-free
+    const int CqS = Cq + 2;
+    double* img = reinterpret_cast<double*>(smem_raw);
+    double* bb = img + 4 * 16 * CqS;
     // operand 0 = rows of X (A in phase 1, Lc in phase 2), operand 1 = rows of Y (Lc, G).
     // load() issues the next chunk's global reads into registers before the
     // MFMAs of the current one; put() writes them to the other LDS buffer after.
+    // A is stored as its lower triangle only (k_info_fused): phase 1 gathers
+    // the chunk's 16 x 16 column tiles left of / on the diagonal as row
+    // segments A[k][c] and those right of it as column segments A[c][k] (16
+    // lanes over k: 128 contiguous bytes of row c), so every read stays coalesced.
     double r0[Q], r1[Q], rb = 0.0;
+    int pos[Q];
     auto load = [&](int ph, int k0) {
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
             const int e = tid + NT * q;
-            const int k = e / Cq, c = e - k * Cq, gk = k0 + k;
+            int k, c;
+            if (ph == 0) {
+                const int jt = e >> 8, u = e & 255;
+                const bool up = jt > (k0 >> 4);
+                k = up ? (u & 15) : (u >> 4);
+                c = 16 * jt + (up ? (u >> 4) : (u & 15));
+            } else {
+                k = e / Cq;
+                c = e - k * Cq;
+            }
+            const int gk = k0 + k;
+            pos[q] = k * CqS + c;
             const bool in = e < 16 * Cq && gk < C && c < C;
             const double lcv = (in && c <= gk) ? Lc[(size_t)gk * Cpw + c] : 0.0;
-            // phase 2: G row gk holds the lower tile columns <= gk / 16 only
-            const bool gin = in && (ph == 0 || c < 16 * (gk / 16 + 1));
-            const double ov = gin ? (ph == 0 ? Am : G)[(size_t)gk * ld + c] : 0.0;
+            double ov;
+            if (ph == 0) {
+                ov = in ? Am[c <= gk ? (size_t)gk * ld + c : (size_t)c * ld + gk] : 0.0;
+            } else {   // G row gk holds the lower tile columns <= gk / 16 only
+                ov = (in && c < 16 * (gk / 16 + 1)) ? G[(size_t)gk * ld + c] : 0.0;
+            }
             r0[q] = ph == 0 ? ov : lcv;
             r1[q] = ph == 0 ? lcv : ov;
         }
         if (ph == 1 && tid < 16) rb = k0 + tid < C ? Am[(size_t)(k0 + tid) * ld + ws.Cmax] : 0.0;
     };
     auto put = [&](int ph, int buf) {
-        double* i0 = img + (2 * buf) * 16 * Cq;
+        double* i0 = img + (2 * buf) * 16 * CqS;
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
             const int e = tid + NT * q;
             if (e < 16 * Cq) {
-                i0[e] = r0[q];
-                i0[16 * Cq + e] = r1[q];
+                i0[pos[q]] = r0[q];
+                i0[16 * CqS + pos[q]] = r1[q];
             }
         }
         if (ph == 1 && tid < 16) bb[buf * 16 + tid] = rb;
@@ -725,11 +747,11 @@ __global__ void __launch_bounds__(64 * NW) k_kal_b(DevState<T> st, Params<T> prm
             const int buf = it & 1;
             const bool more = k0 + 16 < C;
             if (more) load(0, k0 + 16);
-            const double* i0 = img + (2 * buf) * 16 * Cq;
-            const double* i1 = i0 + 16 * Cq;
+            const double* i0 = img + (2 * buf) * 16 * CqS;
+            const double* i1 = i0 + 16 * CqS;
 #pragma unroll
             for (int kc = 0; kc < 4; ++kc) {
-                const int kr = (4 * kc + lr) * Cq;
+                const int kr = (4 * kc + lr) * CqS;
 #pragma unroll
                 for (int s = 0; s < TP2; ++s) {
                     // Lc[k][j] = 0 for j > k: column tile gc needs k >= 16 gc
@@ -774,11 +796,11 @@ __global__ void __launch_bounds__(64 * NW) k_kal_b(DevState<T> st, Params<T> prm
             const int buf = it & 1;
             const bool more = k0 + 16 < C;
             if (more) load(1, k0 + 16);
-            const double* i0 = img + (2 * buf) * 16 * Cq;
-            const double* i1 = i0 + 16 * Cq;
+            const double* i0 = img + (2 * buf) * 16 * CqS;
+            const double* i1 = i0 + 16 * CqS;
 #pragma unroll
             for (int kc = 0; kc < 4; ++kc) {
-                const int kr = (4 * kc + lr) * Cq;
+                const int kr = (4 * kc + lr) * CqS;
 #pragma unroll
                 for (int s = 0; s < TP2; ++s) {
                     // Lc[k][i] = 0 for i > k: row tile ti needs k >= 16 ti
@@ -789,7 +811,7 @@ __global__ void __launch_bounds__(64 * NW) k_kal_b(DevState<T> st, Params<T> prm
             }
             if (tid < C) {
 #pragma unroll
-                for (int k = 0; k < 16; ++k) ca += i0[k * Cq + tid] * bb[buf * 16 + k];
+                for (int k = 0; k < 16; ++k) ca += i0[k * CqS + tid] * bb[buf * 16 + k];
             }
             if (more) put(1, buf ^ 1);
             __syncthreads();
@@ -1313,9 +1335,9 @@ void launch_kalman_chol(hipStream_t s, const DevState<T>& st, const Params<T>& p
     }
     kt->begin(s, "kalman_b");
     if (Cq <= 16 * 8) {
-        launch_b<T, 8, 8>(s, st, prm, ws, (4 * 16 * (size_t)Cq + 32) * sizeof(double));
+        launch_b<T, 8, 8>(s, st, prm, ws, (4 * 16 * (size_t)(Cq + 2) + 32) * sizeof(double));
     } else if (Cq <= 16 * 12) {
-        launch_b<T, 16, 12>(s, st, prm, ws, (4 * 16 * (size_t)Cq + 32) * sizeof(double));
+        launch_b<T, 16, 12>(s, st, prm, ws, (4 * 16 * (size_t)(Cq + 2) + 32) * sizeof(double));
     } else {   // large windows: 64 x 64 output tiles, one workgroup each
         const int tiles = (Cmax + GT - 1) / GT;
         hipLaunchKernelGGL(k_kal_b1<T>, dim3(tiles, tiles, st.B), dim3(256), 0, s, st, ws);

@@ -2528,10 +2528,8 @@ __global__ void __launch_bounds__(64 * IM_NW) k_info_mfma(DevState<T> st, FeatBa
             while (x * (x + 1) / 2 > de) --x;
             while ((x + 1) * (x + 2) / 2 <= de) ++x;
             const int y = de - x * (x + 1) / 2;
-            const size_t i0 = (size_t)(6 * dc + x) * ldf + 6 * dc + y, i1 = (size_t)(6 * dc + y) * ldf + 6 * dc + x;
-            const double v = F[i0] + dsum;
-            F[i0] = v;
-            if (x != y) F[i1] = v;
+            const size_t i0 = (size_t)(6 * dc + x) * ldf + 6 * dc + y;   // x >= y: lower triangle
+            F[i0] += dsum;
         } else {
             F[(size_t)(6 * dc + de - 21) * ldf + Cmax] = dsum;
         }
@@ -2705,11 +2703,8 @@ __device__ __forceinline__ void info_owner(const double* buf, const unsigned* ft
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int row = 16 * ti + lr + 4 * r, col = 16 * tj + lc;
-            if (row < C && col < C) {
-                const double v = -tacc[q][r];
-                F[(size_t)row * ldf + col] = v;
-                F[(size_t)col * ldf + row] = v;
-            }
+            // the lower triangle only: stage B reads A from it (k_kal_b)
+            if (row < C && col <= row) F[(size_t)row * ldf + col] = -tacc[q][r];
         }
     }
 }
@@ -3009,10 +3004,8 @@ __global__ void __launch_bounds__(64 * NW) k_info_fused(DevState<T> st, Params<T
             while (x * (x + 1) / 2 > de) --x;
             while ((x + 1) * (x + 2) / 2 <= de) ++x;
             const int y = de - x * (x + 1) / 2;
-            const size_t i0 = (size_t)(6 * dc + x) * ldf + 6 * dc + y, i1 = (size_t)(6 * dc + y) * ldf + 6 * dc + x;
-            const double v = F[i0] + dsum;
-            F[i0] = v;
-            if (x != y) F[i1] = v;
+            const size_t i0 = (size_t)(6 * dc + x) * ldf + 6 * dc + y;   // x >= y: lower triangle
+            F[i0] += dsum;
         } else {
             F[(size_t)(6 * dc + de - 21) * ldf + Cmax] = dsum;
         }
