@@ -67,8 +67,8 @@ def test_scheduler_matches_single_filter_runs():
 def test_scheduler_fp32_runs_and_tracks():
     streams = [FeatureStream.from_synthetic(synth.make_sequence(80, s)) for s in (21, 22, 23, 24)]
     multi = MultiMSCKF(len(streams), dtype=np.float32)
-    try:
-        trajs = multi.run_streams(streams)
+    try:   # messages built beforehand, as tools/bench_sequences.py times it
+        trajs = multi.run_streams(streams, messages=[s.messages() for s in streams])
     finally:
         multi.close()
     for st, tr in zip(streams, trajs):

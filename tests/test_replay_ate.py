@@ -195,3 +195,18 @@ def test_oracle_replay_ate_vs_reference():
     assert ate(traj, ref, align="none") < 1e-9
     e_gt = ate(traj, st.gt)
     assert e_gt < 0.05, e_gt
+
+
+def test_stream_messages_are_its_events(seq):
+    """messages() (built once before a timed replay) holds the same IMU and
+    frame messages as events(), split by kind."""
+    st = FeatureStream.from_synthetic(seq)
+    imu, frames = st.messages()
+    ev = st.events()
+    assert len(imu) == sum(1 for k, _ in ev if k == 0) and len(frames) == st.n_frames
+    for a, (_, b) in zip(imu, [e for e in ev if e[0] == 0]):
+        assert a.vio_timestamp__ == b.vio_timestamp__
+        np.testing.assert_array_equal(a.linear_acceleration, b.linear_acceleration)
+    for a, (_, b) in zip(frames, [e for e in ev if e[0] == 1]):
+        assert a.timestamp == b.timestamp
+        assert [(f.id, f.u0, f.v1) for f in a.vio_features] == [(f.id, f.u0, f.v1) for f in b.vio_features]

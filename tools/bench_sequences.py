@@ -3,7 +3,9 @@ the same shape (EuRoC is not reachable here): S stereo+IMU sequences replayed
 through ONE device context by the multi-sequence scheduler
 (msckf_amd.scheduler.MultiMSCKF), against the same S sequences replayed one
 after another through the single-filter drop-in class.  Prints one JSON line:
-frames/s of both, the batched launch counts, and ATE vs ground truth.
+frames/s of both, the batched launch counts, and ATE vs ground truth.  The
+replayed messages (the front-end's output) are built before both timed
+regions.
 
     python tools/bench_sequences.py [--seqs 11] [--frames 200] [--fp32]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
@@ -45,9 +47,12 @@ def main():
     streams = [FeatureStream.from_synthetic(synth.make_sequence(a.frames, 100 + i)) for i in mine]
     n_frames = sum(s.n_frames for s in streams)
     multi = MultiMSCKF(len(streams), dtype=dtype, device=grp.local_rank) if streams else None
+    # the messages are the front-end's output: built before either timed
+    # region (as the bench's ATE leg does), fresh objects for each run
+    msgs = [s.messages() for s in streams]
     grp.barrier()
     t0 = time.perf_counter()
-    trajs = multi.run_streams(streams) if multi else []
+    trajs = multi.run_streams(streams, messages=msgs) if multi else []
     el_b = grp.max_over_ranks(time.perf_counter() - t0)
     total_frames = grp.sum_over_ranks(n_frames)
     launches = dict(multi.launches) if multi else {}
@@ -59,10 +64,11 @@ def main():
            "batched_launches_rank0": launches,
            "ate_vs_gt_m_rank0": [round(ate(t, s.gt), 5) for t, s in zip(trajs, streams)]}
     if not a.no_single and grp.world == 1:
+        evs = [s.events() for s in streams]
         t0 = time.perf_counter()
-        for s in streams:
+        for s, ev in zip(streams, evs):
             flt = msckf_amd.MSCKF(dtype=dtype)
-            replay(flt, s)
+            replay(flt, s, events=ev)
             flt.close()
         el_s = time.perf_counter() - t0
         out["single_frames_per_s"] = round(n_frames / el_s, 1)

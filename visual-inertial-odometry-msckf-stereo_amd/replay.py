@@ -78,6 +78,11 @@ class FeatureStream:
                  for i in range(a, b)]
         return FeatureMsg(float(self.frame_t[k]), feats)
 
+    def messages(self):
+        """(IMU messages, frame messages) of the whole stream: the front-end's
+        output, built once (a timed replay leaves their construction out)."""
+        return self.imu_msgs(), [self.frame_msg(k) for k in range(self.n_frames)]
+
     def events(self):
         """(kind, msg) in strict time order, IMU first on ties; kind 0 = IMU,
         1 = frame."""

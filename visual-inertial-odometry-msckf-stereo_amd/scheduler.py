@@ -182,13 +182,17 @@ class MultiMSCKF:
         return out
 
     # -------------------------------------------------------------- streams --
-    def run_streams(self, streams, on_frame=None):
+    def run_streams(self, streams, on_frame=None, messages=None):
         """Replays ``streams`` (replay.FeatureStream, one per lane) in lock
         step -- frame k of every stream in one batched round, each lane fed
         its own IMU samples up to its frame stamp first (IMU first on ties,
-        as replay.FeatureStream.events) -- and returns one Trajectory per lane."""
+        as replay.FeatureStream.events) -- and returns one Trajectory per lane.
+        ``messages``: the streams' ``messages()`` built by the caller
+        beforehand (the front-end's output; a timed run leaves them out)."""
         if len(streams) > len(self.lanes):
             raise ValueError("%d streams for %d filter slots" % (len(streams), len(self.lanes)))
+        if messages is not None and len(messages) != len(streams):
+            raise ValueError("%d message sets for %d streams" % (len(messages), len(streams)))
         imu_pos = [0] * len(streams)
         results = [[] for _ in streams]
         n_rounds = max(s.n_frames for s in streams) if streams else 0
@@ -199,10 +203,15 @@ class MultiMSCKF:
                     continue
                 t = st.frame_t[k]
                 j = int(np.searchsorted(st.imu[:, 0], t, side="right"))
-                for r in st.imu[imu_pos[i]:j]:
-                    self.imu_callback(i, _imu_msg(r))
+                if messages is None:
+                    for r in st.imu[imu_pos[i]:j]:
+                        self.imu_callback(i, _imu_msg(r))
+                    msgs[i] = st.frame_msg(k)
+                else:
+                    for m in messages[i][0][imu_pos[i]:j]:
+                        self.imu_callback(i, m)
+                    msgs[i] = messages[i][1][k]
                 imu_pos[i] = j
-                msgs[i] = st.frame_msg(k)
             out = self.feature_callbacks(msgs)
             for i, res in out.items():
                 if res is not None:
@@ -210,8 +219,12 @@ class MultiMSCKF:
             if on_frame is not None:
                 on_frame(k, out)
         for i, st in enumerate(streams):        # trailing IMU samples
-            for r in st.imu[imu_pos[i]:]:
-                self.imu_callback(i, _imu_msg(r))
+            if messages is None:
+                for r in st.imu[imu_pos[i]:]:
+                    self.imu_callback(i, _imu_msg(r))
+            else:
+                for m in messages[i][0][imu_pos[i]:]:
+                    self.imu_callback(i, m)
         return [Trajectory.from_results(r) for r in results]
 
 
