@@ -12,6 +12,7 @@
 #   stats          rocprofv3 kernel-trace stats of a short fp32 bench
 #   sq             SQ counters of the hot kernels (one fp32 step)
 #   pmc            FETCH_SIZE / WRITE_SIZE passes (tools/profile_round.sh)
+#   pmc50 / pmc50d / pmc80   the same (+ kernel stats) at 50x400 fp32 / fp64, 80x1000 fp32
 #   seq            the 11-lane scheduler vs single filters (tools/bench_sequences.py)
 #   frame          the drop-in per-frame path (tools/profile_frame.py)
 #   prop           the propagation sweep + kernel stats (tools/gpu/prop.sh)
@@ -42,6 +43,9 @@ for step in "$@"; do
     stats) bash tools/gpu/stats.sh $TAG/st --no-fp64 || exit 1 ;;
     sq) bash tools/gpu/sq.sh $TAG/sq "k_gate|k_info|k_kal|k_feature|k_prop|k_triang" || exit 1 ;;
     pmc) bash tools/profile_round.sh $TAG 3 || exit 1 ;;
+    pmc50) bash tools/profile_round.sh ${TAG}_50x400 2 --N 50 --F 400 --no-fp64 || exit 1 ;;
+    pmc50d) bash tools/profile_round.sh ${TAG}_50x400_fp64 2 --N 50 --F 400 --dtype fp64 || exit 1 ;;
+    pmc80) bash tools/profile_round.sh ${TAG}_80x1000 2 --N 80 --F 1000 --batch 512 --no-fp64 || exit 1 ;;
     seq) run seq 600 python -u tools/bench_sequences.py --seqs 11; tail -c 400 $OUT/seq.out ;;
     frame) run frame 300 python -u tools/profile_frame.py; tail -c 300 $OUT/frame.out ;;
     prop) bash tools/gpu/prop.sh $TAG/prop || exit 1 ;;

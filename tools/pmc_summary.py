@@ -23,9 +23,9 @@ STAGES = [
     ("gate", r"k_gate"),
     ("select", r"k_select"),
     ("compress", r"k_info|k_compress|k_widen"),
-    ("kalman_a", r"k_kal_a|k_kal_mchol<\w+, \d+, \d+, 0"),
+    ("kalman_a", r"k_kal_a|k_kal_mchol<\w+, \d+, \d+, 0|k_gchol_a_|k_gchol_\w+<0"),
     ("kalman_b", r"k_kal_b"),
-    ("kalman_c", r"k_kal_c|k_kal_mchol<\w+, \d+, \d+, 1"),
+    ("kalman_c", r"k_kal_c|k_kal_mchol<\w+, \d+, \d+, 1|k_gchol_c_|k_gchol_\w+<1"),
     ("kalman_e", r"k_kal_e"),
     ("kalman_correct", r"k_correct"),
 ]
