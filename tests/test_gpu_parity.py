@@ -266,14 +266,17 @@ def _batched(problems, dtype, triangulate=True, row_cap=0, cap=None):
     return ctx, ds, feat_off, acc, gam, pw, valid, rows
 
 
-@pytest.mark.parametrize("N,F,B,cap", [(30, 200, 2, 30), (30, 200, 1, 32), (32, 80, 1, None), (34, 60, 1, None),
-                                       (50, 120, 1, None), (50, 120, 1, 50), (80, 40, 1, None), (100, 20, 1, None)])
+@pytest.mark.parametrize("N,F,B,cap", [(30, 200, 2, 30), (30, 200, 1, 32), (32, 80, 1, None), (20, 480, 1, None),
+                                       (34, 60, 1, None), (50, 120, 1, None), (50, 120, 1, 50), (80, 40, 1, None),
+                                       (100, 20, 1, None)])
 def test_batched_fp64_vs_oracle(N, F, B, cap):
     """cap = cam capacity of the context (default N).  Paths exercised:
-    30 -- register-tile Kalman stages, MFMA information assembly
-    (k_info_mfma), one-wave gating for every size class; 30 in cap 32 and
-    32 -- the largest register-tile Kalman window and the full 12 x 12 tile
-    triangle of k_info_mfma (32 cams: C = 192, 864 block-diagonal owners);
+    30 -- register-tile Kalman stages, the fused information assembly
+    (k_info_fused, A stored as its lower triangle), one-wave gating for every
+    size class; 30 in cap 32 and 32 -- the largest register-tile Kalman
+    window and the full 12 x 12 tile triangle (32 cams: C = 192);
+    20 x 480 -- more features per filter than the fused assembly's LDS holds
+    (> 453): Gram records through k_info_mfma (full A) into the same stage B;
     34 (cap 36) -- the one-workgroup-per-tile-row k_info and the smallest
     global-memory Kalman window; 50 (cap 50: four staged features per k_info
     batch, cap 52: three) -- multi-workgroup assembly, global-memory Kalman stages A / C,
