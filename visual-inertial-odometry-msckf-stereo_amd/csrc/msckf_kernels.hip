@@ -268,13 +268,15 @@ __global__ void __launch_bounds__(64) k_propagate(DevState<T> st, Params<T> prm,
                     for (int j = 0; j < 4; ++j) a1 += sk[PK_M1 + 4 * i + j] * q[j];
                     dq[i] = a1;
                 }
-                const T nq = sqrt(dq[0] * dq[0] + dq[1] * dq[1] + dq[2] * dq[2] + dq[3] * dq[3]);
-                for (int i = 0; i < 4; ++i) dq[i] /= nq;
-                const T nn = sqrt(dq[0] * dq[0] + dq[1] * dq[1] + dq[2] * dq[2] + dq[3] * dq[3]);
+                // one division per normalisation on this serial chain (x * (1 / n)
+                // instead of x / n: within an ulp of the reference's division)
+                const T rq = T(1) / sqrt(dq[0] * dq[0] + dq[1] * dq[1] + dq[2] * dq[2] + dq[3] * dq[3]);
+                for (int i = 0; i < 4; ++i) dq[i] *= rq;
+                const T rn = T(1) / sqrt(dq[0] * dq[0] + dq[1] * dq[1] + dq[2] * dq[2] + dq[3] * dq[3]);
                 for (int i = 0; i < 4; ++i) {
                     sk[PK_Q + i] = q[i];
                     sk[PK_DQ + i] = dq[i];
-                    q[i] = dq[i] / nn;
+                    q[i] = dq[i] * rn;
                     sk[PK_QN + i] = q[i];
                 }
             }
@@ -341,10 +343,10 @@ __global__ void __launch_bounds__(64) k_propagate(DevState<T> st, Params<T> prm,
             T p[3] = {s_imu[I_P], s_imu[I_P + 1], s_imu[I_P + 2]};
             for (int k = 0; k < kc; ++k) {
                 T* sk = SK + k * PROP_SC;
-                const T dt = sk[PK_DT];
+                const T dt6 = sk[PK_DT] / T(6);   // off the v / p chains
                 for (int i = 0; i < 3; ++i) {
                     const T v1 = v[i] + sk[PK_H + i], v2 = v[i] + sk[PK_H + 3 + i], v3 = v[i] + sk[PK_H + 6 + i];
-                    const T pn = p[i] + (v[i] + 2 * v1 + 2 * v2 + v3) * dt / T(6);
+                    const T pn = p[i] + (v[i] + 2 * v1 + 2 * v2 + v3) * dt6;
                     const T vn = v[i] + sk[PK_VI + i];
                     sk[PK_V + i] = vn;
                     sk[PK_P + i] = pn;
@@ -460,7 +462,9 @@ __global__ void __launch_bounds__(64) k_propagate(DevState<T> st, Params<T> prm,
                     const int i = 3 * rb + g;
                     const unsigned m = (unsigned)(PM_F2 >> (7 * rb)) & 0x7fu;
                     const T s3 = m ? prop_dot(QQ + i * RS, fcol, m) : T(0);
-                    T ph = (i == c ? T(1) : T(0)) + fo[rb] + f2o[rb] / T(2) + s3 / T(6);
+                    // F^3 / 6 as a multiply by 1/6 (within an ulp of the division; the
+                    // IEEE division sequence sat on every sample's chain)
+                    T ph = (i == c ? T(1) : T(0)) + fo[rb] + f2o[rb] / T(2) + s3 * T(1.0 / 6.0);
                     if (rb == 0 && c < 3) ph = sk[PK_PHI00 + 3 * g + c];
                     PH[i * RS + c] = ph;
                 }
