@@ -379,7 +379,22 @@ def propagation_leg(ctx, args, n_samples=10, steps=5):
             "wall_samples_per_s": round(n * steps / el, 1), "filters": B, "samples_per_filter": n_samples,
             "D": D, "kernel_ms": round(kms, 4),
             "roofline": {"bound": "hbm", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(gbs / HBM_PEAK_GBS, 5), "bytes_per_launch": nbytes}}
+                         "frac": round(gbs / HBM_PEAK_GBS, 5), "bytes_per_launch": nbytes,
+                         "traffic": prop_traffic(args.dtype, B, n_samples, D)}}
+
+
+def prop_traffic(dtype, B, n_samples, D):
+    """HBM bytes of one propagation launch (2 x FETCH_SIZE + WRITE_SIZE) from the
+    committed rocprofv3 passes (profiles/pmc_propagation.json, tools/gpu/prop_pmc.sh),
+    or None if they were taken on another shape."""
+    path = os.path.join(ROOT, "profiles", "pmc_propagation.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as fh:
+        d = json.load(fh)
+    if (d.get("dtype"), d.get("filters"), d.get("samples_per_filter"), d.get("D")) != (dtype, B, n_samples, D):
+        return None
+    return d.get("fetch_x2_bytes_per_launch")
 
 
 def ate_leg():
