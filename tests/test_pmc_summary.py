@@ -55,3 +55,31 @@ def test_committed_summary_has_every_gate_class():
     d = json.load(open(os.path.join(ROOT, "profiles", "pmc_summary.json")))
     gate = d["stages"]["gate"]["kernels"]
     assert "" not in gate and len(gate) >= 2, sorted(gate)
+
+
+def test_stage_map_covers_large_window_choleskys():
+    """The global-memory Cholesky kernels of large windows (k_gchol_*<STAGE, T>)
+    land in kalman_a / kalman_c, not outside every stage."""
+    names = {"void msckf::k_gchol_update<0, float>(msckf::DevState<float>, msckf::UpdWs<float>, int)": "kalman_a",
+             "void msckf::k_gchol_trsm<1, double>(msckf::DevState<double>, msckf::UpdWs<double>, int)": "kalman_c",
+             "void msckf::k_gchol_a_load<float>(msckf::DevState<float>, msckf::UpdWs<float>)": "kalman_a",
+             "void msckf::k_gchol_c_store<double>(msckf::DevState<double>, msckf::UpdWs<double>)": "kalman_c"}
+    import re
+    for n, want in names.items():
+        got = [st for st, rx in pmc_summary.STAGES if re.search(rx, n)]
+        assert got and got[0] == want, (n, got)
+
+
+def test_bench_propagation_traffic_matches_its_shape(tmp_path, monkeypatch):
+    """bench.prop_traffic reads profiles/pmc_propagation.json only for the shape
+    it was measured on."""
+    sys.path.insert(0, ROOT)
+    import bench
+    p = tmp_path / "profiles"
+    p.mkdir()
+    (p / "pmc_propagation.json").write_text(json.dumps(
+        {"dtype": "fp32", "filters": 2048, "samples_per_filter": 10, "D": 201, "fetch_x2_bytes_per_launch": 123}))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    assert bench.prop_traffic("fp32", 2048, 10, 201) == 123
+    assert bench.prop_traffic("fp64", 2048, 10, 201) is None
+    assert bench.prop_traffic("fp32", 1024, 10, 201) is None
