@@ -45,8 +45,9 @@ namespace msckf {
 // column c (or row c):
 //   C1..C5  F dt, F^2, Phi = I + F + F^2/2 + F^3/6 with the edits, Phi G Qc and
 //       the Q term (Phi G Qc G^T) Phi^T
-//   D1..D3  A = Phi P11 and the cumulative Phi, P11' = A Phi^T + Q dt,
-//       P11 = (P11' + P11'^T) / 2
+//   D1, D2  A = Phi P11 and the cumulative Phi, P11' = A Phi^T + Q dt; the
+//       symmetrisation P11 = (P11' + P11'^T) / 2 is formed as the next sample's
+//       D1 reads P11 (and by the write-back after the last sample)
 // Products run over the structurally non-zero 3x3 blocks only (skipped terms
 // are exact zeros: same sums, same order); the lane's Phi rows stay in
 // registers for C5, D1 and D2.  The IMU x cam cross block is updated once with
@@ -211,6 +212,7 @@ __global__ void __launch_bounds__(64) k_propagate(DevState<T> st, Params<T> prm,
     const int le = lane < 63 ? lane : 62;
     const int g = le / 21, c = le - 21 * (le / 21);
     constexpr bool act = true;
+    bool symm = false;   // P11 in Pa still needs the last sample's symmetrisation
     for (int k0 = 0; k0 < n; k0 += PKC) {
         const int kc = min(PKC, n - k0);
         PPROBE_T(t_c0);
@@ -533,8 +535,18 @@ __global__ void __launch_bounds__(64) k_propagate(DevState<T> st, Params<T> prm,
             // ---- D1: A = Phi P11 (column c), cumulative Phi (row c of its transpose) ----
             if (act) {
                 T prow[21], crow[21];
+                // P11 = (P11' + P11'^T) / 2 (msckf.py:362-363) of the previous sample,
+                // formed as it is read (row c = column c) instead of in a phase of its
+                // own; the launch's first sample reads P11 as loaded
+                if (symm) {
 #pragma unroll
-                for (int q = 0; q < 21; ++q) { prow[q] = Pa[c * RS + q]; crow[q] = cTa[c * RS + q]; }   // P11 symmetric
+                    for (int q = 0; q < 21; ++q) prow[q] = (Pa[c * RS + q] + Pa[q * RS + c]) / T(2);
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 21; ++q) prow[q] = Pa[c * RS + q];
+                }
+#pragma unroll
+                for (int q = 0; q < 21; ++q) crow[q] = cTa[c * RS + q];
 #pragma unroll
                 for (int rb = 0; rb < 7; ++rb) {
                     const int i = 3 * rb + g;
@@ -565,21 +577,12 @@ __global__ void __launch_bounds__(64) k_propagate(DevState<T> st, Params<T> prm,
             PPROBE_T(t_s4);
             t_ph[4] += t_s4 - t_s3;
 #endif
-            // ---- D3: P11 = (P11' + P11'^T) / 2 (msckf.py:362-363) ----
-            if (act) {
-#pragma unroll
-                for (int jb = 0; jb < 7; ++jb) {
-                    const int j = 3 * jb + g;
-                    Pb[c * RS + j] = (Pa[c * RS + j] + Pa[j * RS + c]) / T(2);
-                }
-            }
-            prop_sync();
 #ifdef MSCKF_GATE_PROBE
             PPROBE_T(t_s5);
             t_ph[5] += t_s5 - t_s4;
 #endif
-            T* t = Pa; Pa = Pb; Pb = t;
-            t = cTa; cTa = cTb; cTb = t;
+            symm = true;
+            T* t = cTa; cTa = cTb; cTb = t;   // P11' stays in Pa, A in Pb
         }
     }
     PPROBE_T(t_end0);
@@ -589,7 +592,7 @@ __global__ void __launch_bounds__(64) k_propagate(DevState<T> st, Params<T> prm,
     // write back P11 and the IMU record; the cross blocks with the cumulative Phi
     for (int e = lane; e < 441; e += 64) {
         const int i = e / 21, j = e - 21 * i;
-        P[i * ld + j] = Pa[i * RS + j];
+        P[i * ld + j] = (Pa[i * RS + j] + Pa[j * RS + i]) / T(2);   // the last sample's symmetrisation
         PH[i * RS + j] = cTa[j * RS + i];   // cumulative Phi, row-major
     }
     if (lane < IMU_STRIDE) imu[lane] = s_imu[lane];
