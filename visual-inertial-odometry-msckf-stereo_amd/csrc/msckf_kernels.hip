@@ -68,10 +68,9 @@ __device__ __forceinline__ T skew_sel(const T* w, int r, int c) {
     return r == c ? T(0) : ((d == 1 || d == 4) ? -v : v);
 }
 
-// LDS row strides of the 21-wide matrices and of Phi G Qc (21 x 12): a lane per
+// LDS row strides of the 21-wide matrices: a lane per
 // row (stride RS) hits distinct banks (25 dwords; 42 dwords per fp64 row)
 template <typename T> constexpr int prop_rs() { return sizeof(T) == 4 ? 25 : 21; }
-constexpr int PGS = 13;
 template <typename T> constexpr int prop_mat() { return 21 * prop_rs<T>(); }
 constexpr int PROP_SC = 104;   // per-sample scalars (PropSample)
 enum PropSample { PK_DT = 0, PK_W = 1, PK_A = 4, PK_M1 = 7, PK_M2 = 23, PK_Q = 39, PK_DQ = 43, PK_QN = 47,
@@ -181,7 +180,7 @@ __global__ void __launch_bounds__(64) k_propagate(DevState<T> st, Params<T> prm,
     T* cTb = cTa + MAT;
     T* PH = cTb + MAT;                       // Phi_k
     T* QQ = PH + MAT;                        // F^2, then (Phi G Qc G^T) Phi^T
-    T* FP = QQ + MAT;                        // F dt, then Phi G Qc (21 x 12)
+    T* FP = QQ + MAT;                        // F dt
     T* SK = FP + MAT;                        // [PKC][PROP_SC]
     T* s_imu = SK + PKC * PROP_SC;
     T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
@@ -500,18 +499,19 @@ __global__ void __launch_bounds__(64) k_propagate(DevState<T> st, Params<T> prm,
                 for (int q = 0; q < 21; ++q)
                     phr[rb][q] = (m >> (q / 3) & 1u) && act ? PH[(3 * rb + g) * RS + q] : T(0);
             }
-            // ---- C4: Phi G Qc (G: jit_utils.py:30-34), row c, columns 3 mb + g ----
+            // ---- C4 + C5: Q term row c: (Phi G Qc G^T)[c][q] Phi[j][q], j = 3 jb + g.
+            // Every lane forms all of row c of Phi G Qc (G: jit_utils.py:30-34) from
+            // row c of Phi itself -- 12 entries, no exchange through LDS ----
             if (act) {
                 const T* ph = PH + c * RS;
-                FP[c * PGS + g] = ph[g] * T(-1) * prm.qc_gyro;
-                FP[c * PGS + 3 + g] = ph[3 + g] * T(1) * prm.qc_gbias;
-                FP[c * PGS + 6 + g] = (ph[6] * -R[3 * g] + ph[7] * -R[3 * g + 1] + ph[8] * -R[3 * g + 2]) * prm.qc_acc;
-                FP[c * PGS + 9 + g] = ph[9 + g] * T(1) * prm.qc_abias;
-            }
-            prop_sync();
-            // ---- C5: Q term row c: (Phi G Qc G^T)[c][q] Phi[j][q], j = 3 jb + g ----
-            if (act) {
-                const T* pg = FP + c * PGS;
+                T pg[12];
+#pragma unroll
+                for (int r = 0; r < 3; ++r) {
+                    pg[r] = ph[r] * T(-1) * prm.qc_gyro;
+                    pg[3 + r] = ph[3 + r] * T(1) * prm.qc_gbias;
+                    pg[6 + r] = (ph[6] * -R[3 * r] + ph[7] * -R[3 * r + 1] + ph[8] * -R[3 * r + 2]) * prm.qc_acc;
+                    pg[9 + r] = ph[9 + r] * T(1) * prm.qc_abias;
+                }
                 T fr[12];
 #pragma unroll
                 for (int q = 0; q < 12; ++q) {
