@@ -247,6 +247,68 @@ def test_update_empty_is_noop():
     np.testing.assert_array_equal(P, d["P"])
 
 
+def _debug_call(ctx, name, *args):
+    import ctypes as C
+    fn = getattr(ctx.lib, name)
+    if name == "msckf_debug_set_workspace":
+        fn.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_double), C.c_size_t]
+    else:
+        fn.argtypes = [C.c_void_p]
+    fn.restype = C.c_int
+    ctx._check(fn(ctx.h, *args))
+
+
+@pytest.mark.parametrize("ncams,chol", [(10, "tiles"), (10, "mfma"), (34, "tiles")])
+@pytest.mark.parametrize("depth,fails", [(1e-12, False), (1e-6, True)])
+def test_stage_c_pivot_bound_every_path(ncams, chol, depth, fails, monkeypatch):
+    """Stage C floors a pivot of T = s2 I + Lc^T A Lc at s2 only down to
+    -1e-9 x max diag(T), and fails the update below that (rc -3, "innovation
+    covariance"), on every path: register tiles (k_kal_c1), fp64 MFMA
+    (k_kal_mchol) and the global-memory Cholesky of windows over 32 cams
+    (k_gchol_diag<1>, 34 cams).  T is driven through the debug hooks: with
+    P = diag(p), Lc = diag(sqrt(p_cc)), and A = Lc^-T (D - s2 I) Lc^-1 makes
+    T = D to rounding; D = I but one entry -depth (-1e-12: rounding level,
+    floored; -1e-6: a corrupted T)."""
+    import ctypes as C
+    monkeypatch.setenv("MSCKF_KALMAN_CHOL", chol)
+    pr = synth.make_update_problem(ncams, 40, seed=77)
+    d = problem_to_dict(pr)
+    Cn, D = 6 * ncams, 21 + 6 * ncams
+    p = 1e-3 * (1.0 + np.random.default_rng(5).random(D))
+    P = np.diag(p)
+    ctx = Context(FilterConfig(), n_filters=1, n_cam_capacity=ncams, dtype=np.float64)
+    imu, cams = imu_record(d), pack_cams(pr.cam_q, pr.cam_p, pr.cam_q_null)
+    ctx.set_state(0, imu, cams, P)
+    ctx.batch_load([0, pr.F], pr.obs_off, pr.obs_cam, pr.obs_z, None, np.full(pr.F, 1e30))
+    ctx.batch_update(row_cap=0, triangulate=True)
+    rows = ctx.batch_results()[4]
+    assert rows[0] > 0
+    s2 = FilterConfig().observation_noise
+    dg = np.ones(Cn)
+    dg[Cn // 2] = -depth
+    H = np.zeros((Cn, Cn + 1))
+    H[:, :Cn] = np.diag((dg - s2) / p[21:])
+    H[:, Cn] = 1e-3
+    ctx.set_state(0, imu, cams, P)   # the pre-update state again
+    _debug_call(ctx, "msckf_debug_set_workspace", 6, H.ctypes.data_as(C.POINTER(C.c_double)), H.size)
+    _debug_call(ctx, "msckf_debug_kalman")
+    if fails:
+        with pytest.raises(RuntimeError, match="innovation covariance not positive definite.*rc=-3"):
+            ctx.batch_results()
+    else:
+        ctx.batch_results()
+        _, _, P1 = ctx.get_state(0)
+        assert np.isfinite(P1).all()
+        # P+_cc = s2 Lc T^-1 Lc^T = s2 diag(p_cc / T_ii): the floored pivot (s2 in
+        # place of -1e-12) leaves its variance unchanged, the others shrink by s2
+        dd = np.diag(P1)[21:]
+        k = Cn // 2
+        assert abs(dd[k] - p[21 + k]) < 1e-9 * p[21 + k]
+        other = np.arange(Cn) != k
+        np.testing.assert_allclose(dd[other], s2 * p[21:][other], rtol=1e-9)
+    ctx.close()
+
+
 # --------------------------------------------------- full-size batched mode --
 
 def _batched(problems, dtype, triangulate=True, row_cap=0, cap=None):

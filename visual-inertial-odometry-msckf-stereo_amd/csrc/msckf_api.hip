@@ -461,6 +461,21 @@ int load_features(msckf_ctx* c, int nf, const int32_t* feat_off, int single_filt
         }
         for (int k = 0; k < GateClasses::NC; ++k) {
             gc.off[k] = (int)gflat.size();
+            if (k == GateClasses::NC - 2) {   // large tracks by block count (the fp32 launches split them)
+                constexpr int NS = GateClasses::BIG_NB1 - GateClasses::BIG_NB0 + 1;
+                std::vector<int> sub[NS];
+                for (int f : cls[k]) {
+                    const int M = obs_off[f + 1] - obs_off[f], nb = (3 * M + 4 + 15) / 16 - GateClasses::BIG_NB0;
+                    sub[nb].push_back(f);
+                    gc.big_maxM[nb] = std::max(gc.big_maxM[nb], M);
+                }
+                for (int j = 0; j < NS; ++j) {
+                    gc.big_off[j] = (int)gflat.size();
+                    gflat.insert(gflat.end(), sub[j].begin(), sub[j].end());
+                }
+                gc.big_off[NS] = (int)gflat.size();
+                continue;
+            }
             gflat.insert(gflat.end(), cls[k].begin(), cls[k].end());
         }
         gc.off[GateClasses::NC] = (int)gflat.size();
@@ -607,6 +622,18 @@ int run_update_chain(msckf_ctx* c, int row_cap, bool triangulate) {
         HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
         join.armed = false;   // the main stream now orders everything after stage A
     }
+    launch_kalman<T>(s, st, prm, ws, &c->timer);
+    HIPC(hipGetLastError());
+    return 0;
+}
+
+template <typename T>
+int run_kalman_only(msckf_ctx* c) {
+    hipStream_t s = c->stream;
+    DevState<T> st = dev_state<T>(c);
+    Params<T> prm = make_params<T>(c);
+    UpdWs<T> ws = upd_ws<T>(c);
+    if (kalman_chol_supported(c->Cmax)) launch_kalman_a_reg<T>(s, st, ws, &c->timer);
     launch_kalman<T>(s, st, prm, ws, &c->timer);
     HIPC(hipGetLastError());
     return 0;
@@ -1333,6 +1360,27 @@ int msckf_debug_workspace(msckf_ctx_t* c, int which, double* out, size_t count) 
     HIPSYNC(c, hipStreamSynchronize(c->stream));
     HIPC(hipMemcpy(out, src, count * sizeof(double), hipMemcpyDeviceToHost));
     return 0;
+}
+
+// Debug (not in include/msckf_hip.h): overwrite the first `count` doubles of a
+// Kalman workspace buffer (6: H_thin [A | b], [B][Cmax][Cmax + 1]) from the host.
+int msckf_debug_set_workspace(msckf_ctx_t* c, int which, const double* in, size_t count) {
+    if (!c || !in) FAIL(-1, "null argument");
+    void* dst = which == 6 ? (void*)c->Hthin.p : nullptr;
+    if (!dst) FAIL(-1, "unknown workspace %d", which);
+    if (count * sizeof(double) > c->Hthin.cap) FAIL(-1, "%zu doubles exceed H_thin", count);
+    HIPSYNC(c, hipStreamSynchronize(c->stream));
+    HIPC(hipMemcpy(dst, in, count * sizeof(double), hipMemcpyHostToDevice));
+    return 0;
+}
+
+// Debug: the Kalman stages alone -- stage A (on the main stream), B, C, E and the
+// state correction -- on the batch's current H_thin and stacking info, so that a
+// test can drive the innovation factorisation with a chosen information matrix.
+int msckf_debug_kalman(msckf_ctx_t* c) {
+    if (c) c->last_async = "msckf_debug_kalman";
+    if (!c) FAIL(-1, "null context");
+    return DISPATCH(c, run_kalman_only, c);
 }
 
 }  // extern "C"

@@ -1,5 +1,6 @@
 // msckf_gate_mfma.hip -- chi^2 gating of the fp32 contexts (msckf.py:606-614)
-// on fp32 MFMA tiles, one wavefront per feature (M <= 40).
+// on fp32 MFMA tiles: one wavefront per feature (M <= 41), and for the large
+// tracks (41 < M <= 82) a 2- to 8-wave workgroup per feature (k_gate_mfma_wt).
 //
 // Same mathematics as k_gate_wave (msckf_kernels.hip): gamma = r0^T S^-1 r0
 // is read off an LDL^T elimination of the rank-3 reduced saddle-point matrix
@@ -98,7 +99,7 @@ __host__ __device__ constexpr int gm_wave_floats(int Mmax, int capf, int RS = 1)
 }
 // Pair k = a (a + 1) / 2 + b (b <= a) of the Y phase: a | b << 8 | (stage offset
 // of element (3a, 3b)) << 16, one table load instead of a square-root decode.
-constexpr int GM_MAXM = 41;   // gm_nb(41) = 8, the largest one-wave class
+constexpr int GM_MAXM = 84;   // gm_nb(84) = 16: the fp32 large-track class (k_gate_mfma_wt)
 struct GmPairTab {
     unsigned v[GM_MAXM * (GM_MAXM + 1) / 2];
     constexpr GmPairTab() : v() {
@@ -656,202 +657,194 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_wav
 }
 
 // ---------------------------------------------------------------------------
-// Large tracks (40 < M <= 82, nb <= 16 blocks): the same MFMA elimination on a
-// workgroup of four waves per feature.  Wave w owns block rows RB = w + 4 i
-// (i < 4) -- at most 40 accumulator blocks (acc row i holds blocks 0..4 i + 3).
-// Per 4-pivot step the owners of the pivot columns dump them to a
-// double-buffered LDS panel, one barrier, then every wave factors the 4x4
-// diagonal, forms the B operands of every block row and the A operands of its
-// own rows, and updates its blocks.  The Y pairs are staged in passes over
-// observation rows by all 256 threads, each pass followed by the owners'
-// assembly.  (Replaces k_gate_big's fp64 register tiles in the fp32 contexts.)
-constexpr int GW_NB = 16;
-__host__ __device__ constexpr int gw_off(int i) { return 2 * i * (i + 1); }
-__host__ __device__ constexpr int gw_pan() { return 2 * 16 * GW_NB * 4; }   // floats, double-buffered
-__host__ __device__ constexpr int gw_floats(int Mmax, int capb) {
-    return gm_head(Mmax) + gw_pan() + ((9 * capb + 3) & ~3) + ((Mmax + 3) & ~3);
+// Large tracks, round 6: k_gate_mfma_wt<NB, W> -- the one-wave kernel's
+// elimination spread over a W-wave workgroup per feature of exactly NB blocks
+// (the host lists the 40 < M <= 82 class by block count, GateClasses::big_off).
+// Wave WV owns block rows RB = WV + W i: every wave runs its own compile-time
+// specialised body (gt_body<NB, W, WV>), so its accumulator slots, block
+// indices and trailing-update ranges are constants -- no per-block branches,
+// no slots for blocks right of the diagonal.  Per 4-pivot step the owners of
+// the pivot columns dump them to a double-buffered LDS panel, one barrier,
+// then every wave factors the 4x4 diagonal itself (one-hot solves, no
+// divisions or selects, as k_gate_mfma), reads the B operands of the block
+// rows at or below the panel and updates its own blocks with one
+// v_mfma_f32_16x16x4_f32 each.  The Y pairs come from the dense lower stage
+// and the pair table of the one-wave kernel, staged by all 64 W threads in
+// block-row passes, each followed by the owners' assembly.
+// (Replaces round 5's k_gate_mfma_wg: runtime block counts, the B operands of
+// all 16 block rows formed every step, a square-root pair decode and per-
+// element index arithmetic in the assembly -- 6.0k VALU per wave at 50x400.)
+constexpr int GT_NBMIN = 9, GT_NBMAX = 16;   // block counts k_gate_mfma_wt is built for (41 < M <= 84)
+__host__ __device__ constexpr int gt_rows(int NB, int W, int WV) { return WV < NB ? (NB - 1 - WV) / W + 1 : 0; }
+__host__ __device__ constexpr int gt_off(int W, int WV, int i) { return i * (WV + 1) + W * i * (i - 1) / 2; }
+__host__ __device__ constexpr int gt_slots(int NB, int W, int WV) { return gt_off(W, WV, gt_rows(NB, W, WV)); }
+__host__ __device__ constexpr int gt_maxslots(int NB, int W) {
+    int m = 0;
+    for (int v = 0; v < W; ++v) m = gt_slots(NB, W, v) > m ? gt_slots(NB, W, v) : m;
+    return m;
+}
+// waves per SIMD the largest wave's accumulators leave room for
+__host__ __device__ constexpr int gt_waves(int NB, int W) {
+    return 4 * gt_maxslots(NB, W) + 96 <= 168 ? 3 : (4 * gt_maxslots(NB, W) + 96 <= 256 ? 2 : 1);
+}
+// LDS (floats): records | stage / [2][16 NB][4] panel | junk [W][64] | B rows [4][16 NB], zero row [16 NB] | slot, coff
+__host__ __device__ constexpr int gt_area(int NB, int capf) { return capf + 16 > 128 * NB ? ((capf + 16 + 3) & ~3) : 128 * NB; }
+__host__ __device__ constexpr int gt_floats(int Mmax, int NB, int W, int capf) {
+    return gm_head(Mmax) + gt_area(NB, capf) + 64 * W + 80 * NB + 2 * ((Mmax + 3) & ~3);
 }
 
-__global__ void __launch_bounds__(256) k_gate_mfma_wg(DevState<float> st, Params<float> prm, FeatBatch<float> fb,
-                                                      const int* __restrict__ flist, int Mmax, int capb) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int f = __builtin_amdgcn_readfirstlane(flist[blockIdx.x]);
-    if (!fb.valid[f]) {
-        if (tid == 0) { fb.gamma[f] = NAN; fb.accept[f] = 0; }
-        return;
-    }
-    const float chi2 = fb.chi2[f];
-    const int b = __builtin_amdgcn_readfirstlane(fb.feat_filter[f]);
-    const int o0 = __builtin_amdgcn_readfirstlane(fb.obs_off[f]);
-    const int M = __builtin_amdgcn_readfirstlane(fb.obs_off[f + 1]) - o0, M3 = 3 * M;
-    const int nY = (M3 + 3) >> 2;
-    const int nb = gm_nb(M);
-    const int nB = 16 * nb - 4;
-    float* ht = reinterpret_cast<float*>(smem_raw);
-    float* rt = ht + 18 * Mmax;
-    float* pan = ht + gm_head(Mmax);               // [2][16 GW_NB][4]
-    float* stage = pan + gw_pan();                 // [capb][9]
-    int* slot = reinterpret_cast<int*>(stage + ((9 * capb + 3) & ~3));
-    {   // records as element pairs and cam slots, all loads issued before the first wait (as k_gate_mfma)
-        constexpr int NCH = (12 * 84 + 255) / 256;   // gm_nb(M) <= GW_NB: M <= 84
-        const F2* src = reinterpret_cast<const F2*>(fb.obs_ht + (size_t)o0 * OBS_HTS);
-        F2 cv[NCH];
-#pragma unroll
-        for (int j = 0; j < NCH; ++j) {
-            const int k = tid + 256 * j;
-            cv[j] = k < 12 * M ? src[k] : F2{0, 0};
-        }
-        const int sl = tid < M ? fb.obs_cam[o0 + tid] : 0;
-#pragma unroll
-        for (int j = 0; j < NCH; ++j) {
-            const int k = tid + 256 * j, o = k / 12, e = 2 * (k - 12 * o);
-            if (k < 12 * M) {
-                if (e < OBS_RT) *reinterpret_cast<F2*>(ht + 18 * o + e) = cv[j];
-                else if (e < OBS_RT + 4) *reinterpret_cast<F2*>(rt + 4 * o + (e - OBS_RT)) = cv[j];
-            }
-        }
-        if (tid < M) slot[tid] = sl;
-    }
-    __syncthreads();
-    float rn2 = 0;
-    for (int e = 4 * lane + 3; e < 4 * M; e += 256) rn2 += rt[e] * rt[e];
-    rn2 = wave_sum(rn2);
+template <int NB, int W, int WV>
+__device__ __forceinline__ void gt_body(const DevState<float>& st, const FeatBatch<float>& fb, int f, int b, int M,
+                                        float s2, float chi2, float* ht, float* rt, float* area, float* junk,
+                                        float* brow, float* zrow, const int* slot, const int* coff, int capf) {
+    constexpr int NT = 64 * W, R = gt_rows(NB, W, WV), NS = gt_slots(NB, W, WV);
+    constexpr int nB = 16 * NB - 4;
+    const int tid = threadIdx.x, lane = tid & 63, M3 = 3 * M;
+    float* stage = area;
+    float* pan = area;
+    F4 acc[NS > 0 ? NS : 1];
 
-    const int col_l = lane & 15, rg = lane >> 4;
-    F4 acc[gw_off(4)];
-    const float s2 = prm.sigma2;
-    // Assembly of this wave's blocks (RB = w + 4 i, CB = c <= RB) whose block
-    // row lies in [R0, R1): every element written once, as in k_gate_mfma --
-    // Y entries from the pass's pair stage (kbase = its first pair), B rows,
-    // unit padding pivots, zeros.  The Y passes are aligned to block rows, so
-    // no accumulator is ever read back (a read-modify-write kept ~100 of them
-    // live in VGPRs across the pass loop).
-    auto assemble = [&](int R0, int R1, int kbase) {
-        // opaque copies: the index arithmetic stays inside the pass loop
-        int col_l = lane & 15, rg = lane >> 4;
-        asm volatile("" : "+v"(col_l), "+v"(rg));
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int RB = w + 4 * i;
-            if (RB >= nb || RB < R0 || RB >= R1) continue;
-            const bool brow = RB == nb - 1 && rg == 3;
-            int rofs[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int q = 16 * RB + 4 * rg + r, oa = q / 3;
-                rofs[r] = 9 * (oa * (oa + 1) / 2 - kbase) + 3 * (q - 3 * oa);
-            }
-#pragma unroll
-            for (int c = 0; c < 4 * i + 4; ++c) {
-                if (c > RB) continue;
-                const int p = 16 * c + col_l, ob = p / 3, cp = p - 3 * ob;
-                float bval[4] = {0.f, 0.f, 0.f, 0.f};
-                if (RB == nb - 1) {
-                    const bool pv = brow && p < M3;
-                    const int o = pv ? ob : 0;
-#pragma unroll
-                    for (int r = 0; r < 3; ++r) bval[r] = pv ? -ht[18 * o + 6 * cp + 3 + r] : 0.f;
-                    bval[3] = pv ? rt[4 * o + cp] : 0.f;
-                }
-                F4 a;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int q = 16 * RB + 4 * rg + r;
-                    const bool take = q < M3 && q >= p;
-                    const float y = stage[take ? rofs[r] + 9 * ob + cp : 0];
-                    float v = bval[r];
-                    if (q == p && q >= M3 && q < nB) v = 1.f;
-                    a[r] = take ? y + (q == p ? s2 : 0.f) : v;
-                }
-                acc[gw_off(i) + c] = a;
-                asm volatile("" : "+a"(acc[gw_off(i) + c]));
-            }
-        }
-    };
-
+    // ---- Y: pair blocks Ht_a P_ab Ht_b^T into the dense lower stage, in passes of block rows
     const float* P = st.P + (size_t)b * st.Dmax * st.Dmax;
     const int ldp = st.Dmax;
-    // Y passes over block rows [R0, R1): the pairs of observation rows
-    // [16 R0 / 3, (16 R1 - 1) / 3] (rows straddling a pass boundary twice)
-    for (int R0 = 0; R0 < nb;) {
+    const float* Prow[6];
+#pragma unroll
+    for (int u = 0; u < 6; ++u) Prow[u] = P + u * ldp;
+    auto npairs = [&](int lo, int hi) { return hi < lo ? 0 : (hi + 1) * (hi + 2) / 2 - lo * (lo + 1) / 2; };
+    for (int R0 = 0; R0 < NB;) {
         const int alo = (16 * R0) / 3;
         int R1 = R0 + 1, ahi = min(M - 1, (16 * R1 - 1) / 3);
-        auto npairs = [&](int lo, int hi) { return hi < lo ? 0 : (hi * (hi + 1) / 2 + hi + 1) - lo * (lo + 1) / 2; };
-        while (R1 < nb) {
+        while (R1 < NB) {
             const int ah2 = min(M - 1, (16 * (R1 + 1) - 1) / 3);
-            if (npairs(alo, ah2) > capb) break;
+            if (gm_dense(alo, ah2) > capf) break;
             ++R1;
             ahi = ah2;
         }
         const int kbase = alo * (alo + 1) / 2, nbp = npairs(alo, ahi);
-#pragma unroll 1
-        for (int kk = tid; kk < nbp; kk += 256) {
-            const int k = kbase + kk;
-            int a = (int)((sqrtf(8.0f * (float)k + 1.0f) - 1.0f) * 0.5f);
-            if (a * (a + 1) / 2 > k) --a;
-            if ((a + 1) * (a + 2) / 2 <= k) ++a;
-            const int bo = k - a * (a + 1) / 2;
-            const float* Pb = P + (size_t)(21 + 6 * slot[a]) * ldp + 21 + 6 * slot[bo];
+        const int soff0 = gm_rowoff(3 * alo);
+        unsigned pen = g_gm_pairs.v[kbase + (tid < nbp ? tid : 0)];
+        for (int kk = tid; kk < nbp; kk += NT) {
+            const unsigned pe = pen;
+            if (kk + NT < nbp) pen = g_gm_pairs.v[kbase + kk + NT];
+            const int a = pe & 0xff, bo = (pe >> 8) & 0xff;
+            const unsigned boff = (unsigned)(slot[a] + coff[bo]) * (unsigned)sizeof(float);
             float Pl[36];
 #pragma unroll
-            for (int u = 0; u < 6; ++u) __builtin_memcpy(Pl + 6 * u, Pb + (size_t)u * ldp, 6 * sizeof(float));
+            for (int u = 0; u < 6; ++u)
+                __builtin_memcpy(Pl + 6 * u, reinterpret_cast<const char*>(Prow[u]) + boff, 6 * sizeof(float));
             const float* Ha = ht + 18 * a;
             const float* Hb = ht + 18 * bo;
-            float* dst = stage + 9 * kk;
+            float* d0 = stage + ((int)(pe >> 16) - soff0);
+            float* dst[3] = {d0, d0 + 3 * a + 3, d0 + 6 * a + 7};
+            F2 hb01[6];
+#pragma unroll
+            for (int u = 0; u < 6; ++u) hb01[u] = F2{Hb[3 * u], Hb[3 * u + 1]};
 #pragma unroll
             for (int x = 0; x < 3; ++x) {
                 F2 t2[3] = {F2{0, 0}, F2{0, 0}, F2{0, 0}};
 #pragma unroll
                 for (int u = 0; u < 6; ++u) {
-                    const float h = Ha[6 * x + u];
+                    const float h = Ha[3 * u + x];
 #pragma unroll
                     for (int c = 0; c < 3; ++c)
                         t2[c] = __builtin_elementwise_fma(F2{h, h}, F2{Pl[6 * u + 2 * c], Pl[6 * u + 2 * c + 1]}, t2[c]);
                 }
                 const float t1[6] = {t2[0].x, t2[0].y, t2[1].x, t2[1].y, t2[2].x, t2[2].y};
+                F2 y01 = {0, 0};
+                float y2 = 0;
 #pragma unroll
-                for (int y = 0; y < 3; ++y) {
-                    float acc_y = 0;
-#pragma unroll
-                    for (int u = 0; u < 6; ++u) acc_y = fmaf(t1[u], Hb[6 * y + u], acc_y);
-                    dst[3 * x + y] = acc_y;
+                for (int u = 0; u < 6; ++u) {
+                    y01 = __builtin_elementwise_fma(F2{t1[u], t1[u]}, hb01[u], y01);
+                    y2 = fmaf(t1[u], Hb[3 * u + 2], y2);
                 }
+                dst[x][0] = y01.x;
+                dst[x][1] = y01.y;
+                dst[x][2] = y2;
             }
         }
         __syncthreads();
-        assemble(R0, R1, kbase);
-        __syncthreads();
+        // assembly of this wave's block rows in [R0, R1) (as gm_assemble)
+        {
+            int col_l = lane & 15, rg = lane >> 4;
+            asm volatile("" : "+v"(col_l), "+v"(rg));
+            int r[4];
+            bool up[4], dg[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                r[i] = 4 * rg + i;
+                up[i] = r[i] < col_l;
+                dg[i] = r[i] == col_l;
+            }
+#pragma unroll
+            for (int i = 0; i < R; ++i) {
+                const int RB = WV + W * i;
+                if (RB < R0 || RB >= R1) continue;   // uniform
+                const float* src[4];
+#pragma unroll
+                for (int ii = 0; ii < 4; ++ii) {
+                    const int q = 16 * RB + r[ii];
+                    const float* ptr = stage + (gm_rowoff(q) - soff0) + col_l;
+                    if (RB >= NB - 2) {
+                        ptr = q < M3 ? ptr : zrow + col_l;
+                        if (RB == NB - 1) ptr = q >= nB ? brow + (q - nB) * (16 * NB) + col_l : ptr;
+                    }
+                    src[ii] = ptr;
+                }
+#pragma unroll
+                for (int c = 0; c <= RB; ++c) {
+                    F4 v;
+#pragma unroll
+                    for (int ii = 0; ii < 4; ++ii) v[ii] = src[ii][16 * c];
+                    if (c == RB) {
+#pragma unroll
+                        for (int ii = 0; ii < 4; ++ii) {
+                            const int q = 16 * RB + r[ii];
+                            const float dv = RB < NB - 2 ? s2 : (q < M3 ? s2 : (q < nB ? 1.f : 0.f));
+                            v[ii] = up[ii] ? 0.f : (dg[ii] ? v[ii] + dv : v[ii]);
+                        }
+                    }
+                    acc[gt_off(W, WV, i) + c] = v;
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+        }
+        __syncthreads();   // stage reads done before the next pass / the panel reuse
         R0 = R1;
     }
 
-    bool fail = false;
-    const int csel = rg;
+    // ---- blocked LDL^T, 4 pivots per step, MFMA trailing updates
+    const int col_l = lane & 15, rg = lane >> 4, csel = rg;
+    const bool owner[4] = {(col_l >> 2) == 0, (col_l >> 2) == 1, (col_l >> 2) == 2, (col_l >> 2) == 3};
+    float* jk = junk + lane;
+    float dmin = 1.f;
+    float onehot[4];
 #pragma unroll
-    for (int KB = 0; KB < GW_NB; ++KB) {
-        if (4 * KB >= nY || fail) break;
+    for (int k = 0; k < 4; ++k) onehot[k] = csel == k ? 1.f : 0.f;
+#pragma unroll
+    for (int KB = 0; KB < NB; ++KB) {
+#pragma unroll
         for (int sc = 0; sc < 4; ++sc) {
-            const int j = 4 * KB + sc;
-            if (j >= nY) break;
-            const int p0 = 4 * j;
-            float* pb = pan + (j & 1) * (16 * GW_NB * 4);
-            if ((col_l >> 2) == sc) {
+            if (KB == NB - 1 && sc == 3) break;   // the last four rows are the B rows
+            const int p0 = 16 * KB + 4 * sc;
+            float* pb = pan + ((4 * KB + sc) & 1) * (64 * NB);
+            // 1. the owners of columns p0 .. p0 + 3 dump this wave's blocks (RB, KB)
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    if (KB >= 4 * i + 4) continue;   // no block (RB, KB) in acc row i (compile time)
-                    const int RB = w + 4 * i;
-                    if (RB < KB || RB >= nb) continue;
-                    const F4 v = acc[gw_off(i) + KB];
-                    float* dd = pb + 4 * (16 * RB + 4 * rg) + (col_l & 3);
-                    dd[0] = v[0]; dd[4] = v[1]; dd[8] = v[2]; dd[12] = v[3];
-                }
+            for (int i = 0; i < R; ++i) {
+                const int RB = WV + W * i;
+                if (RB < KB) continue;
+                const F4 v = acc[gt_off(W, WV, i) + KB];
+                float* dd = owner[sc] ? pb + 4 * (16 * RB + 4 * rg) + (col_l & 3) : jk;
+                dd[0] = v[0]; dd[4] = v[1]; dd[8] = v[2]; dd[12] = v[3];
             }
             LDS_BARRIER();
+            // 2. every wave factors A_d = L D L^T
             const F4 r0 = *reinterpret_cast<const F4*>(pb + 4 * p0);
             const F4 r1 = *reinterpret_cast<const F4*>(pb + 4 * p0 + 4);
             const F4 r2 = *reinterpret_cast<const F4*>(pb + 4 * p0 + 8);
             const F4 r3 = *reinterpret_cast<const F4*>(pb + 4 * p0 + 12);
+            float bv[NB];
+#pragma unroll
+            for (int CB = KB; CB < NB; ++CB) bv[CB] = pb[4 * (16 * CB + col_l) + csel];
             const float d0 = r0.x, e0 = pivot_rcp(d0);
             const float l10 = r1.x * e0, l20 = r2.x * e0, l30 = r3.x * e0;
             const float d1 = r1.y - l10 * r1.x, e1 = pivot_rcp(d1);
@@ -861,51 +854,49 @@ __global__ void __launch_bounds__(256) k_gate_mfma_wg(DevState<float> st, Params
             const float m32 = r3.z - l30 * r2.x - l31 * m21;
             const float l32 = m32 * e2;
             const float d3 = r3.w - l30 * r3.x - l31 * m31 - l32 * m32;
-            if (!(d0 > 0.f) || !(d1 > 0.f) || !(d2 > 0.f) || !(d3 > 0.f)) { fail = true; break; }   // same in every wave
+            dmin = fminf(dmin, fminf(fminf(d0, d1), fminf(d2, d3)));
+            // formed here: a wave with no block row left would otherwise sink the
+            // pivots of every later step to the end, their panel rows live till then
+            asm volatile("" : "+v"(dmin));
             const float e3 = pivot_rcp(d3);
-            const float i10 = -l10, i21 = -l21, i32 = -l32;
-            const float i20 = -l20 - l21 * i10, i31 = -l31 - l32 * i21;
-            const float i30 = -l30 - l31 * i10 - l32 * i20;
-            const float g0 = csel == 0 ? 1.f : (csel == 1 ? i10 : (csel == 2 ? i20 : i30));
-            const float g1 = csel == 0 ? 0.f : (csel == 1 ? 1.f : (csel == 2 ? i21 : i31));
-            const float g2 = csel <= 1 ? 0.f : (csel == 2 ? 1.f : i32);
-            const float g3 = csel == 3 ? 1.f : 0.f;
-            const float esel = -(csel == 0 ? e0 : (csel == 1 ? e1 : (csel == 2 ? e2 : e3)));
-            // B operands of every block row, four panel rows in flight at a time (VGPR budget)
-            float bv[GW_NB];
+            const float h0 = onehot[0];
+            const float h1 = fmaf(-l10, h0, onehot[1]);
+            const float h2 = fmaf(-l21, h1, fmaf(-l20, h0, onehot[2]));
+            const float h3 = fmaf(-l32, h2, fmaf(-l31, h1, fmaf(-l30, h0, onehot[3])));
+            const float u0 = h0 * e0, u1 = h1 * e1, u2 = h2 * e2, u3 = h3 * e3;
+            const float m2 = fmaf(-l32, u3, u2);
+            const float m1 = fmaf(-l31, u3, fmaf(-l21, m2, u1));
+            const float m0 = fmaf(-l30, u3, fmaf(-l20, m2, fmaf(-l10, m1, u0)));
+            const float mm3 = -u3, mm2 = -m2, mm1 = -m1, mm0 = -m0;
+            // 3. this wave's block rows at or below the panel: C -= X A_d^-1 X^T
 #pragma unroll
-            for (int CB = KB; CB < GW_NB; ++CB) {
-                const F4 x = *reinterpret_cast<const F4*>(pb + 4 * (16 * CB + col_l));
-                const float wv = fmaf(x.w, g3, fmaf(x.z, g2, fmaf(x.y, g1, x.x * g0)));
-                bv[CB] = (16 * CB + col_l <= p0 + 3 || CB >= nb) ? 0.f : wv;
-                if ((CB & 3) == 3) __builtin_amdgcn_sched_barrier(0);
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int RB = w + 4 * i;
-                if (RB < KB || RB >= nb) continue;   // uniform
+            for (int i = 0; i < R; ++i) {
+                const int RB = WV + W * i;
+                if (RB < KB) continue;
                 const F4 x = *reinterpret_cast<const F4*>(pb + 4 * (16 * RB + col_l));
-                const float wv = fmaf(x.w, g3, fmaf(x.z, g2, fmaf(x.y, g1, x.x * g0)));
-                const float av = (16 * RB + col_l <= p0 + 3) ? 0.f : wv * esel;
+                const float a = fmaf(x.w, mm3, fmaf(x.z, mm2, fmaf(x.y, mm1, x.x * mm0)));
 #pragma unroll
-                for (int c = KB; c < 4 * i + 4; ++c)
-                    if (c <= RB && (c > KB || sc < 3))   // a block's last step leaves its own column finished
-                        acc[gw_off(i) + c] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[c], acc[gw_off(i) + c], 0, 0, 0);
+                for (int CB = KB; CB <= RB; ++CB)
+                    if (CB > KB || sc < 3)   // a block's last step leaves its own column finished
+                        acc[gt_off(W, WV, i) + CB] =
+                            __builtin_amdgcn_mfma_f32_16x16x4f32(a, bv[CB], acc[gt_off(W, WV, i) + CB], 0, 0, 0);
             }
         }
     }
-    // the B rows' 4x4 Schur block: block (nb-1, nb-1), owned by wave (nb-1) % 4
-    float* fin = pan;
-    LDS_BARRIER();
+    // ---- gamma from the B rows' 4x4 Schur block (block (NB - 1, NB - 1), rows / cols 12..15)
+    float* fin = brow;   // the B rows are free after the assembly
+    if constexpr ((NB - 1) % W == WV) {
+        if (col_l >= 12 && rg == 3) {
+            const F4 v = acc[gt_off(W, WV, R - 1) + NB - 1];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int c = 0; c < 4 * i + 4; ++c)
-            if (w + 4 * i == nb - 1 && c == nb - 1 && rg == 3 && col_l >= 12) {
-                const F4 v = acc[gw_off(i) + c];
-#pragma unroll
-                for (int r = 0; r < 4; ++r) fin[4 * r + (col_l - 12)] = v[r];
-            }
+            for (int i = 0; i < 4; ++i) fin[4 * i + (col_l - 12)] = v[i];
+        }
+    }
+    float rn2 = 0.f;
+    if constexpr (WV == 0) {
+        for (int o = lane; o < M; o += 64) rn2 += rt[4 * o + 3] * rt[4 * o + 3];
+        rn2 = wave_sum(rn2);
+    }
     LDS_BARRIER();
     if (tid == 0) {
         const float* a = fin;
@@ -918,10 +909,114 @@ __global__ void __launch_bounds__(256) k_gate_mfma_wg(DevState<float> st, Params
         const float l32 = (a[14] - l30 * l20 * d0 - l31 * l21 * d1) / d2;
         const float d3 = a[15] - l30 * l30 * d0 - l31 * l31 * d1 - l32 * l32 * d2;
         float gam = -d3 + rn2 / s2;
-        if (fail || !(d0 < 0.f) || !(d1 < 0.f) || !(d2 < 0.f) || !(gam == gam)) gam = INFINITY;
+        if (!(dmin > 0.f) || !(d0 < 0.f) || !(d1 < 0.f) || !(d2 < 0.f) || !(gam == gam)) gam = INFINITY;
         fb.gamma[f] = gam;
         fb.accept[f] = (gam < chi2) ? 1 : 0;
     }
+}
+
+template <int NB, int W>
+__global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(gt_waves(NB, W))))
+k_gate_mfma_wt(DevState<float> st, Params<float> prm, FeatBatch<float> fb, const int* __restrict__ flist, int nlist,
+               int Mmax, int capf) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    constexpr int NT = 64 * W;
+    const int tid = threadIdx.x;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int li = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x));
+    if (li >= nlist) return;
+    const int f = __builtin_amdgcn_readfirstlane(flist[li]);
+    if (!fb.valid[f]) {
+        if (tid == 0) { fb.gamma[f] = NAN; fb.accept[f] = 0; }
+        return;
+    }
+    const float chi2 = fb.chi2[f];
+    const int b = __builtin_amdgcn_readfirstlane(fb.feat_filter[f]);
+    const int o0 = __builtin_amdgcn_readfirstlane(fb.obs_off[f]);
+    const int M = __builtin_amdgcn_readfirstlane(fb.obs_off[f + 1]) - o0, M3 = 3 * M;
+    float* ht = reinterpret_cast<float*>(smem_raw);
+    float* rt = ht + 18 * Mmax;
+    float* area = ht + gm_head(Mmax);
+    float* junk = area + gt_area(NB, capf) + 64 * w;
+    float* brow = area + gt_area(NB, capf) + 64 * W;   // [4][16 NB] B rows, then the zero row
+    float* zrow = brow + 64 * NB;
+    int* slot = reinterpret_cast<int*>(zrow + 16 * NB);
+    int* coff = slot + ((Mmax + 3) & ~3);
+    {   // records (Ht transposed, as k_gate_mfma) and cam slots: every load issued before the first wait
+        constexpr int MCAP = (16 * NB - 4) / 3;
+        constexpr int NCH = (12 * MCAP + NT - 1) / NT;
+        static_assert(MCAP <= NT, "one thread per observation");
+        const F2* src = reinterpret_cast<const F2*>(fb.obs_ht + (size_t)o0 * OBS_HTS);
+        F2 cv[NCH];
+#pragma unroll
+        for (int j = 0; j < NCH; ++j) {
+            const int k = tid + NT * j;
+            cv[j] = k < 12 * M ? src[k] : F2{0, 0};
+        }
+        const int sl = tid < M ? fb.obs_cam[o0 + tid] : 0;
+#pragma unroll
+        for (int j = 0; j < NCH; ++j) {
+            const int k = tid + NT * j, o = k / 12, e = 2 * (k - 12 * o);
+            if (k < 12 * M) {
+                if (e < OBS_RT) {
+                    const int x = e / 6, u = e - 6 * x;
+                    float* d = ht + 18 * o + 3 * u + x;
+                    d[0] = cv[j].x;
+                    d[3] = cv[j].y;
+                } else if (e < OBS_RT + 4) {
+                    *reinterpret_cast<F2*>(rt + 4 * o + (e - OBS_RT)) = cv[j];
+                }
+            }
+        }
+        if (tid < M) {
+            slot[tid] = (21 + 6 * sl) * st.Dmax + 21;
+            coff[tid] = 6 * sl;
+        }
+    }
+    __syncthreads();
+    for (int p = tid; p < 16 * NB; p += NT) {   // B rows [H_f~^T ; r~^T] (zero past 3M) and the zero row
+        const bool pv = p < M3;
+        const int o = pv ? p / 3 : 0, cp = p - 3 * o;
+        const float* h = ht + 18 * o + 9 + cp;
+        brow[p] = pv ? -h[0] : 0.f;
+        brow[16 * NB + p] = pv ? -h[3] : 0.f;
+        brow[32 * NB + p] = pv ? -h[6] : 0.f;
+        brow[48 * NB + p] = pv ? rt[4 * o + cp] : 0.f;
+        zrow[p] = 0.f;
+    }
+    // (the first Y pass's barrier orders these before the assembly)
+    const float s2 = prm.sigma2;
+    switch (w) {
+        case 0: gt_body<NB, W, 0>(st, fb, f, b, M, s2, chi2, ht, rt, area, junk, brow, zrow, slot, coff, capf); break;
+        case 1: gt_body<NB, W, 1>(st, fb, f, b, M, s2, chi2, ht, rt, area, junk, brow, zrow, slot, coff, capf); break;
+#define GT_CASE(V) \
+        case V: if constexpr (W > V) gt_body<NB, W, V>(st, fb, f, b, M, s2, chi2, ht, rt, area, junk, brow, zrow, slot, coff, capf); break;
+        GT_CASE(2) GT_CASE(3) GT_CASE(4) GT_CASE(5) GT_CASE(6) GT_CASE(7)
+#undef GT_CASE
+        default: break;
+    }
+    static_assert(W <= 8, "at most eight waves per feature");
+}
+
+template <int NB, int W>
+void launch_wt(hipStream_t s, const DevState<float>& st, const Params<float>& prm, const FeatBatch<float>& fb,
+               const int* list, int cnt, int Mmax) {
+    // LDS: the CU's 160 KB over its workgroups (gt_waves per SIMD); the Y pairs
+    // staged in as many block-row passes as that leaves room for
+    constexpr int wgs = (4 * gt_waves(NB, W) + W - 1) / W;
+    const int budget = (160 * 1024 / wgs - 512) / (int)sizeof(float);
+    const int full = gm_dense(0, Mmax - 1);
+    int cmin = 0;   // one block row per pass at least
+    for (int R = 0; R < NB; ++R) {
+        const int alo = 16 * R / 3, ahi = (16 * R + 15) / 3 < Mmax - 1 ? (16 * R + 15) / 3 : Mmax - 1;
+        cmin = gm_dense(alo, ahi) > cmin ? gm_dense(alo, ahi) : cmin;
+    }
+    int capf = full;
+    while (capf > cmin && gt_floats(Mmax, NB, W, capf) > budget) capf -= 32;
+    if (capf < cmin) capf = cmin;
+    const size_t lds = (size_t)gt_floats(Mmax, NB, W, capf) * sizeof(float);
+    lds_limit((const void*)k_gate_mfma_wt<NB, W>, lds);
+    hipLaunchKernelGGL((k_gate_mfma_wt<NB, W>), dim3(cnt), dim3(64 * W), lds, s, st, prm, fb, list, cnt, Mmax, capf);
 }
 
 template <typename T, int NB, bool MP>
@@ -977,24 +1072,32 @@ void launch_nb(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const
 // (round 5: 31 <= M <= 36 off k_gate_wave, 50x400 fp64 gate 60.4 -> 56.0 ms,
 // profiles/r05/ab_gate_fp64_nb7/); NB = 8 would spill
 bool gate_mfma_fits(int maxM, int ts) { return maxM >= 1 && gm_nb(maxM) <= (ts == 8 ? 7 : 8); }
-bool gate_mfma_wg_fits(int maxM) { return maxM >= 1 && gm_nb(maxM) <= GW_NB; }
+bool gate_mfma_wt_fits(int maxM) { return maxM >= 1 && gm_nb(maxM) <= GT_NBMAX; }
 
 // (round 5 ran the same elimination on fp64 MFMA for 41 <= M <= 62, three
 // block rows per wave: 256 VGPRs + 192 AGPRs, one workgroup per CU, parity
 // green but the 50x400 fp64 gate 55.9 -> 61.5 ms against k_gate_big's register
 // tiles at two workgroups per CU -- profiles/r05/exp_gate_mfma_wg64/)
-void launch_gate_mfma_wg(hipStream_t s, const DevState<float>& st, const Params<float>& prm,
-                         const FeatBatch<float>& fb, const int* list, int cnt, int maxM) {
+
+// fp32 tracks of exactly nb blocks, GT_NBMIN <= nb <= GT_NBMAX: waves per
+// feature by block count (round 6, profiles/r06/wt/: at 80x1000 two waves beat
+// four for nb <= 11 -- 1.07 / 1.62 / 1.55 against 1.16 / 2.21 / 1.91 ms -- but
+// spill at nb = 12; eight waves keep nb = 16 off scratch, 2.34 ms against 7.93,
+// and lose to four below it)
+void launch_gate_mfma_wt(hipStream_t s, const DevState<float>& st, const Params<float>& prm, const FeatBatch<float>& fb,
+                         const int* list, int cnt, int nb, int maxM) {
     if (cnt <= 0) return;
-    // LDS for two workgroups per CU: the Y pairs staged in as many passes as that needs
-    const int fixed = gm_head(maxM) + gw_pan() + ((maxM + 3) & ~3) + 4;
-    int capb = ((78 * 1024) / (int)sizeof(float) - fixed) / 9;
-    const int nbk = maxM * (maxM + 1) / 2;
-    if (capb > nbk) capb = nbk;
-    if (capb < 6 * maxM) capb = 6 * maxM;   // one block row (up to six observation rows) per pass at least
-    const size_t lds = (size_t)gw_floats(maxM, capb) * sizeof(float);
-    lds_limit((const void*)k_gate_mfma_wg, lds);
-    hipLaunchKernelGGL(k_gate_mfma_wg, dim3(cnt), dim3(256), lds, s, st, prm, fb, list, maxM, capb);
+    switch (nb) {
+        case 9: launch_wt<9, 2>(s, st, prm, fb, list, cnt, maxM); break;
+        case 10: launch_wt<10, 2>(s, st, prm, fb, list, cnt, maxM); break;
+        case 11: launch_wt<11, 2>(s, st, prm, fb, list, cnt, maxM); break;
+        case 12: launch_wt<12, 4>(s, st, prm, fb, list, cnt, maxM); break;
+        case 13: launch_wt<13, 4>(s, st, prm, fb, list, cnt, maxM); break;
+        case 14: launch_wt<14, 4>(s, st, prm, fb, list, cnt, maxM); break;
+        case 15: launch_wt<15, 4>(s, st, prm, fb, list, cnt, maxM); break;
+        case 16: launch_wt<16, 8>(s, st, prm, fb, list, cnt, maxM); break;
+        default: break;   // launch_gate sends only GT_NBMIN <= nb <= GT_NBMAX here
+    }
 }
 
 template <typename T>

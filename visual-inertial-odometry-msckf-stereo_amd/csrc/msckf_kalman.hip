@@ -359,13 +359,21 @@ __global__ void __launch_bounds__(64) k_gchol_diag(DevState<T> st, UpdWs<T> ws, 
         const int i = e / nb, j = e - i * nb;
         d[i][j] = j <= i ? A[(size_t)(k + i) * ld + k + j] : 0.0;
     }
-    // stage A: pivots floored as in k_kal_a (pcc_pivot_floor); stage C: at s2 (k_kal_c1)
-    double floor = STAGE == 0 ? 0.0 : ws.s2, lo = -INFINITY;
+    // stage A: pivots floored as in k_kal_a (pcc_pivot_floor); stage C: at s2 down
+    // to -T_FLOOR_NEG x max diag(T), as k_kal_c1 / k_kal_mchol (T itself is still
+    // intact in ws.Tm: k_gchol_c_load factors a copy)
+    double floor = STAGE == 0 ? 0.0 : ws.s2, lo;
     if (STAGE == 0) {
         const T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
         for (int i = lane; i < nelim; i += 64) floor = fmax(floor, (double)P[(size_t)(21 + i) * st.Dmax + 21 + i]);
         floor = wave_max(floor) * KALMAN_PIVOT_FLOOR;
         lo = -PIVOT_FLOOR_NEG * floor;
+    } else {
+        const int ldt = ws.Cmax + 1;
+        const KT* Tm = ws.Tm + (size_t)b * ws.Cmax * ldt;
+        double tmax = 0.0;
+        for (int i = lane; i < nelim; i += 64) tmax = fmax(tmax, (double)Tm[(size_t)i * ldt + i]);
+        lo = -T_FLOOR_NEG * wave_max(tmax);
     }
     __syncthreads();
     bool bad = false;
@@ -1075,10 +1083,13 @@ __device__ __forceinline__ bool mk_factor(const DevState<T>& st, const UpdWs<T>&
                 const double z0 = x[0], z1 = x[1] - l10 * z0, z2 = x[2] - l20 * z0 - l21 * z1;
                 const double z3 = x[3] - l30 * z0 - l31 * z1 - l32 * z2;
                 const int k = r - p0;   // rows of the diagonal block: zeros above the diagonal
-                const double y0 = z0 * rchol_rsq(d0);
-                const double y1 = k >= 1 ? z1 * rchol_rsq(d1) : 0.0;
-                const double y2 = k >= 2 ? z2 * rchol_rsq(d2) : 0.0;
-                const double y3 = k >= 3 ? z3 * rchol_rsq(d3) : 0.0;
+                // the diagonal entries take the (possibly floored) pivot itself: z_k
+                // of row p0 + k is the unfloored Schur value (a floored -1e-12 would
+                // otherwise give L_kk = -1e-12 / sqrt(s2) instead of sqrt(s2))
+                const double y0 = (k == 0 ? d0 : z0) * rchol_rsq(d0);
+                const double y1 = k >= 1 ? (k == 1 ? d1 : z1) * rchol_rsq(d1) : 0.0;
+                const double y2 = k >= 2 ? (k == 2 ? d2 : z2) * rchol_rsq(d2) : 0.0;
+                const double y3 = k >= 3 ? (k == 3 ? d3 : z3) * rchol_rsq(d3) : 0.0;
                 if (STAGE == 0) {
                     KT* dst = r < Cp ? Lc + (size_t)r * Cpw + p0 : Vi + (size_t)(r - Cp) * Cpw + p0;
                     dst[0] = y0; dst[1] = y1; dst[2] = y2; dst[3] = y3;

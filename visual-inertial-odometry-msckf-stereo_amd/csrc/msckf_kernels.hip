@@ -3222,15 +3222,26 @@ void launch_gate(hipStream_t s, const DevState<T>& st, const Params<T>& prm, con
         if (cnt == 0) continue;
         const int maxM = gc.maxM[c];
         const int* list = gc.list + gc.off[c];
+        if constexpr (sizeof(T) == 4) {
+            // fp32 large tracks (40 < M <= 82): by their block-count sub-lists, 8
+            // blocks (M = 41) on the one-wave kernel, 9 .. 16 on k_gate_mfma_wt, a 2- to
+            // 8-wave workgroup per feature (round 6; the one-wave classes of 7 and 8
+            // blocks on k_gate_mfma_wt<7 / 8, 2> measured slower: 50x400 gate 12.05 ->
+            // 12.39 ms, profiles/r06/wt2/)
+            constexpr int wt_lo = 9;
+            if (c == GateClasses::NC - 2 && gate_mfma_wt_fits(maxM)) {
+                for (int j = 0; j + GateClasses::BIG_NB0 <= GateClasses::BIG_NB1; ++j) {
+                    const int n = gc.big_off[j + 1] - gc.big_off[j], nb = j + GateClasses::BIG_NB0;
+                    if (n == 0) continue;
+                    if (nb < wt_lo) launch_gate_mfma<T>(s, st, prm, fb, gc.list + gc.big_off[j], n, gc.big_maxM[j]);
+                    else launch_gate_mfma_wt(s, st, prm, fb, gc.list + gc.big_off[j], n, nb, gc.big_maxM[j]);
+                }
+                continue;
+            }
+        }
         if (c < GateClasses::NC - 2 && gate_mfma_fits(maxM, (int)sizeof(T))) {   // MFMA tiles (msckf_gate_mfma.hip)
             launch_gate_mfma<T>(s, st, prm, fb, list, cnt, maxM);
             continue;
-        }
-        if constexpr (sizeof(T) == 4) {   // fp32 large tracks: MFMA tiles, one workgroup per feature
-            if (c == GateClasses::NC - 2 && gate_mfma_wg_fits(maxM)) {
-                launch_gate_mfma_wg(s, st, prm, fb, list, cnt, maxM);
-                continue;
-            }
         }
         // (round 5: fp64 30 < M <= 40 on k_gate_big instead of k_gate_wave measured
         // slower, gate 60.5 -> 63.4 ms at 50x400, profiles/r05/exp_gate_big_fp64_31_40/)

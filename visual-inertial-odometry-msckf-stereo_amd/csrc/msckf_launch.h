@@ -113,9 +113,11 @@ template <typename T>
 void launch_feature(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&, const SegClasses&);
 // Feature index lists per gating size class (device pointer + host offsets).
 // Gating size classes by observation count M.  Class c < NC-2 runs the
-// one-wave register-tile kernel with TPL[c] 4x4 tiles per lane; class NC-2
-// (M <= 82) the workgroup register-tile kernel k_gate_big; the last class the
-// workgroup LDS kernel (or its global-memory variant).
+// one-wave MFMA kernel (fp32; fp64 up to 7 blocks) or the one-wave register-tile
+// kernel with TPL[c] 4x4 tiles per lane (fp64); class NC-2 (M <= 82) the fp32
+// multi-wave MFMA kernel k_gate_mfma_wt by block count, or the fp64 workgroup
+// register-tile kernel k_gate_big; the last class the workgroup LDS kernel (or
+// its global-memory variant).
 struct GateClasses {
     // one-wave classes by the tiles of the reduced (3M + 4)-square matrix,
     // ceil((gate_nt(M) (gate_nt(M) + 1) / 2) / 64) per lane; then the
@@ -128,6 +130,12 @@ struct GateClasses {
     const int* list = nullptr;
     int off[NC + 1] = {};
     int maxM[NC] = {};
+    // class NC - 2 (40 < M <= 82) ordered by the 16-row block count nb =
+    // ceil((3M + 4) / 16) = BIG_NB0 .. BIG_NB1: features of block count nb at
+    // list[big_off[nb - BIG_NB0] .. big_off[nb - BIG_NB0 + 1])
+    static constexpr int BIG_NB0 = 8, BIG_NB1 = 16;
+    int big_off[BIG_NB1 - BIG_NB0 + 2] = {};
+    int big_maxM[BIG_NB1 - BIG_NB0 + 1] = {};
 };
 template <typename T>
 void launch_gate(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&, const GateClasses&);
@@ -137,11 +145,11 @@ bool gate_mfma_fits(int maxM, int scalar_bytes);
 template <typename T>
 void launch_gate_mfma(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&, const int* list, int cnt,
                       int maxM);
-// fp32 gating of large tracks (40 < M <= 82) on MFMA tiles, one 4-wave
-// workgroup per feature
-bool gate_mfma_wg_fits(int maxM);
-void launch_gate_mfma_wg(hipStream_t, const DevState<float>&, const Params<float>&, const FeatBatch<float>&,
-                         const int* list, int cnt, int maxM);
+// fp32 gating of the tracks of exactly nb 16-row blocks (9 <= nb <= 16, 41 < M <= 84)
+// on a 2- / 4- / 8-wave workgroup per feature (k_gate_mfma_wt)
+bool gate_mfma_wt_fits(int maxM);
+void launch_gate_mfma_wt(hipStream_t, const DevState<float>&, const Params<float>&, const FeatBatch<float>&,
+                         const int* list, int cnt, int nb, int maxM);
 template <typename T>
 void launch_select(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const UpdWs<T>&, int row_cap);
 template <typename T>
