@@ -148,14 +148,18 @@ def pmc_traffic(stage, dtype, workload):
     summary (tools/pmc_summary.py; FETCH_SIZE and WRITE_SIZE from separate
     passes, FETCH_SIZE doubled as MI355X_MICROARCH.md prescribes for gfx950),
     or None if no summary covers them."""
-    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
-    if not os.path.exists(path):
-        return None
-    with open(path) as fh:
-        summ = json.load(fh)
-    if summ.get("dtype") != dtype or summ.get("workload", "N30xF200xB2048") != workload:
-        return None
-    return summ.get("stages", {}).get(stage, {}).get("fetch_x2_bytes_per_step")
+    # the headline workload's summary, or one per (workload, dtype) for the other
+    # configs (tools/profile_round.sh writes profiles/pmc_summary_<workload>_<dtype>.json)
+    for name in ("pmc_summary.json", "pmc_summary_%s_%s.json" % (workload, dtype)):
+        path = os.path.join(ROOT, "profiles", name)
+        if not os.path.exists(path):
+            continue
+        with open(path) as fh:
+            summ = json.load(fh)
+        if summ.get("dtype") != dtype or summ.get("workload", "N30xF200xB2048") != workload:
+            continue
+        return summ.get("stages", {}).get(stage, {}).get("fetch_x2_bytes_per_step")
+    return None
 
 
 # ------------------------------------------------------------ cpu_baseline --

@@ -338,7 +338,7 @@ def test_batched_fp64_vs_oracle(N, F, B, cap):
     size class; 30 in cap 32 and 32 -- the largest register-tile Kalman
     window and the full 12 x 12 tile triangle (32 cams: C = 192);
     20 x 480 -- more features per filter than the fused assembly's LDS holds
-    (> 453): Gram records through k_info_mfma (full A) into the same stage B;
+    (> 453): Gram records through k_info_mfma (lower triangle of A) into the same stage B;
     34 (cap 36) -- the one-workgroup-per-tile-row k_info and the smallest
     global-memory Kalman window; 50 (cap 50: four staged features per k_info
     batch, cap 52: three) -- multi-workgroup assembly, global-memory Kalman stages A / C,

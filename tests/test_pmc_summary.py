@@ -83,3 +83,17 @@ def test_bench_propagation_traffic_matches_its_shape(tmp_path, monkeypatch):
     assert bench.prop_traffic("fp32", 2048, 10, 201) == 123
     assert bench.prop_traffic("fp64", 2048, 10, 201) is None
     assert bench.prop_traffic("fp32", 1024, 10, 201) is None
+
+
+def test_workload_label_from_bench_log(tmp_path):
+    """The summary is labelled with the workload of the passes' own bench line
+    (round-5 verdict: the 50x400 / 80x1000 summaries carried the default label)."""
+    f, w, o, log = tmp_path / "f.csv", tmp_path / "w.csv", tmp_path / "o.json", tmp_path / "bench.log"
+    _csv(f, "FETCH_SIZE", [100.0, 300.0, 1.0])
+    _csv(w, "WRITE_SIZE", [10.0, 30.0, 1.0])
+    log.write_text("noise\n" + json.dumps({"dtype": "f64", "config": {"cam_states": 50, "features": 400,
+                                                                      "filters_per_gpu": 2048}}) + "\n")
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_summary.py"), str(f), str(w),
+                    "--bench-log", str(log), "--steps", "2", "-o", str(o)], check=True, capture_output=True)
+    d = json.load(open(o))
+    assert d["workload"] == "N50xF400xB2048" and d["dtype"] == "fp64"

@@ -73,6 +73,21 @@ def read(path):
     return out, count
 
 
+def workload_of_log(path):
+    """(workload key, dtype) of the bench line in a bench.py log (the last JSON line)."""
+    line = None
+    for ln in open(path):
+        ln = ln.strip()
+        if ln.startswith("{") and '"config"' in ln:
+            line = ln
+    if line is None:
+        return None, None
+    d = json.loads(line)
+    c = d["config"]
+    return ("N%dxF%dxB%d" % (c["cam_states"], c["features"], c["filters_per_gpu"]),
+            "fp64" if d.get("dtype") == "f64" else "fp32")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("fetch")
@@ -82,9 +97,17 @@ def main():
     ap.add_argument("--dtype", default="fp32")
     ap.add_argument("-o", "--out", default="profiles/pmc_summary.json")
     ap.add_argument("--source", default="")
-    ap.add_argument("--workload", default="N30xF200xB2048",
-                    help="bench workload the passes ran (bench.py only uses the traffic for the same one)")
+    ap.add_argument("--workload", default=None,
+                    help="bench workload the passes ran, N<cams>xF<features>xB<filters> (bench.py only uses the "
+                         "traffic for the same one); default: read from --bench-log, else N30xF200xB2048")
+    ap.add_argument("--bench-log", default=None,
+                    help="log of the pass's bench.py run: its JSON line gives the workload (and --dtype)")
     a = ap.parse_args()
+    if a.bench_log:
+        wl, dt = workload_of_log(a.bench_log)
+        a.workload = a.workload or wl
+        a.dtype = dt or a.dtype
+    a.workload = a.workload or "N30xF200xB2048"
     fetch, nf = read(a.fetch)
     write, nw = read(a.write)
     tname = "float" if a.dtype == "fp32" else "double"

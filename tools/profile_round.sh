@@ -14,3 +14,7 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "msckf" -d $
     python3 bench.py --steps 1 --warmup 0 --no-cpu --no-ate --no-prop "$@" > $OUT/fetch/bench.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "msckf" -d $OUT/write -o run --output-format csv -- \
     python3 bench.py --steps 1 --warmup 0 --no-cpu --no-ate --no-prop "$@" > $OUT/write/bench.log 2>&1
+# the per-stage summary, labelled with the workload and dtype of the passes' own bench line
+python3 tools/pmc_summary.py $OUT/fetch/run_counter_collection.csv $OUT/write/run_counter_collection.csv \
+    --bench-log $OUT/fetch/bench.log --source "$TAG: rocprofv3 FETCH_SIZE / WRITE_SIZE passes" \
+    -o $OUT/pmc_summary.json > $OUT/pmc_summary.txt

@@ -109,7 +109,7 @@ struct FeatBatch {
 using KT = double;
 template <typename T>
 struct UpdWs {
-    KT* Hthin;   // [B][Cmax][Cmax+1]   [A | b] = [H^T H | H^T r]; A full (k_info) or its lower triangle (k_info_fused)
+    KT* Hthin;   // [B][Cmax][Cmax+1]   [A | b] = [H^T H | H^T r]; A full (k_info) or its lower triangle (k_info_fused, k_info_mfma)
     KT* dx;      // [B][Dmax + Cmax]
     int* info;   // [B][4]: rows stacked, C (0: no update), compress flag, status
     int Cmax;

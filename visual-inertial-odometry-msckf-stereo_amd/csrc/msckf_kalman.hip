@@ -1162,8 +1162,9 @@ k_kal_mchol(DevState<T> st, UpdWs<T> ws) {
         if (!ok && tid == 0) ws.info[4 * b + 3] = -1;
         return;
     }
+    __shared__ int nfail, failed[64];
+    auto failed_b = [&](int k) { return failed[k]; };
     if (RETRY) {   // the failed filters of this workgroup's share, found in one parallel pass
-        __shared__ int nfail, failed[64];
         if (tid == 0) nfail = 0;
         __syncthreads();
         for (int i = tid; blockIdx.x + (size_t)i * gridDim.x < (size_t)st.B; i += blockDim.x) {
@@ -1193,6 +1194,11 @@ k_kal_mchol(DevState<T> st, UpdWs<T> ws) {
     }
     for (int b = blockIdx.x; b < st.B; b += gridDim.x) {
         if (RETRY && ws.afail[b] == 0) continue;   // uniform
+        if (RETRY) {   // the first 64 of the share were retried above: not again
+            bool done = false;
+            for (int k = 0; k < 64; ++k) done |= failed_b(k) == b;
+            if (done) continue;   // uniform
+        }
         const int C = 6 * st.ncams[b];
         const double floor = pcc_pivot_floor(st.P + (size_t)b * st.Dmax * st.Dmax, st.Dmax, C, red);
         bool ok = false;

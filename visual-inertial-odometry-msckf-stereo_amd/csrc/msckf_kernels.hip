@@ -114,7 +114,12 @@ __device__ __forceinline__ T prop_dot(const T (&x)[21], const T (&y)[N], unsigne
 // Phase boundary of the one-wave kernel.  One wave's LDS operations execute in
 // issue order, so a lane's read issued after another lane's write sees it: only
 // the compiler must not move LDS accesses across the boundary (no hardware wait).
+// This holds only for a 64-thread workgroup that is ONE wave: k_propagate is
+// launched with blockDim 64 (launch_propagate) and built for wave64 only.
 __device__ __forceinline__ void prop_sync() { asm volatile("" ::: "memory"); }
+#if defined(__AMDGCN_WAVEFRONT_SIZE) && __AMDGCN_WAVEFRONT_SIZE != 64
+#error "k_propagate's phase boundaries (prop_sync) assume a 64-thread workgroup is one wave"
+#endif
 
 // Phase timing of k_propagate (probe builds only, `make probe`:
 // -DMSCKF_GATE_PROBE; tools/probes/prop_phases.py reads it): per scalar type,
@@ -160,6 +165,8 @@ __device__ __forceinline__ void xb_rows(T* P, int ld, int j0, int nj, const T* x
     }
 }
 
+// One wave per filter: __launch_bounds__(64) with wave64 (see prop_sync) -- the
+// phase boundaries are compiler barriers only, which is safe inside one wave.
 template <typename T, int PKC>
 __global__ void __launch_bounds__(64) k_propagate(DevState<T> st, Params<T> prm, int nfilt,
                                                   const int* __restrict__ filters,
@@ -2539,11 +2546,9 @@ __global__ void __launch_bounds__(64 * IM_NW) k_info_mfma(DevState<T> st, FeatBa
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int row = 16 * pti[q] + lr + 4 * r, col = 16 * ptj[q] + lc;
-            if (row < C && col < C) {
-                const double v = -acc[q][r];
-                F[(size_t)row * ldf + col] = v;
-                F[(size_t)col * ldf + row] = v;
-            }
+            // lower triangle only (stage B reads nothing else; the block-diagonal
+            // owners below add their terms to the lower elements)
+            if (row < C && col <= row) F[(size_t)row * ldf + col] = -acc[q][r];
         }
     }
     __syncthreads();   // the tiles' stores are visible to the block-diagonal owners

@@ -236,7 +236,10 @@ class ReplicaGroup:
         errs = self._hub_gather(err)
         if not all(oks):
             if comm is not None:
-                comm.close()
+                try:   # this rank came up but another did not: the hub carries on for all of them
+                    comm.close()
+                except RuntimeError as e:   # an aborted teardown is recorded, not raised
+                    errs = errs + ["rank %d teardown: %s" % (self.rank, e)]
             self.transport = "tcp-hub (rccl unavailable: %s)" % next(e for e in errs if e)
             return {"transport": self.transport}
         comm.set_timeout(collective_timeout_s)
@@ -274,17 +277,26 @@ class ReplicaGroup:
         return self._hub_gather(obj)
 
     def close(self):
-        if self._rccl is not None:
-            self._rccl.close()
-            self._rccl = None
-        if self._sock is not None:
-            self._hub_call("close")
-            self._sock.close()
-            self._sock = None
-        if self._hub is not None:
-            self._hub.thread.join(timeout=30)
-        if self._rdzv and os.path.exists(self._rdzv):
-            os.unlink(self._rdzv)
+        # the hub, the socket and the rendezvous file are released even when the
+        # RCCL teardown raises (an aborted ncclCommFinalize, rc -4): a stale
+        # rendezvous file keyed by MASTER_PORT and ppid would be picked up by a
+        # later run
+        try:
+            if self._rccl is not None:
+                comm, self._rccl = self._rccl, None
+                comm.close()
+        finally:
+            try:
+                if self._sock is not None:
+                    self._hub_call("close")
+            finally:
+                if self._sock is not None:
+                    self._sock.close()
+                    self._sock = None
+                if self._hub is not None:
+                    self._hub.thread.join(timeout=30)
+                if self._rdzv and os.path.exists(self._rdzv):
+                    os.unlink(self._rdzv)
 
 
 def _rdzv_path():
