@@ -489,9 +489,10 @@ def test_gate_fp64_gamma_vs_oracle(N, F, B, nmin):
     """fp64 gating against the oracle's gamma (msckf.py:606-614), relative
     1e-9: the one-wave fp64 MFMA kernel (v_mfma_f64_16x16x4_f64, its own
     accumulator row layout) for every class up to 7 blocks (M <= 36, single- and
-    multi-pass Y staging), k_gate_wave for 37 <= M <= 40, k_gate_big
-    (workgroup register tiles) for 41 <= M <= 82 (N = 50: classes up to 50
-    observations, the 50x400 bench shape); decisions identical."""
+    multi-pass Y staging), and k_gate_mfma_wt (fp64 MFMA, four waves up to 10
+    blocks, eight beyond) for 37 <= M <= 82 (N = 50: classes up to 50
+    observations, the 50x400 bench shape; N = 82: up to 16 blocks); decisions
+    identical."""
     problems = [synth.make_update_problem(N, F, seed=700 + b) for b in range(B)]
     ctx, ds, feat_off, acc, gam, pw, valid, rows = _batched(problems, np.float64)
     n = 0

@@ -674,7 +674,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gm_wav
 // (Replaces round 5's k_gate_mfma_wg: runtime block counts, the B operands of
 // all 16 block rows formed every step, a square-root pair decode and per-
 // element index arithmetic in the assembly -- 6.0k VALU per wave at 50x400.)
-constexpr int GT_NBMIN = 9, GT_NBMAX = 16;   // block counts k_gate_mfma_wt is built for (41 < M <= 84)
+constexpr int GT_NBMAX = 16;   // block counts k_gate_mfma_wt is built for: fp32 9.., fp64 8.. (M <= 84)
 __host__ __device__ constexpr int gt_rows(int NB, int W, int WV) { return WV < NB ? (NB - 1 - WV) / W + 1 : 0; }
 __host__ __device__ constexpr int gt_off(int W, int WV, int i) { return i * (WV + 1) + W * i * (i - 1) / 2; }
 __host__ __device__ constexpr int gt_slots(int NB, int W, int WV) { return gt_off(W, WV, gt_rows(NB, W, WV)); }
@@ -684,30 +684,36 @@ __host__ __device__ constexpr int gt_maxslots(int NB, int W) {
     return m;
 }
 // waves per SIMD the largest wave's accumulators leave room for
-__host__ __device__ constexpr int gt_waves(int NB, int W) {
-    return 4 * gt_maxslots(NB, W) + 96 <= 168 ? 3 : (4 * gt_maxslots(NB, W) + 96 <= 256 ? 2 : 1);
+// (ts: bytes of the scalar type = VGPRs per accumulator block / 4 x 4)
+__host__ __device__ constexpr int gt_waves(int NB, int W, int ts = 4) {
+    return ts * gt_maxslots(NB, W) + (ts == 8 ? 112 : 96) <= 168 ? 3
+         : (ts * gt_maxslots(NB, W) + (ts == 8 ? 112 : 96) <= 256 ? 2 : 1);
 }
-// LDS (floats): records | stage / [2][16 NB][4] panel | junk [W][64] | B rows [4][16 NB], zero row [16 NB] | slot, coff
+// LDS (elements of T): records | stage / [2][16 NB][4] panel | junk [W][128] | B rows [4][16 NB], zero row [16 NB] |
+// slot, coff
 __host__ __device__ constexpr int gt_area(int NB, int capf) { return capf + 16 > 128 * NB ? ((capf + 16 + 3) & ~3) : 128 * NB; }
 __host__ __device__ constexpr int gt_floats(int Mmax, int NB, int W, int capf) {
-    return gm_head(Mmax) + gt_area(NB, capf) + 64 * W + 80 * NB + 2 * ((Mmax + 3) & ~3);
+    return gm_head(Mmax) + gt_area(NB, capf) + 128 * W + 80 * NB + 2 * ((Mmax + 3) & ~3);
 }
 
-template <int NB, int W, int WV>
-__device__ __forceinline__ void gt_body(const DevState<float>& st, const FeatBatch<float>& fb, int f, int b, int M,
-                                        float s2, float chi2, float* ht, float* rt, float* area, float* junk,
-                                        float* brow, float* zrow, const int* slot, const int* coff, int capf) {
+template <typename T, int NB, int W, int WV>
+__device__ __forceinline__ void gt_body(const DevState<T>& st, const FeatBatch<T>& fb, int f, int b, int M, T s2,
+                                        T chi2, T* ht, T* rt, T* area, T* junk, T* brow, T* zrow, const int* slot,
+                                        const int* coff, int capf) {
+    using V4 = typename GM<T>::V4;
+    using V2 = typename GM<T>::V2;
+    constexpr int RS = GM<T>::RS, RG = GM<T>::RG;
     constexpr int NT = 64 * W, R = gt_rows(NB, W, WV), NS = gt_slots(NB, W, WV);
     constexpr int nB = 16 * NB - 4;
     const int tid = threadIdx.x, lane = tid & 63, M3 = 3 * M;
-    float* stage = area;
-    float* pan = area;
-    F4 acc[NS > 0 ? NS : 1];
+    T* stage = area;
+    T* pan = area;
+    V4 acc[NS > 0 ? NS : 1];
 
     // ---- Y: pair blocks Ht_a P_ab Ht_b^T into the dense lower stage, in passes of block rows
-    const float* P = st.P + (size_t)b * st.Dmax * st.Dmax;
+    const T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
     const int ldp = st.Dmax;
-    const float* Prow[6];
+    const T* Prow[6];
 #pragma unroll
     for (int u = 0; u < 6; ++u) Prow[u] = P + u * ldp;
     auto npairs = [&](int lo, int hi) { return hi < lo ? 0 : (hi + 1) * (hi + 2) / 2 - lo * (lo + 1) / 2; };
@@ -727,35 +733,59 @@ __device__ __forceinline__ void gt_body(const DevState<float>& st, const FeatBat
             const unsigned pe = pen;
             if (kk + NT < nbp) pen = g_gm_pairs.v[kbase + kk + NT];
             const int a = pe & 0xff, bo = (pe >> 8) & 0xff;
-            const unsigned boff = (unsigned)(slot[a] + coff[bo]) * (unsigned)sizeof(float);
-            float Pl[36];
+            const unsigned boff = (unsigned)(slot[a] + coff[bo]) * (unsigned)sizeof(T);
+            const T* Ha = ht + 18 * a;
+            const T* Hb = ht + 18 * bo;
+            T* d0 = stage + ((int)(pe >> 16) - soff0);
+            T* dst[3] = {d0, d0 + 3 * a + 3, d0 + 6 * a + 7};
+            V2 t[3][3];   // Ha[x] P as three column pairs
 #pragma unroll
-            for (int u = 0; u < 6; ++u)
-                __builtin_memcpy(Pl + 6 * u, reinterpret_cast<const char*>(Prow[u]) + boff, 6 * sizeof(float));
-            const float* Ha = ht + 18 * a;
-            const float* Hb = ht + 18 * bo;
-            float* d0 = stage + ((int)(pe >> 16) - soff0);
-            float* dst[3] = {d0, d0 + 3 * a + 3, d0 + 6 * a + 7};
-            F2 hb01[6];
+            for (int x = 0; x < 3; ++x)
 #pragma unroll
-            for (int u = 0; u < 6; ++u) hb01[u] = F2{Hb[3 * u], Hb[3 * u + 1]};
+                for (int c = 0; c < 3; ++c) t[x][c] = V2{0, 0};
+            if constexpr (sizeof(T) == 8) {
+                // fp64: P streamed a row at a time (as the one-wave kernel's multi-pass Y phase)
+#pragma unroll
+                for (int u = 0; u < 6; ++u) {
+                    T pr[6];
+                    __builtin_memcpy(pr, reinterpret_cast<const char*>(Prow[u]) + boff, 6 * sizeof(T));
+#pragma unroll
+                    for (int x = 0; x < 3; ++x) {
+                        const T h = Ha[3 * u + x];
+#pragma unroll
+                        for (int c = 0; c < 3; ++c)
+                            t[x][c] = __builtin_elementwise_fma(V2{h, h}, V2{pr[2 * c], pr[2 * c + 1]}, t[x][c]);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);   // one P row in flight
+                }
+            } else {
+                T Pl[36];
+#pragma unroll
+                for (int u = 0; u < 6; ++u)
+                    __builtin_memcpy(Pl + 6 * u, reinterpret_cast<const char*>(Prow[u]) + boff, 6 * sizeof(T));
+#pragma unroll
+                for (int x = 0; x < 3; ++x)
+#pragma unroll
+                    for (int u = 0; u < 6; ++u) {
+                        const T h = Ha[3 * u + x];
+#pragma unroll
+                        for (int c = 0; c < 3; ++c)
+                            t[x][c] = __builtin_elementwise_fma(V2{h, h}, V2{Pl[6 * u + 2 * c], Pl[6 * u + 2 * c + 1]},
+                                                                t[x][c]);
+                    }
+            }
+            V2 hb01[6];
+#pragma unroll
+            for (int u = 0; u < 6; ++u) hb01[u] = V2{Hb[3 * u], Hb[3 * u + 1]};
 #pragma unroll
             for (int x = 0; x < 3; ++x) {
-                F2 t2[3] = {F2{0, 0}, F2{0, 0}, F2{0, 0}};
+                const T t1[6] = {t[x][0].x, t[x][0].y, t[x][1].x, t[x][1].y, t[x][2].x, t[x][2].y};
+                V2 y01 = {0, 0};
+                T y2 = 0;
 #pragma unroll
                 for (int u = 0; u < 6; ++u) {
-                    const float h = Ha[3 * u + x];
-#pragma unroll
-                    for (int c = 0; c < 3; ++c)
-                        t2[c] = __builtin_elementwise_fma(F2{h, h}, F2{Pl[6 * u + 2 * c], Pl[6 * u + 2 * c + 1]}, t2[c]);
-                }
-                const float t1[6] = {t2[0].x, t2[0].y, t2[1].x, t2[1].y, t2[2].x, t2[2].y};
-                F2 y01 = {0, 0};
-                float y2 = 0;
-#pragma unroll
-                for (int u = 0; u < 6; ++u) {
-                    y01 = __builtin_elementwise_fma(F2{t1[u], t1[u]}, hb01[u], y01);
-                    y2 = fmaf(t1[u], Hb[3 * u + 2], y2);
+                    y01 = __builtin_elementwise_fma(V2{t1[u], t1[u]}, hb01[u], y01);
+                    y2 = gfma(t1[u], Hb[3 * u + 2], y2);
                 }
                 dst[x][0] = y01.x;
                 dst[x][1] = y01.y;
@@ -771,7 +801,7 @@ __device__ __forceinline__ void gt_body(const DevState<float>& st, const FeatBat
             bool up[4], dg[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                r[i] = 4 * rg + i;
+                r[i] = RG * rg + RS * i;
                 up[i] = r[i] < col_l;
                 dg[i] = r[i] == col_l;
             }
@@ -779,11 +809,11 @@ __device__ __forceinline__ void gt_body(const DevState<float>& st, const FeatBat
             for (int i = 0; i < R; ++i) {
                 const int RB = WV + W * i;
                 if (RB < R0 || RB >= R1) continue;   // uniform
-                const float* src[4];
+                const T* src[4];
 #pragma unroll
                 for (int ii = 0; ii < 4; ++ii) {
                     const int q = 16 * RB + r[ii];
-                    const float* ptr = stage + (gm_rowoff(q) - soff0) + col_l;
+                    const T* ptr = stage + (gm_rowoff(q) - soff0) + col_l;
                     if (RB >= NB - 2) {
                         ptr = q < M3 ? ptr : zrow + col_l;
                         if (RB == NB - 1) ptr = q >= nB ? brow + (q - nB) * (16 * NB) + col_l : ptr;
@@ -792,15 +822,15 @@ __device__ __forceinline__ void gt_body(const DevState<float>& st, const FeatBat
                 }
 #pragma unroll
                 for (int c = 0; c <= RB; ++c) {
-                    F4 v;
+                    V4 v;
 #pragma unroll
                     for (int ii = 0; ii < 4; ++ii) v[ii] = src[ii][16 * c];
                     if (c == RB) {
 #pragma unroll
                         for (int ii = 0; ii < 4; ++ii) {
                             const int q = 16 * RB + r[ii];
-                            const float dv = RB < NB - 2 ? s2 : (q < M3 ? s2 : (q < nB ? 1.f : 0.f));
-                            v[ii] = up[ii] ? 0.f : (dg[ii] ? v[ii] + dv : v[ii]);
+                            const T dv = RB < NB - 2 ? s2 : (q < M3 ? s2 : (q < nB ? T(1) : T(0)));
+                            v[ii] = up[ii] ? T(0) : (dg[ii] ? v[ii] + dv : v[ii]);
                         }
                     }
                     acc[gt_off(W, WV, i) + c] = v;
@@ -815,110 +845,113 @@ __device__ __forceinline__ void gt_body(const DevState<float>& st, const FeatBat
     // ---- blocked LDL^T, 4 pivots per step, MFMA trailing updates
     const int col_l = lane & 15, rg = lane >> 4, csel = rg;
     const bool owner[4] = {(col_l >> 2) == 0, (col_l >> 2) == 1, (col_l >> 2) == 2, (col_l >> 2) == 3};
-    float* jk = junk + lane;
-    float dmin = 1.f;
-    float onehot[4];
+    T* jk = junk + lane;
+    T dmin = T(1);
+    T onehot[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) onehot[k] = csel == k ? 1.f : 0.f;
+    for (int k = 0; k < 4; ++k) onehot[k] = csel == k ? T(1) : T(0);
 #pragma unroll
     for (int KB = 0; KB < NB; ++KB) {
 #pragma unroll
         for (int sc = 0; sc < 4; ++sc) {
             if (KB == NB - 1 && sc == 3) break;   // the last four rows are the B rows
             const int p0 = 16 * KB + 4 * sc;
-            float* pb = pan + ((4 * KB + sc) & 1) * (64 * NB);
+            T* pb = pan + ((4 * KB + sc) & 1) * (64 * NB);
             // 1. the owners of columns p0 .. p0 + 3 dump this wave's blocks (RB, KB)
 #pragma unroll
             for (int i = 0; i < R; ++i) {
                 const int RB = WV + W * i;
                 if (RB < KB) continue;
-                const F4 v = acc[gt_off(W, WV, i) + KB];
-                float* dd = owner[sc] ? pb + 4 * (16 * RB + 4 * rg) + (col_l & 3) : jk;
-                dd[0] = v[0]; dd[4] = v[1]; dd[8] = v[2]; dd[12] = v[3];
+                const V4 v = acc[gt_off(W, WV, i) + KB];
+                T* dd = owner[sc] ? pb + 4 * (16 * RB + RG * rg) + (col_l & 3) : jk;
+                dd[0] = v[0]; dd[4 * RS] = v[1]; dd[8 * RS] = v[2]; dd[12 * RS] = v[3];
             }
             LDS_BARRIER();
             // 2. every wave factors A_d = L D L^T
-            const F4 r0 = *reinterpret_cast<const F4*>(pb + 4 * p0);
-            const F4 r1 = *reinterpret_cast<const F4*>(pb + 4 * p0 + 4);
-            const F4 r2 = *reinterpret_cast<const F4*>(pb + 4 * p0 + 8);
-            const F4 r3 = *reinterpret_cast<const F4*>(pb + 4 * p0 + 12);
-            float bv[NB];
+            const V4 r0 = *reinterpret_cast<const V4*>(pb + 4 * p0);
+            const V4 r1 = *reinterpret_cast<const V4*>(pb + 4 * p0 + 4);
+            const V4 r2 = *reinterpret_cast<const V4*>(pb + 4 * p0 + 8);
+            const V4 r3 = *reinterpret_cast<const V4*>(pb + 4 * p0 + 12);
+            T bv[NB];
 #pragma unroll
             for (int CB = KB; CB < NB; ++CB) bv[CB] = pb[4 * (16 * CB + col_l) + csel];
-            const float d0 = r0.x, e0 = pivot_rcp(d0);
-            const float l10 = r1.x * e0, l20 = r2.x * e0, l30 = r3.x * e0;
-            const float d1 = r1.y - l10 * r1.x, e1 = pivot_rcp(d1);
-            const float m21 = r2.y - l20 * r1.x, m31 = r3.y - l30 * r1.x;
-            const float l21 = m21 * e1, l31 = m31 * e1;
-            const float d2 = r2.z - l20 * r2.x - l21 * m21, e2 = pivot_rcp(d2);
-            const float m32 = r3.z - l30 * r2.x - l31 * m21;
-            const float l32 = m32 * e2;
-            const float d3 = r3.w - l30 * r3.x - l31 * m31 - l32 * m32;
-            dmin = fminf(dmin, fminf(fminf(d0, d1), fminf(d2, d3)));
+            const T d0 = r0.x, e0 = pivot_rcp(d0);
+            const T l10 = r1.x * e0, l20 = r2.x * e0, l30 = r3.x * e0;
+            const T d1 = r1.y - l10 * r1.x, e1 = pivot_rcp(d1);
+            const T m21 = r2.y - l20 * r1.x, m31 = r3.y - l30 * r1.x;
+            const T l21 = m21 * e1, l31 = m31 * e1;
+            const T d2 = r2.z - l20 * r2.x - l21 * m21, e2 = pivot_rcp(d2);
+            const T m32 = r3.z - l30 * r2.x - l31 * m21;
+            const T l32 = m32 * e2;
+            const T d3 = r3.w - l30 * r3.x - l31 * m31 - l32 * m32;
+            dmin = fmin(dmin, fmin(fmin(d0, d1), fmin(d2, d3)));
             // formed here: a wave with no block row left would otherwise sink the
             // pivots of every later step to the end, their panel rows live till then
             asm volatile("" : "+v"(dmin));
-            const float e3 = pivot_rcp(d3);
-            const float h0 = onehot[0];
-            const float h1 = fmaf(-l10, h0, onehot[1]);
-            const float h2 = fmaf(-l21, h1, fmaf(-l20, h0, onehot[2]));
-            const float h3 = fmaf(-l32, h2, fmaf(-l31, h1, fmaf(-l30, h0, onehot[3])));
-            const float u0 = h0 * e0, u1 = h1 * e1, u2 = h2 * e2, u3 = h3 * e3;
-            const float m2 = fmaf(-l32, u3, u2);
-            const float m1 = fmaf(-l31, u3, fmaf(-l21, m2, u1));
-            const float m0 = fmaf(-l30, u3, fmaf(-l20, m2, fmaf(-l10, m1, u0)));
-            const float mm3 = -u3, mm2 = -m2, mm1 = -m1, mm0 = -m0;
+            const T e3 = pivot_rcp(d3);
+            const T h0 = onehot[0];
+            const T h1 = gfma(-l10, h0, onehot[1]);
+            const T h2 = gfma(-l21, h1, gfma(-l20, h0, onehot[2]));
+            const T h3 = gfma(-l32, h2, gfma(-l31, h1, gfma(-l30, h0, onehot[3])));
+            const T u0 = h0 * e0, u1 = h1 * e1, u2 = h2 * e2, u3 = h3 * e3;
+            const T m2 = gfma(-l32, u3, u2);
+            const T m1 = gfma(-l31, u3, gfma(-l21, m2, u1));
+            const T m0 = gfma(-l30, u3, gfma(-l20, m2, gfma(-l10, m1, u0)));
+            const T mm3 = -u3, mm2 = -m2, mm1 = -m1, mm0 = -m0;
             // 3. this wave's block rows at or below the panel: C -= X A_d^-1 X^T
 #pragma unroll
             for (int i = 0; i < R; ++i) {
                 const int RB = WV + W * i;
                 if (RB < KB) continue;
-                const F4 x = *reinterpret_cast<const F4*>(pb + 4 * (16 * RB + col_l));
-                const float a = fmaf(x.w, mm3, fmaf(x.z, mm2, fmaf(x.y, mm1, x.x * mm0)));
+                const V4 x = *reinterpret_cast<const V4*>(pb + 4 * (16 * RB + col_l));
+                const T a = gfma(x.w, mm3, gfma(x.z, mm2, gfma(x.y, mm1, x.x * mm0)));
 #pragma unroll
                 for (int CB = KB; CB <= RB; ++CB)
                     if (CB > KB || sc < 3)   // a block's last step leaves its own column finished
-                        acc[gt_off(W, WV, i) + CB] =
-                            __builtin_amdgcn_mfma_f32_16x16x4f32(a, bv[CB], acc[gt_off(W, WV, i) + CB], 0, 0, 0);
+                        acc[gt_off(W, WV, i) + CB] = GM<T>::mfma(a, bv[CB], acc[gt_off(W, WV, i) + CB]);
             }
         }
     }
     // ---- gamma from the B rows' 4x4 Schur block (block (NB - 1, NB - 1), rows / cols 12..15)
-    float* fin = brow;   // the B rows are free after the assembly
+    T* fin = brow;   // the B rows are free after the assembly
     if constexpr ((NB - 1) % W == WV) {
-        if (col_l >= 12 && rg == 3) {
-            const F4 v = acc[gt_off(W, WV, R - 1) + NB - 1];
+        if (col_l >= 12) {
+            const V4 v = acc[gt_off(W, WV, R - 1) + NB - 1];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) fin[4 * i + (col_l - 12)] = v[i];
+            for (int i = 0; i < 4; ++i) {
+                const int row = RG * rg + RS * i;   // rows 12..15 of the block: the B rows
+                if (row >= 12) fin[4 * (row - 12) + (col_l - 12)] = v[i];
+            }
         }
     }
-    float rn2 = 0.f;
+    T rn2 = T(0);
     if constexpr (WV == 0) {
         for (int o = lane; o < M; o += 64) rn2 += rt[4 * o + 3] * rt[4 * o + 3];
         rn2 = wave_sum(rn2);
     }
     LDS_BARRIER();
     if (tid == 0) {
-        const float* a = fin;
-        const float d0 = a[0];
-        const float l10 = a[4] / d0, l20 = a[8] / d0, l30 = a[12] / d0;
-        const float d1 = a[5] - l10 * l10 * d0;
-        const float l21 = (a[9] - l20 * l10 * d0) / d1;
-        const float l31 = (a[13] - l30 * l10 * d0) / d1;
-        const float d2 = a[10] - l20 * l20 * d0 - l21 * l21 * d1;
-        const float l32 = (a[14] - l30 * l20 * d0 - l31 * l21 * d1) / d2;
-        const float d3 = a[15] - l30 * l30 * d0 - l31 * l31 * d1 - l32 * l32 * d2;
-        float gam = -d3 + rn2 / s2;
-        if (!(dmin > 0.f) || !(d0 < 0.f) || !(d1 < 0.f) || !(d2 < 0.f) || !(gam == gam)) gam = INFINITY;
+        const T* a = fin;
+        const T d0 = a[0];
+        const T l10 = a[4] / d0, l20 = a[8] / d0, l30 = a[12] / d0;
+        const T d1 = a[5] - l10 * l10 * d0;
+        const T l21 = (a[9] - l20 * l10 * d0) / d1;
+        const T l31 = (a[13] - l30 * l10 * d0) / d1;
+        const T d2 = a[10] - l20 * l20 * d0 - l21 * l21 * d1;
+        const T l32 = (a[14] - l30 * l20 * d0 - l31 * l21 * d1) / d2;
+        const T d3 = a[15] - l30 * l30 * d0 - l31 * l31 * d1 - l32 * l32 * d2;
+        T gam = -d3 + rn2 / s2;
+        if (!(dmin > T(0)) || !(d0 < T(0)) || !(d1 < T(0)) || !(d2 < T(0)) || !(gam == gam)) gam = T(INFINITY);
         fb.gamma[f] = gam;
         fb.accept[f] = (gam < chi2) ? 1 : 0;
     }
 }
 
-template <int NB, int W>
-__global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(gt_waves(NB, W))))
-k_gate_mfma_wt(DevState<float> st, Params<float> prm, FeatBatch<float> fb, const int* __restrict__ flist, int nlist,
-               int Mmax, int capf) {
+template <typename T, int NB, int W>
+__global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(gt_waves(NB, W, sizeof(T)))))
+k_gate_mfma_wt(DevState<T> st, Params<T> prm, FeatBatch<T> fb, const int* __restrict__ flist, int nlist, int Mmax,
+               int capf) {
+    using V2 = typename GM<T>::V2;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     constexpr int NT = 64 * W;
     const int tid = threadIdx.x;
@@ -930,28 +963,28 @@ k_gate_mfma_wt(DevState<float> st, Params<float> prm, FeatBatch<float> fb, const
         if (tid == 0) { fb.gamma[f] = NAN; fb.accept[f] = 0; }
         return;
     }
-    const float chi2 = fb.chi2[f];
+    const T chi2 = fb.chi2[f];
     const int b = __builtin_amdgcn_readfirstlane(fb.feat_filter[f]);
     const int o0 = __builtin_amdgcn_readfirstlane(fb.obs_off[f]);
     const int M = __builtin_amdgcn_readfirstlane(fb.obs_off[f + 1]) - o0, M3 = 3 * M;
-    float* ht = reinterpret_cast<float*>(smem_raw);
-    float* rt = ht + 18 * Mmax;
-    float* area = ht + gm_head(Mmax);
-    float* junk = area + gt_area(NB, capf) + 64 * w;
-    float* brow = area + gt_area(NB, capf) + 64 * W;   // [4][16 NB] B rows, then the zero row
-    float* zrow = brow + 64 * NB;
+    T* ht = reinterpret_cast<T*>(smem_raw);
+    T* rt = ht + 18 * Mmax;
+    T* area = ht + gm_head(Mmax);
+    T* junk = area + gt_area(NB, capf) + 128 * w;
+    T* brow = area + gt_area(NB, capf) + 128 * W;   // [4][16 NB] B rows, then the zero row
+    T* zrow = brow + 64 * NB;
     int* slot = reinterpret_cast<int*>(zrow + 16 * NB);
     int* coff = slot + ((Mmax + 3) & ~3);
     {   // records (Ht transposed, as k_gate_mfma) and cam slots: every load issued before the first wait
         constexpr int MCAP = (16 * NB - 4) / 3;
         constexpr int NCH = (12 * MCAP + NT - 1) / NT;
         static_assert(MCAP <= NT, "one thread per observation");
-        const F2* src = reinterpret_cast<const F2*>(fb.obs_ht + (size_t)o0 * OBS_HTS);
-        F2 cv[NCH];
+        const V2* src = reinterpret_cast<const V2*>(fb.obs_ht + (size_t)o0 * OBS_HTS);
+        V2 cv[NCH];
 #pragma unroll
         for (int j = 0; j < NCH; ++j) {
             const int k = tid + NT * j;
-            cv[j] = k < 12 * M ? src[k] : F2{0, 0};
+            cv[j] = k < 12 * M ? src[k] : V2{0, 0};
         }
         const int sl = tid < M ? fb.obs_cam[o0 + tid] : 0;
 #pragma unroll
@@ -960,11 +993,11 @@ k_gate_mfma_wt(DevState<float> st, Params<float> prm, FeatBatch<float> fb, const
             if (k < 12 * M) {
                 if (e < OBS_RT) {
                     const int x = e / 6, u = e - 6 * x;
-                    float* d = ht + 18 * o + 3 * u + x;
+                    T* d = ht + 18 * o + 3 * u + x;
                     d[0] = cv[j].x;
                     d[3] = cv[j].y;
                 } else if (e < OBS_RT + 4) {
-                    *reinterpret_cast<F2*>(rt + 4 * o + (e - OBS_RT)) = cv[j];
+                    *reinterpret_cast<V2*>(rt + 4 * o + (e - OBS_RT)) = cv[j];
                 }
             }
         }
@@ -977,20 +1010,20 @@ k_gate_mfma_wt(DevState<float> st, Params<float> prm, FeatBatch<float> fb, const
     for (int p = tid; p < 16 * NB; p += NT) {   // B rows [H_f~^T ; r~^T] (zero past 3M) and the zero row
         const bool pv = p < M3;
         const int o = pv ? p / 3 : 0, cp = p - 3 * o;
-        const float* h = ht + 18 * o + 9 + cp;
-        brow[p] = pv ? -h[0] : 0.f;
-        brow[16 * NB + p] = pv ? -h[3] : 0.f;
-        brow[32 * NB + p] = pv ? -h[6] : 0.f;
-        brow[48 * NB + p] = pv ? rt[4 * o + cp] : 0.f;
-        zrow[p] = 0.f;
+        const T* h = ht + 18 * o + 9 + cp;
+        brow[p] = pv ? -h[0] : T(0);
+        brow[16 * NB + p] = pv ? -h[3] : T(0);
+        brow[32 * NB + p] = pv ? -h[6] : T(0);
+        brow[48 * NB + p] = pv ? rt[4 * o + cp] : T(0);
+        zrow[p] = T(0);
     }
     // (the first Y pass's barrier orders these before the assembly)
-    const float s2 = prm.sigma2;
+    const T s2 = prm.sigma2;
     switch (w) {
-        case 0: gt_body<NB, W, 0>(st, fb, f, b, M, s2, chi2, ht, rt, area, junk, brow, zrow, slot, coff, capf); break;
-        case 1: gt_body<NB, W, 1>(st, fb, f, b, M, s2, chi2, ht, rt, area, junk, brow, zrow, slot, coff, capf); break;
+        case 0: gt_body<T, NB, W, 0>(st, fb, f, b, M, s2, chi2, ht, rt, area, junk, brow, zrow, slot, coff, capf); break;
+        case 1: gt_body<T, NB, W, 1>(st, fb, f, b, M, s2, chi2, ht, rt, area, junk, brow, zrow, slot, coff, capf); break;
 #define GT_CASE(V) \
-        case V: if constexpr (W > V) gt_body<NB, W, V>(st, fb, f, b, M, s2, chi2, ht, rt, area, junk, brow, zrow, slot, coff, capf); break;
+        case V: if constexpr (W > V) gt_body<T, NB, W, V>(st, fb, f, b, M, s2, chi2, ht, rt, area, junk, brow, zrow, slot, coff, capf); break;
         GT_CASE(2) GT_CASE(3) GT_CASE(4) GT_CASE(5) GT_CASE(6) GT_CASE(7)
 #undef GT_CASE
         default: break;
@@ -998,13 +1031,13 @@ k_gate_mfma_wt(DevState<float> st, Params<float> prm, FeatBatch<float> fb, const
     static_assert(W <= 8, "at most eight waves per feature");
 }
 
-template <int NB, int W>
-void launch_wt(hipStream_t s, const DevState<float>& st, const Params<float>& prm, const FeatBatch<float>& fb,
-               const int* list, int cnt, int Mmax) {
+template <typename T, int NB, int W>
+void launch_wt(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const FeatBatch<T>& fb, const int* list,
+               int cnt, int Mmax) {
     // LDS: the CU's 160 KB over its workgroups (gt_waves per SIMD); the Y pairs
     // staged in as many block-row passes as that leaves room for
-    constexpr int wgs = (4 * gt_waves(NB, W) + W - 1) / W;
-    const int budget = (160 * 1024 / wgs - 512) / (int)sizeof(float);
+    constexpr int wgs = (4 * gt_waves(NB, W, sizeof(T)) + W - 1) / W;
+    const int budget = (160 * 1024 / wgs - 512) / (int)sizeof(T);
     const int full = gm_dense(0, Mmax - 1);
     int cmin = 0;   // one block row per pass at least
     for (int R = 0; R < NB; ++R) {
@@ -1014,9 +1047,9 @@ void launch_wt(hipStream_t s, const DevState<float>& st, const Params<float>& pr
     int capf = full;
     while (capf > cmin && gt_floats(Mmax, NB, W, capf) > budget) capf -= 32;
     if (capf < cmin) capf = cmin;
-    const size_t lds = (size_t)gt_floats(Mmax, NB, W, capf) * sizeof(float);
-    lds_limit((const void*)k_gate_mfma_wt<NB, W>, lds);
-    hipLaunchKernelGGL((k_gate_mfma_wt<NB, W>), dim3(cnt), dim3(64 * W), lds, s, st, prm, fb, list, cnt, Mmax, capf);
+    const size_t lds = (size_t)gt_floats(Mmax, NB, W, capf) * sizeof(T);
+    lds_limit((const void*)k_gate_mfma_wt<T, NB, W>, lds);
+    hipLaunchKernelGGL((k_gate_mfma_wt<T, NB, W>), dim3(cnt), dim3(64 * W), lds, s, st, prm, fb, list, cnt, Mmax, capf);
 }
 
 template <typename T, int NB, bool MP>
@@ -1079,26 +1112,49 @@ bool gate_mfma_wt_fits(int maxM) { return maxM >= 1 && gm_nb(maxM) <= GT_NBMAX; 
 // green but the 50x400 fp64 gate 55.9 -> 61.5 ms against k_gate_big's register
 // tiles at two workgroups per CU -- profiles/r05/exp_gate_mfma_wg64/)
 
-// fp32 tracks of exactly nb blocks, GT_NBMIN <= nb <= GT_NBMAX: waves per
+// tracks of exactly nb blocks (fp32 9 <= nb <= 16, fp64 8 <= nb <= 16): waves per
 // feature by block count (round 6, profiles/r06/wt/: at 80x1000 two waves beat
 // four for nb <= 11 -- 1.07 / 1.62 / 1.55 against 1.16 / 2.21 / 1.91 ms -- but
 // spill at nb = 12; eight waves keep nb = 16 off scratch, 2.34 ms against 7.93,
 // and lose to four below it)
-void launch_gate_mfma_wt(hipStream_t s, const DevState<float>& st, const Params<float>& prm, const FeatBatch<float>& fb,
+template <typename T>
+void launch_gate_mfma_wt(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const FeatBatch<T>& fb,
                          const int* list, int cnt, int nb, int maxM) {
     if (cnt <= 0) return;
-    switch (nb) {
-        case 9: launch_wt<9, 2>(s, st, prm, fb, list, cnt, maxM); break;
-        case 10: launch_wt<10, 2>(s, st, prm, fb, list, cnt, maxM); break;
-        case 11: launch_wt<11, 2>(s, st, prm, fb, list, cnt, maxM); break;
-        case 12: launch_wt<12, 4>(s, st, prm, fb, list, cnt, maxM); break;
-        case 13: launch_wt<13, 4>(s, st, prm, fb, list, cnt, maxM); break;
-        case 14: launch_wt<14, 4>(s, st, prm, fb, list, cnt, maxM); break;
-        case 15: launch_wt<15, 4>(s, st, prm, fb, list, cnt, maxM); break;
-        case 16: launch_wt<16, 8>(s, st, prm, fb, list, cnt, maxM); break;
-        default: break;   // launch_gate sends only GT_NBMIN <= nb <= GT_NBMAX here
+    if constexpr (sizeof(T) == 4) {
+        switch (nb) {
+            case 9: launch_wt<T, 9, 2>(s, st, prm, fb, list, cnt, maxM); break;
+            case 10: launch_wt<T, 10, 2>(s, st, prm, fb, list, cnt, maxM); break;
+            case 11: launch_wt<T, 11, 2>(s, st, prm, fb, list, cnt, maxM); break;
+            case 12: launch_wt<T, 12, 4>(s, st, prm, fb, list, cnt, maxM); break;
+            case 13: launch_wt<T, 13, 4>(s, st, prm, fb, list, cnt, maxM); break;
+            case 14: launch_wt<T, 14, 4>(s, st, prm, fb, list, cnt, maxM); break;
+            case 15: launch_wt<T, 15, 4>(s, st, prm, fb, list, cnt, maxM); break;
+            case 16: launch_wt<T, 16, 8>(s, st, prm, fb, list, cnt, maxM); break;
+            default: break;   // launch_gate sends only 9 <= nb <= GT_NBMAX here
+        }
+    } else {
+        // fp64 (8 VGPRs per accumulator block): four waves up to 10 blocks, eight
+        // beyond (50x400 fp64 gate 42.8 ms with eight waves for every count, 32.2
+        // with four up to 10 blocks; profiles/r06/wt64/)
+        switch (nb) {
+            case 8: launch_wt<T, 8, 4>(s, st, prm, fb, list, cnt, maxM); break;
+            case 9: launch_wt<T, 9, 4>(s, st, prm, fb, list, cnt, maxM); break;
+            case 10: launch_wt<T, 10, 4>(s, st, prm, fb, list, cnt, maxM); break;
+            case 11: launch_wt<T, 11, 8>(s, st, prm, fb, list, cnt, maxM); break;
+            case 12: launch_wt<T, 12, 8>(s, st, prm, fb, list, cnt, maxM); break;
+            case 13: launch_wt<T, 13, 8>(s, st, prm, fb, list, cnt, maxM); break;
+            case 14: launch_wt<T, 14, 8>(s, st, prm, fb, list, cnt, maxM); break;
+            case 15: launch_wt<T, 15, 8>(s, st, prm, fb, list, cnt, maxM); break;
+            case 16: launch_wt<T, 16, 8>(s, st, prm, fb, list, cnt, maxM); break;
+            default: break;   // launch_gate sends only 8 <= nb <= GT_NBMAX here
+        }
     }
 }
+template void launch_gate_mfma_wt<float>(hipStream_t, const DevState<float>&, const Params<float>&,
+                                         const FeatBatch<float>&, const int*, int, int, int);
+template void launch_gate_mfma_wt<double>(hipStream_t, const DevState<double>&, const Params<double>&,
+                                          const FeatBatch<double>&, const int*, int, int, int);
 
 template <typename T>
 void launch_gate_mfma(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const FeatBatch<T>& fb,

@@ -1566,8 +1566,7 @@ __global__ void __launch_bounds__(256) k_gate_lds(DevState<T> st, Params<T> prm,
     }
 }
 
-// One-wavefront gating with the matrix in registers (production path for
-// M <= 40).  With Y = Hx P Hx^T + s2 I (4M x 4M, PD) and N an orthonormal basis
+// Gating mathematics (M <= 82).  With Y = Hx P Hx^T + s2 I (4M x 4M, PD) and N an orthonormal basis
 // of the left nullspace of H_f, the reference's S = N^T Y N (msckf.py:607-609
 // on H0 = N^T Hx) satisfies the oblique-projection identity
 //   N S^-1 N^T = Y^-1 - Y^-1 H_f (H_f^T Y^-1 H_f)^-1 H_f^T Y^-1,
@@ -1583,504 +1582,11 @@ __global__ void __launch_bounds__(256) k_gate_lds(DevState<T> st, Params<T> prm,
 // s2).  gamma is invariant under these orthogonal row maps (quirk Q4), so
 //   gamma = gamma(saddle point of the 3M range rows) + sum_i r_n,i^2 / s2,
 // a (3M + 4)-square elimination instead of (4M + 4): ~(3/4)^3 of the flops.
-// Layout: the 3M range rows padded to n3 = 4 ceil(3M/4) (padding rows are
-// unit pivots) plus the B row [H_f~^T ; r~^T], as 4x4 tiles (lower triangle,
-// column-major tile order; tile t belongs to lane t % 64, slot t / 64).
-// Y tiles: the wave forms the 3x3 observation-pair blocks
-// Ht_a P_{s_a s_b} Ht_b^T (a >= b) into LDS (in passes over observation
-// columns when the LDS budget is smaller), then every lane assembles its
-// 4x4 tiles of the compact row space from there.
-// Blocked LDL^T, one tile column per step: the diagonal tile's owner factors
-// it, the panel tiles' owners publish W = A L_d^-T by row through LDS, and
-// every tile right of the panel takes the rank-4 update from registers; slots
-// whose tiles all lie in finished columns are skipped.  The last tile's owner
-// finishes with the three negative pivots.  No workgroup barriers:
-// up to 4 independent features (waves) per workgroup, as many as the LDS allows.
-// Panel buffers hold one 4x4 block per tile row, padded to GB floats (80 B) /
-// doubles (144 B) so that consecutive lanes' ds_read_b128 of consecutive
-// blocks hit distinct banks.
-template <typename T>
-__host__ __device__ constexpr int gate_blk() { return sizeof(T) == 8 ? 18 : 20; }
-__host__ __device__ constexpr int gate_nt(int M) { return (3 * M + 3) / 4 + 1; }   // tile rows: Y rows + B row
-template <typename T>
-__host__ __device__ constexpr int gate_area_T(int Mmax, int capb) {   // Y block staging / panel buffers
-    return 9 * capb > 2 * gate_blk<T>() * gate_nt(Mmax) ? 9 * capb : 2 * gate_blk<T>() * gate_nt(Mmax);
-}
-template <typename T>
-__host__ __device__ constexpr int gate_wave_lds_T(int Mmax, int capb) {
-    return 22 * Mmax + gate_area_T<T>(Mmax, capb);   // Ht rows, [r~ | r_n], staging / panels
-}
-
-template <typename T, int TPL, bool MP>
-__global__ void __launch_bounds__(256) k_gate_wave(DevState<T> st, Params<T> prm, FeatBatch<T> fb,
-                                                   const int* __restrict__ flist, int nlist, int Mmax, int capb) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, wpb = blockDim.x >> 6;
-    const int li = xcd_remap(blockIdx.x, gridDim.x) * wpb + wv;
-    if (li >= nlist) return;
-    const int f = flist[li];
-    if (!fb.valid[f]) {
-        if (lane == 0) { fb.gamma[f] = T(NAN); fb.accept[f] = 0; }
-        return;
-    }
-    const int b = fb.feat_filter[f];
-    const int o0 = fb.obs_off[f], M = fb.obs_off[f + 1] - o0, M3 = 3 * M;
-    const int nY = (M3 + 3) >> 2;               // Y tile rows = elimination steps
-    const int nT = nY + 1, ntiles = nT * (nT + 1) / 2;
-    T* ht = reinterpret_cast<T*>(smem_raw) + (size_t)wv * gate_wave_lds_T<T>(Mmax, capb);
-    T* rt = ht + 18 * Mmax;                    // [Mmax][4]: r~ (3), r_n
-    T* area = rt + 4 * Mmax;
-    constexpr int GB = gate_blk<T>();
-    T* stage = area;                           // [capb][9] Y blocks of one pass, column-major lower
-    T* wd = area;                              // [nT][GB]  panel rows: raw tile rows, then W D^-1
-    T* wt = area + GB * gate_nt(Mmax);         // [nT][GB]  W^T per 4-row block: wt[blk][4 c + y] = W[4 blk + y][c]
-    int* slot = reinterpret_cast<int*>(reinterpret_cast<T*>(smem_raw) + wpb * gate_wave_lds_T<T>(Mmax, capb)) + wv * Mmax;
-    const T* ws = fb.obs_ht + (size_t)o0 * OBS_HTS;
-    for (int e = lane; e < 18 * M; e += 64) {
-        const int o = e / 18;
-        ht[e] = ws[(size_t)o * OBS_HTS + OBS_HT + (e - 18 * o)];
-    }
-    T rn2 = 0;
-    for (int e = lane; e < 4 * M; e += 64) {
-        const T v = ws[(size_t)(e >> 2) * OBS_HTS + OBS_RT + (e & 3)];
-        rt[e] = v;
-        if ((e & 3) == 3) rn2 += v * v;
-    }
-    rn2 = wave_sum(rn2);
-    const T inv_s2 = T(1) / prm.sigma2;
-    for (int i = lane; i < M; i += 64) slot[i] = fb.obs_cam[o0 + i];
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-
-    // tile coordinates (column-major lower triangle of the nT x nT tile grid),
-    // packed ti | tl << 16 in one register; tlmax[s] (wave-uniform) is the last
-    // tile column present in slot s
-    int crd[TPL], tlmax[TPL];
-#pragma unroll
-    for (int s = 0; s < TPL; ++s) {
-        const int t = 64 * s + lane;
-        const int c = colmajor_col(t < ntiles ? t : 0, nT);
-        const int rem = (t < ntiles ? t : 0) - (c * nT - c * (c - 1) / 2);
-        crd[s] = t < ntiles ? ((c + rem) | (c << 16)) : -1;
-        const int tm = 64 * s + 63 < ntiles - 1 ? 64 * s + 63 : ntiles - 1;
-        tlmax[s] = 64 * s < ntiles ? colmajor_col(tm, nT) : -1;
-    }
-#define TI(s) (crd[s] & 0xffff)
-#define TL(s) (crd[s] >> 16)
-#define OK(s) (crd[s] >= 0)
-
-    // ---- Y: the observation-pair blocks Ht_a P_ab Ht_b^T (a >= b, 3x3) into
-    // LDS (column-major lower block order), then each lane assembles its tiles
-    // from there.  When the LDS budget holds fewer than all M (M + 1) / 2
-    // blocks (capb), this runs in passes over observation-column ranges that
-    // are multiples of four: columns [c0, c1) <-> tile columns [3 c0 / 4, 3 c1 / 4).
-    const T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
-    const int ldp = st.Dmax;
-    const T s2 = prm.sigma2;
-    constexpr int BIF = MP ? 1 : 2;   // blocks per lane in flight (multi-pass: the tiles are live meanwhile)
-    T a[TPL][4][4];
-    bool tiles_init = false;
-    auto init_tiles = [&]() {
-#pragma unroll
-        for (int s = 0; s < TPL; ++s) {
-    #pragma unroll
-            for (int x = 0; x < 4; ++x)
-    #pragma unroll
-                for (int y = 0; y < 4; ++y) a[s][x][y] = 0;
-            // B row: [H_f~^T ; r~^T] with H_f~ = -Ht[:, 3:6]
-            if (!OK(s) || TI(s) != nY || TL(s) >= nY) continue;
-    #pragma unroll
-            for (int y = 0; y < 4; ++y) {
-                const int p = 4 * TL(s) + y;
-                if (p >= M3) continue;
-                const int o = p / 3, c = p - 3 * o;
-    #pragma unroll
-                for (int x = 0; x < 3; ++x) a[s][x][y] = -ht[18 * o + 6 * c + 3 + x];
-                a[s][3][y] = rt[4 * o + c];
-            }
-        }
-    };
-    if (MP) { init_tiles(); tiles_init = true; }
-    for (int c0 = 0; c0 < M;) {
-        int c1 = c0, nbp = 0;
-        while (c1 < M) {
-            const int ce = c1 + 4 < M ? c1 + 4 : M;
-            int grp = 0;
-            for (int c = c1; c < ce; ++c) grp += M - c;
-            if (c1 > c0 && nbp + grp > capb) break;
-            nbp += grp;
-            c1 = ce;
-        }
-        const int kbase = c0 * M - c0 * (c0 - 1) / 2;
-        for (int k0 = 0; k0 < nbp; k0 += 64 * BIF) {
-            T Pl[BIF][36];
-            int oa[BIF], ob[BIF];
-#pragma unroll
-            for (int j = 0; j < BIF; ++j) {
-                const int kk = k0 + 64 * j + lane;
-                const int k = kbase + (kk < nbp ? kk : 0);
-                const int c = colmajor_col(k, M);
-                ob[j] = c;
-                oa[j] = c + k - (c * M - c * (c - 1) / 2);
-                const T* Pb = P + (size_t)(21 + 6 * slot[oa[j]]) * ldp + 21 + 6 * slot[ob[j]];
-                // each 6-element block row in wide loads (gfx950 takes dword-aligned
-                // multi-dword global loads: dwordx4 + dwordx2 per fp32 row)
-#pragma unroll
-                for (int u = 0; u < 6; ++u) {
-                    if (kk < nbp) {
-                        __builtin_memcpy(Pl[j] + 6 * u, Pb + (size_t)u * ldp, 6 * sizeof(T));
-                    } else {
-#pragma unroll
-                        for (int c2 = 0; c2 < 6; ++c2) Pl[j][6 * u + c2] = T(0);
-                    }
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < BIF; ++j) {
-                const int kk = k0 + 64 * j + lane;
-                if (kk >= nbp) continue;
-                const T* Ha = ht + 18 * oa[j];
-                const T* Hb = ht + 18 * ob[j];
-                T* dst = stage + 9 * kk;
-                // packed: column pairs in one v_pk_fma_f32 (not for TPL <= 2, where the extra
-                // VGPRs would cost an occupancy step the LDS does not already cost)
-                if constexpr (sizeof(T) == 4 && TPL >= 3) {
-                    using F2 = float __attribute__((ext_vector_type(2)));
-                    F2 hb01[6];                   // (Hb[0][u], Hb[1][u])
-#pragma unroll
-                    for (int u = 0; u < 6; ++u) hb01[u] = F2{Hb[u], Hb[6 + u]};
-#pragma unroll
-                    for (int x = 0; x < 3; ++x) {
-                        F2 t2[3] = {F2{0, 0}, F2{0, 0}, F2{0, 0}};   // t1 = Ha[x] P as three column pairs
-#pragma unroll
-                        for (int u = 0; u < 6; ++u) {
-                            const float h = Ha[6 * x + u];
-#pragma unroll
-                            for (int c = 0; c < 3; ++c)
-                                t2[c] = __builtin_elementwise_fma(F2{h, h}, F2{Pl[j][6 * u + 2 * c], Pl[j][6 * u + 2 * c + 1]},
-                                                                  t2[c]);
-                        }
-                        const float t1[6] = {t2[0].x, t2[0].y, t2[1].x, t2[1].y, t2[2].x, t2[2].y};
-                        F2 y01 = {0, 0};
-                        float y2 = 0;
-#pragma unroll
-                        for (int u = 0; u < 6; ++u) {
-                            y01 = __builtin_elementwise_fma(F2{t1[u], t1[u]}, hb01[u], y01);
-                            y2 = fmaf(t1[u], Hb[12 + u], y2);
-                        }
-                        dst[3 * x] = y01.x;
-                        dst[3 * x + 1] = y01.y;
-                        dst[3 * x + 2] = y2;
-                    }
-                } else {
-#pragma unroll
-                    for (int x = 0; x < 3; ++x) {
-                        T t1[6];
-#pragma unroll
-                        for (int c = 0; c < 6; ++c) {
-                            T acc = 0;
-#pragma unroll
-                            for (int u = 0; u < 6; ++u) acc += Ha[6 * x + u] * Pl[j][6 * u + c];
-                            t1[c] = acc;
-                        }
-#pragma unroll
-                        for (int y = 0; y < 3; ++y) {
-                            T acc = 0;
-#pragma unroll
-                            for (int u = 0; u < 6; ++u) acc += t1[u] * Hb[6 * y + u];
-                            dst[3 * x + y] = acc;
-                        }
-                    }
-                }
-            }
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // one wave: its stores are now visible to all lanes
-        if (!MP && !tiles_init) { init_tiles(); tiles_init = true; }   // single pass: tiles born after the blocks
-        const int tl_lo = 3 * c0 / 4, tl_hi = c1 >= M ? nY : 3 * c1 / 4;
-#pragma unroll
-        for (int s = 0; s < TPL; ++s) {
-            if (!OK(s) || tlmax[s] < tl_lo) continue;
-            int cs = crd[s];
-            asm volatile("" : "+v"(cs));   // keep the index arithmetic inside the pass loop (no hoisting)
-            const int tl = cs >> 16, ti = cs & 0xffff;
-            if (tl < tl_lo || tl >= tl_hi || ti >= nY) continue;
-            int oq[4], cq[4], op[4], cp[4];
-#pragma unroll
-            for (int x = 0; x < 4; ++x) {
-                oq[x] = (4 * ti + x) / 3;
-                cq[x] = 4 * ti + x - 3 * oq[x];
-                op[x] = (4 * tl + x) / 3;
-                cp[x] = 4 * tl + x - 3 * op[x];
-            }
-#pragma unroll
-            for (int x = 0; x < 4; ++x)
-#pragma unroll
-                for (int y = 0; y < 4; ++y) {
-                    const int q = 4 * ti + x, p = 4 * tl + y;
-                    T v = q == p ? T(1) : T(0);
-                    if (q < M3 && p < M3) {   // block (max, min) of the pair, column-major lower
-                        const int hi = oq[x] >= op[y] ? oq[x] : op[y], lo = oq[x] >= op[y] ? op[y] : oq[x];
-                        const int e = oq[x] >= op[y] ? 3 * cq[x] + cp[y] : 3 * cp[y] + cq[x];
-                        v = stage[9 * (lo * M - lo * (lo - 1) / 2 + hi - lo - kbase) + e];
-                        if (q == p) v += s2;
-                    }
-                    a[s][x][y] = v;
-                }
-            asm volatile("" ::: "memory");
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads done before the next pass / the panels reuse the area
-        c0 = c1;
-        if (!MP) break;   // single pass (capb >= M (M + 1) / 2): no back edge, the tiles stay dead in the block loop
-    }
-    if (!tiles_init) init_tiles();
-
-    // ---- blocked LDL^T over the nY Y tile columns, 4 pivots per step ----
-    bool fail = false;
-    for (int tj = 0; tj < nY; ++tj) {
-        // 1. owners of the tile column dump it (raw rows 4 tj .. 4 nT - 1)
-#pragma unroll
-        for (int s = 0; s < TPL; ++s) {
-            if (!OK(s) || TL(s) != tj) continue;
-            T* dst = wd + GB * TI(s);
-#pragma unroll
-            for (int x = 0; x < 4; ++x)
-#pragma unroll
-                for (int y = 0; y < 4; ++y) dst[4 * x + y] = a[s][x][y];
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        // 2. every lane factors the diagonal tile (uniform): A_d = L_d D L_d^T
-        // (one reciprocal per pivot: l_i0 d0 = A_i0, l_i1 d1 = A_i1 - l_i0 A_10, ...)
-        const T* dt = wd + GB * tj;
-        const T d0 = dt[0], e0 = pivot_rcp(d0);
-        const T l10 = dt[4] * e0, l20 = dt[8] * e0, l30 = dt[12] * e0;
-        const T d1 = dt[5] - l10 * dt[4], e1 = pivot_rcp(d1);
-        const T m21 = dt[9] - l20 * dt[4], m31 = dt[13] - l30 * dt[4];   // l21 d1, l31 d1
-        const T l21 = m21 * e1, l31 = m31 * e1;
-        const T d2 = dt[10] - l20 * dt[8] - l21 * m21, e2 = pivot_rcp(d2);
-        const T m32 = dt[14] - l30 * dt[8] - l31 * m21;                    // l32 d2
-        const T l32 = m32 * e2;
-        const T d3 = dt[15] - l30 * dt[12] - l31 * m31 - l32 * m32;
-        if (!(d0 > T(0)) || !(d1 > T(0)) || !(d2 > T(0)) || !(d3 > T(0))) { fail = true; break; }
-        const T e3 = pivot_rcp(d3);
-        // 3. panel rows below the diagonal tile: W = A L_d^-T; store W D^-1 by
-        //    row and W transposed by 4-row block
-        for (int q = 4 * tj + 4 + lane; q < 4 * nT; q += 64) {
-            T* row = wd + GB * (q >> 2) + 4 * (q & 3);
-            const T w0 = row[0];
-            const T w1 = row[1] - w0 * l10;
-            const T w2 = row[2] - w0 * l20 - w1 * l21;
-            const T w3 = row[3] - w0 * l30 - w1 * l31 - w2 * l32;
-            row[0] = w0 * e0; row[1] = w1 * e1; row[2] = w2 * e2; row[3] = w3 * e3;
-            T* col = wt + GB * (q >> 2) + (q & 3);
-            col[0] = w0; col[4] = w1; col[8] = w2; col[12] = w3;
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        // 4. trailing update A_il -= (W_i D^-1) W_l^T for tiles right of the panel
-#pragma unroll
-        for (int s = 0; s < TPL; ++s) {
-            if (tlmax[s] <= tj) continue;   // slot entirely in finished columns
-            if (!OK(s) || TL(s) <= tj) continue;
-            const T* ri = wd + GB * TI(s);
-            const T* cl = wt + GB * TL(s);
-            if constexpr (sizeof(T) == 4) {   // packed: column pairs (y, y+1) in one v_pk_fma_f32
-                using F2 = float __attribute__((ext_vector_type(2)));
-                const F2* c2 = reinterpret_cast<const F2*>(cl);   // c2[2 c + h] = (W^T[c][2h], W^T[c][2h+1])
-                F2 w2[4][2];
-#pragma unroll
-                for (int c = 0; c < 4; ++c) { w2[c][0] = c2[2 * c]; w2[c][1] = c2[2 * c + 1]; }
-#pragma unroll
-                for (int x = 0; x < 4; ++x) {
-                    T u[4];
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) u[c] = ri[4 * x + c];
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        F2 acc = {a[s][x][2 * h], a[s][x][2 * h + 1]};
-#pragma unroll
-                        for (int c = 0; c < 4; ++c) acc = __builtin_elementwise_fma(F2{-u[c], -u[c]}, w2[c][h], acc);
-                        a[s][x][2 * h] = acc.x;
-                        a[s][x][2 * h + 1] = acc.y;
-                    }
-                }
-            } else {
-                T u[4][4], w[4][4];
-#pragma unroll
-                for (int x = 0; x < 4; ++x)
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) { u[x][c] = ri[4 * x + c]; w[c][x] = cl[4 * c + x]; }
-#pragma unroll
-                for (int x = 0; x < 4; ++x)
-#pragma unroll
-                    for (int y = 0; y < 4; ++y)
-                        a[s][x][y] -= u[x][0] * w[0][y] + u[x][1] * w[1][y] + u[x][2] * w[2][y] + u[x][3] * w[3][y];
-            }
-            asm volatile("" ::: "memory");   // keep one slot's operands live at a time
-        }
-    }
-    // the last tile [[H_f~^T Y~^-1 H_f~, .], [., r~^T Y~^-1 r~]] (negated): three
-    // negative pivots, then -gamma of the range rows; the null rows add |r_n|^2 / s2
-#pragma unroll
-    for (int s = 0; s < TPL; ++s) {
-        if (64 * s + lane == ntiles - 1) {
-            const T d0 = a[s][0][0];
-            const T l10 = a[s][1][0] / d0, l20 = a[s][2][0] / d0, l30 = a[s][3][0] / d0;
-            const T d1 = a[s][1][1] - l10 * l10 * d0;
-            const T l21 = (a[s][2][1] - l20 * l10 * d0) / d1;
-            const T l31 = (a[s][3][1] - l30 * l10 * d0) / d1;
-            const T d2 = a[s][2][2] - l20 * l20 * d0 - l21 * l21 * d1;
-            const T l32 = (a[s][3][2] - l30 * l20 * d0 - l31 * l21 * d1) / d2;
-            const T d3 = a[s][3][3] - l30 * l30 * d0 - l31 * l31 * d1 - l32 * l32 * d2;
-            T gam = -d3 + rn2 * inv_s2;
-            if (fail || !(d0 < T(0)) || !(d1 < T(0)) || !(d2 < T(0)) || !(gam == gam)) gam = T(INFINITY);
-            fb.gamma[f] = gam;
-            fb.accept[f] = (gam < fb.chi2[f]) ? 1 : 0;
-        }
-    }
-#undef TI
-#undef TL
-#undef OK
-}
-
-// Large-track gating (40 < M <= 82): the reduced saddle-point LDL^T of
-// k_gate_wave (3M range rows padded to 4 ceil(3M/4), then the B row
-// [H_f~^T ; r~^T]) on rchol_core's fp64 register tiles, one workgroup per
-// feature.  The Y pivots are eliminated; the trailing 4x4 tile is the negated
-// [[H_f~^T Y~^-1 H_f~, .], [., r~^T Y~^-1 r~]] block, finished by one thread
-// with the three negative pivots: gamma = -(last pivot) + |r_n|^2 / s2.  Y
-// entries are formed on load from the fp64-staged Ht rows and the P blocks.
-template <typename T, int NT, int TPL>
-__global__ void __launch_bounds__(NT) k_gate_big(DevState<T> st, Params<T> prm, FeatBatch<T> fb,
-                                                 const int* __restrict__ flist) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    const int f = flist[blockIdx.x];
-    if (!fb.valid[f]) {
-        if (threadIdx.x == 0) { fb.gamma[f] = T(NAN); fb.accept[f] = 0; }
-        return;
-    }
-    const int b = fb.feat_filter[f];
-    const int o0 = fb.obs_off[f], M = fb.obs_off[f + 1] - o0, M3 = 3 * M;
-    const int nrow = gate_nt(M), n3 = 4 * (nrow - 1);
-    double* ht = reinterpret_cast<double*>(smem_raw);   // [M][18] Ht rows, then [M][4] r~ | r_n
-    double* rr = ht + 18 * M;
-    double* corner = rr + 4 * M;                         // [16], then the |r_n|^2 partials
-    int* slot = reinterpret_cast<int*>(corner + 16 + NT / 64);   // [M]
-    double* lds = reinterpret_cast<double*>(slot + ((M + 3) & ~3));   // rchol panel buffers
-    const T* ws = fb.obs_ht + (size_t)o0 * OBS_HTS;
-    for (int e = threadIdx.x; e < 18 * M; e += NT) {
-        const int o = e / 18;
-        ht[e] = (double)ws[(size_t)o * OBS_HTS + OBS_HT + (e - 18 * o)];
-    }
-    double rn2 = 0;
-    for (int e = threadIdx.x; e < 4 * M; e += NT) {
-        const double v = (double)ws[(size_t)(e >> 2) * OBS_HTS + OBS_RT + (e & 3)];
-        rr[e] = v;
-        if ((e & 3) == 3) rn2 += v * v;
-    }
-    rn2 = wave_sum(rn2);
-    if ((threadIdx.x & 63) == 0) corner[16 + (threadIdx.x >> 6)] = rn2;
-    for (int i = threadIdx.x; i < M; i += NT) slot[i] = fb.obs_cam[o0 + i];
-    __syncthreads();
-    const T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
-    const int ldp = st.Dmax;
-    const double s2 = (double)prm.sigma2;
-    // whole-tile loader: a 4x4 tile of the compact rows spans at most two
-    // observations each way; every P block (row obs, col obs) it needs is read
-    // once (6 rows of 6, wide loads) and shared by the tile's entries
-    auto load = [&](int i0, int j0, double (&t)[4][4]) {
-        if (i0 >= n3) {   // B row [H_f~^T ; r~^T] (zero corner tile)
-            if (j0 >= n3) return;
-#pragma unroll
-            for (int y = 0; y < 4; ++y) {
-                const int j = j0 + y;
-                if (j >= M3) continue;
-                const int o = j / 3, c = j - 3 * o;
-#pragma unroll
-                for (int x = 0; x < 3; ++x) t[x][y] = -ht[18 * o + 6 * c + 3 + x];
-                t[3][y] = rr[4 * o + c];
-            }
-            return;
-        }
-        const int oa0 = i0 / 3, ob0 = j0 / 3;
-#pragma unroll
-        for (int da = 0; da < 2; ++da)
-#pragma unroll
-            for (int db = 0; db < 2; ++db) {
-                const int oa = oa0 + da, ob = ob0 + db;
-                if (oa >= M || ob >= M) continue;
-                // rows x of the tile on observation oa, columns y on ob
-                int xs = 0, ys = 0;
-#pragma unroll
-                for (int x = 0; x < 4; ++x) xs |= ((i0 + x) / 3 == oa && i0 + x < M3) << x;
-#pragma unroll
-                for (int y = 0; y < 4; ++y) ys |= ((j0 + y) / 3 == ob && j0 + y < M3) << y;
-                if (!xs || !ys) continue;
-                const T* Pb = P + (size_t)(21 + 6 * slot[oa]) * ldp + 21 + 6 * slot[ob];
-                double t1[4][6];
-#pragma unroll
-                for (int x = 0; x < 4; ++x)
-#pragma unroll
-                    for (int v = 0; v < 6; ++v) t1[x][v] = 0.0;
-#pragma unroll
-                for (int u = 0; u < 6; ++u) {
-                    T prow[6];
-                    __builtin_memcpy(prow, Pb + (size_t)u * ldp, 6 * sizeof(T));
-#pragma unroll
-                    for (int x = 0; x < 4; ++x) {
-                        if (!((xs >> x) & 1)) continue;
-                        const double h = ht[18 * oa + 6 * (i0 + x - 3 * oa) + u];
-#pragma unroll
-                        for (int v = 0; v < 6; ++v) t1[x][v] += h * (double)prow[v];
-                    }
-                }
-#pragma unroll
-                for (int x = 0; x < 4; ++x) {
-                    if (!((xs >> x) & 1)) continue;
-#pragma unroll
-                    for (int y = 0; y < 4; ++y) {
-                        if (!((ys >> y) & 1)) continue;
-                        const double* hj = ht + 18 * ob + 6 * (j0 + y - 3 * ob);
-                        double acc = 0.0;
-#pragma unroll
-                        for (int v = 0; v < 6; ++v) acc += t1[x][v] * hj[v];
-                        t[x][y] = acc;
-                    }
-                }
-            }
-#pragma unroll
-        for (int x = 0; x < 4; ++x)   // s2 on the diagonal, unit pivots on the padding rows
-#pragma unroll
-            for (int y = 0; y < 4; ++y)
-                if (i0 + x == j0 + y) t[x][y] += i0 + x < M3 ? s2 : 1.0;
-    };
-    auto panel = [](int, int, double, double, double, double) {};
-    auto trail = [&](int i, int j, double v) { corner[(i - n3) * 4 + (j - n3)] = v; };
-    const bool ok = rchol_core<NT, TPL, decltype(load), decltype(panel), decltype(trail), true>(nrow, nrow, nrow - 1,
-                                                                                              lds, load, panel, trail);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double rsum = 0;
-        for (int w = 0; w < NT / 64; ++w) rsum += corner[16 + w];
-        T gam = T(INFINITY);
-        if (ok) {
-            const double* a = corner;
-            const double d0 = a[0];
-            const double l10 = a[4] / d0, l20 = a[8] / d0, l30 = a[12] / d0;
-            const double d1 = a[5] - l10 * l10 * d0;
-            const double l21 = (a[9] - l20 * l10 * d0) / d1;
-            const double l31 = (a[13] - l30 * l10 * d0) / d1;
-            const double d2 = a[10] - l20 * l20 * d0 - l21 * l21 * d1;
-            const double l32 = (a[14] - l30 * l20 * d0 - l31 * l21 * d1) / d2;
-            const double d3 = a[15] - l30 * l30 * d0 - l31 * l31 * d1 - l32 * l32 * d2;
-            if (d0 < 0.0 && d1 < 0.0 && d2 < 0.0 && -d3 == -d3) gam = (T)(-d3 + rsum / s2);
-        }
-        fb.gamma[f] = gam;
-        fb.accept[f] = (gam < fb.chi2[f]) ? 1 : 0;
-    }
-}
-
-size_t gate_big_lds_bytes(int maxM) {
-    return (22 * (size_t)maxM + 16 + 16) * sizeof(double) + ((maxM + 3) & ~3) * sizeof(int) +
-           rchol_lds_doubles(gate_nt(maxM)) * sizeof(double);
-}
+// (The kernels: msckf_gate_mfma.hip -- k_gate_mfma, one wave per feature, and
+// k_gate_mfma_wt, a 2- to 8-wave workgroup per feature of 9..16 blocks, both on
+// MFMA tiles.  Round 6 removed the fp64 register-tile kernels k_gate_wave and
+// k_gate_big they replaced for 37 <= M <= 82: 50x400 fp64 gate 56.2 -> 32.2 ms,
+// 80x1000 k_gate_big alone 117 ms -> k_gate_mfma_wt 54 ms, profiles/r06/wt64/.)
 
 // ===========================================================================
 // Stacking in feature order with the row cap (msckf.py:671-679): one
@@ -3175,39 +2681,6 @@ size_t gate_lds_bytes(int maxM) {
            (maxM + 4) * sizeof(int);
 }
 
-template <typename T, int TPL, bool MP>
-static void launch_gate_wave_cfg(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const FeatBatch<T>& fb,
-                                 const int* list, int cnt, int Mmax, int capb, int wpb, size_t lds) {
-    lds_limit((const void*)k_gate_wave<T, TPL, MP>, lds);
-    hipLaunchKernelGGL((k_gate_wave<T, TPL, MP>), dim3((cnt + wpb - 1) / wpb), dim3(64 * wpb), lds, s, st, prm, fb,
-                       list, cnt, Mmax, capb);
-}
-
-template <typename T, int TPL>
-static void launch_gate_wave(hipStream_t s, const DevState<T>& st, const Params<T>& prm, const FeatBatch<T>& fb,
-                             const int* list, int cnt, int Mmax) {
-    // Y staging capacity: all M (M + 1) / 2 blocks in one pass unless four
-    // waves would then need more than 80 KB (fewer than two workgroups per
-    // CU); then passes of fewer blocks (at least the first group of four
-    // observation columns) sized for 40 KB.  (Measured at 30x200: passes cost
-    // more than the occupancy they buy while two workgroups still fit --
-    // M <= 28: 1.60 ms multi-pass vs 1.40 ms single.)
-    const int nbk = Mmax * (Mmax + 1) / 2, first = 4 * Mmax - 6 > 1 ? 4 * Mmax - 6 : 1;
-    auto per_wave_of = [&](int cb) {
-        return (size_t)gate_wave_lds_T<T>(Mmax, cb) * sizeof(T) + (size_t)Mmax * sizeof(int);
-    };
-    int capb = nbk;
-    if (4 * per_wave_of(capb) > 80 * 1024)
-        for (int parts = 2; 4 * per_wave_of(capb) > 40 * 1024 && capb > first; ++parts)
-            capb = (nbk + parts - 1) / parts > first ? (nbk + parts - 1) / parts : first;
-    // waves (features) per workgroup: 4 unless their LDS would exceed the CU's 160 KB
-    const size_t per_wave = per_wave_of(capb);
-    const int wpb = 4 * per_wave <= 160 * 1024 ? 4 : (2 * per_wave <= 160 * 1024 ? 2 : 1);
-    const size_t lds = wpb * per_wave;
-    if (capb < nbk) launch_gate_wave_cfg<T, TPL, true>(s, st, prm, fb, list, cnt, Mmax, capb, wpb, lds);
-    else launch_gate_wave_cfg<T, TPL, false>(s, st, prm, fb, list, cnt, Mmax, capb, wpb, lds);
-}
-
 // Features are launched in size classes (by M, listed on the host at load
 // time): the register-tile wave kernel sized for the class, or for the
 // largest features the workgroup LDS kernel (global-memory kernel if even
@@ -3239,40 +2712,27 @@ void launch_gate(hipStream_t s, const DevState<T>& st, const Params<T>& prm, con
                     const int n = gc.big_off[j + 1] - gc.big_off[j], nb = j + GateClasses::BIG_NB0;
                     if (n == 0) continue;
                     if (nb < wt_lo) launch_gate_mfma<T>(s, st, prm, fb, gc.list + gc.big_off[j], n, gc.big_maxM[j]);
-                    else launch_gate_mfma_wt(s, st, prm, fb, gc.list + gc.big_off[j], n, nb, gc.big_maxM[j]);
+                    else launch_gate_mfma_wt<T>(s, st, prm, fb, gc.list + gc.big_off[j], n, nb, gc.big_maxM[j]);
+                }
+                continue;
+            }
+        }
+        if constexpr (sizeof(T) == 8) {
+            // fp64: 8 blocks and more (37 <= M <= 82) on k_gate_mfma_wt (round 6)
+            if (c == GateClasses::NC - 3) {
+                launch_gate_mfma_wt<T>(s, st, prm, fb, list, cnt, c + 1, maxM);
+                continue;
+            }
+            if (c == GateClasses::NC - 2 && gate_mfma_wt_fits(maxM)) {
+                for (int j = 0; j + GateClasses::BIG_NB0 <= GateClasses::BIG_NB1; ++j) {
+                    const int n = gc.big_off[j + 1] - gc.big_off[j], nb = j + GateClasses::BIG_NB0;
+                    if (n > 0) launch_gate_mfma_wt<T>(s, st, prm, fb, gc.list + gc.big_off[j], n, nb, gc.big_maxM[j]);
                 }
                 continue;
             }
         }
         if (c < GateClasses::NC - 2 && gate_mfma_fits(maxM, (int)sizeof(T))) {   // MFMA tiles (msckf_gate_mfma.hip)
             launch_gate_mfma<T>(s, st, prm, fb, list, cnt, maxM);
-            continue;
-        }
-        // (round 5: fp64 30 < M <= 40 on k_gate_big instead of k_gate_wave measured
-        // slower, gate 60.5 -> 63.4 ms at 50x400, profiles/r05/exp_gate_big_fp64_31_40/)
-        if (c == GateClasses::NC - 2) {   // 40 < M <= 82: register tiles, one workgroup per feature
-            const int nrow = gate_nt(maxM), tiles = nrow * (nrow + 1) / 2;
-            const size_t lds = gate_big_lds_bytes(maxM);
-            if (tiles <= 256 * 4) {
-                lds_limit((const void*)k_gate_big<T, 256, 4>, 160 * 1024);
-                hipLaunchKernelGGL((k_gate_big<T, 256, 4>), dim3(cnt), dim3(256), lds, s, st, prm, fb, list);
-            } else {
-                lds_limit((const void*)k_gate_big<T, 512, 4>, 160 * 1024);
-                hipLaunchKernelGGL((k_gate_big<T, 512, 4>), dim3(cnt), dim3(512), lds, s, st, prm, fb, list);
-            }
-            continue;
-        }
-        if (c < GateClasses::NC - 2) {
-            switch (GateClasses::TPL[c]) {
-                case 1: launch_gate_wave<T, 1>(s, st, prm, fb, list, cnt, maxM); break;
-                case 2: launch_gate_wave<T, 2>(s, st, prm, fb, list, cnt, maxM); break;
-                case 3: launch_gate_wave<T, 3>(s, st, prm, fb, list, cnt, maxM); break;
-                case 4: launch_gate_wave<T, 4>(s, st, prm, fb, list, cnt, maxM); break;
-                case 5: launch_gate_wave<T, 5>(s, st, prm, fb, list, cnt, maxM); break;
-                case 6: launch_gate_wave<T, 6>(s, st, prm, fb, list, cnt, maxM); break;
-                case 7: launch_gate_wave<T, 7>(s, st, prm, fb, list, cnt, maxM); break;
-                default: launch_gate_wave<T, 8>(s, st, prm, fb, list, cnt, maxM); break;
-            }
             continue;
         }
         const size_t lds = gate_lds_bytes<T>(maxM);

@@ -112,21 +112,16 @@ void launch_triangulate(hipStream_t, const DevState<T>&, const Params<T>&, const
 template <typename T>
 void launch_feature(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&, const SegClasses&);
 // Feature index lists per gating size class (device pointer + host offsets).
-// Gating size classes by observation count M.  Class c < NC-2 runs the
-// one-wave MFMA kernel (fp32; fp64 up to 7 blocks) or the one-wave register-tile
-// kernel with TPL[c] 4x4 tiles per lane (fp64); class NC-2 (M <= 82) the fp32
-// multi-wave MFMA kernel k_gate_mfma_wt by block count, or the fp64 workgroup
-// register-tile kernel k_gate_big; the last class the workgroup LDS kernel (or
-// its global-memory variant).
+// Gating size classes by observation count M.  Class c < NC-2 holds the
+// tracks of exactly c + 1 16-row blocks (ceil((3M + 4) / 16)) and runs the
+// one-wave MFMA kernel k_gate_mfma (fp64: up to 7 blocks; its 8-block class runs
+// k_gate_mfma_wt); class NC-2 (40 < M <= 82) the multi-wave MFMA kernel
+// k_gate_mfma_wt by block count (fp32: its 8-block sub-list, M = 41, one-wave);
+// the last class the workgroup LDS kernel (or its global-memory variant).
 struct GateClasses {
-    // one-wave classes by the tiles of the reduced (3M + 4)-square matrix,
-    // ceil((gate_nt(M) (gate_nt(M) + 1) / 2) / 64) per lane; then the
-    // register-tile workgroup kernel (nT <= 63) and the global-memory kernel
-    // (the one-wave class limits are also the fp32 MFMA kernel's 16-row block
-    // boundaries: ceil((3M + 4) / 16) = 1..8 for M <= 4, 9, 14, 20, 25, 30, 36, 40)
+    // block boundaries: ceil((3M + 4) / 16) = 1..8 for M <= 4, 9, 14, 20, 25, 30, 36, 40
     static constexpr int NC = 10;
     static constexpr int LIM[NC] = {4, 9, 14, 20, 25, 30, 36, 40, 82, 1 << 30};
-    static constexpr int TPL[NC - 2] = {1, 1, 2, 3, 4, 5, 7, 8};
     const int* list = nullptr;
     int off[NC + 1] = {};
     int maxM[NC] = {};
@@ -148,8 +143,9 @@ void launch_gate_mfma(hipStream_t, const DevState<T>&, const Params<T>&, const F
 // fp32 gating of the tracks of exactly nb 16-row blocks (9 <= nb <= 16, 41 < M <= 84)
 // on a 2- / 4- / 8-wave workgroup per feature (k_gate_mfma_wt)
 bool gate_mfma_wt_fits(int maxM);
-void launch_gate_mfma_wt(hipStream_t, const DevState<float>&, const Params<float>&, const FeatBatch<float>&,
-                         const int* list, int cnt, int nb, int maxM);
+template <typename T>
+void launch_gate_mfma_wt(hipStream_t, const DevState<T>&, const Params<T>&, const FeatBatch<T>&, const int* list,
+                         int cnt, int nb, int maxM);
 template <typename T>
 void launch_select(hipStream_t, const DevState<T>&, const FeatBatch<T>&, const UpdWs<T>&, int row_cap);
 template <typename T>
