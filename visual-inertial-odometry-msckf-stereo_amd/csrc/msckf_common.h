@@ -239,6 +239,17 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
     const int q = nwg >> 3, r = nwg & 7, xcd = orig & 7;
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
 }
+// Block coordinates of a 2-D / 3-D grid with the linear block id remapped so
+// that consecutive ids -- one filter's tiles or chunks (x fastest, then y) --
+// run on one XCD and share its L2 (the dispatcher deals linear ids round-robin
+// over the 8 XCDs, so a filter's tiles would otherwise re-read its operands from
+// HBM on every XCD).
+struct Blk3 { int x, y, z; };
+__device__ __forceinline__ Blk3 xcd_blk3() {
+    const int nx = gridDim.x, ny = gridDim.y, n = nx * ny * gridDim.z;
+    const int r = xcd_remap(blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z), n);
+    return {r % nx, (r / nx) % ny, r / (nx * ny)};
+}
 
 #define LDS_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
 
@@ -279,6 +290,24 @@ __device__ __forceinline__ int colmajor_col(int t, int nrow) {
 }
 
 // ------------------------------------------------------ wave reductions --
+// Per-type MFMA pieces (the gating kernels, the propagation cross block) (fp32 contexts: v_mfma_f32_16x16x4_f32;
+// fp64 contexts: v_mfma_f64_16x16x4_f64).  The A / B operand layouts agree (A:
+// row l & 15, k = l >> 4; B: k = l >> 4, column l & 15), the result layouts do
+// not: lane l holds column l & 15 and rows RG (l >> 4) + RS i, i = 0..3 -- f32:
+// 4 (l >> 4) + i, f64: (l >> 4) + 4 i (tools/probes/mfma_f64_layout.hip).
+template <typename T> struct GM;
+template <> struct GM<float> {
+    using V4 = float __attribute__((ext_vector_type(4)));
+    using V2 = float __attribute__((ext_vector_type(2)));
+    static constexpr int RS = 1, RG = 4;
+    __device__ static V4 mfma(float a, float b, V4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
+};
+template <> struct GM<double> {
+    using V4 = double __attribute__((ext_vector_type(4)));
+    using V2 = double __attribute__((ext_vector_type(2)));
+    static constexpr int RS = 4, RG = 1;
+    __device__ static V4 mfma(double a, double b, V4 c) { return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0); }
+};
 template <typename T>
 __device__ __forceinline__ T wave_sum(T x) {
 #pragma unroll

@@ -52,24 +52,7 @@ using F2 = float __attribute__((ext_vector_type(2)));
 using D4 = double __attribute__((ext_vector_type(4)));
 using D2 = double __attribute__((ext_vector_type(2)));
 
-// Per-type pieces of the one-wave kernel (fp32 contexts: v_mfma_f32_16x16x4_f32;
-// fp64 contexts: v_mfma_f64_16x16x4_f64).  The A / B operand layouts agree (A:
-// row l & 15, k = l >> 4; B: k = l >> 4, column l & 15), the result layouts do
-// not: lane l holds column l & 15 and rows RG (l >> 4) + RS i, i = 0..3 -- f32:
-// 4 (l >> 4) + i, f64: (l >> 4) + 4 i (tools/probes/mfma_f64_layout.hip).
-template <typename T> struct GM;
-template <> struct GM<float> {
-    using V4 = F4;
-    using V2 = F2;
-    static constexpr int RS = 1, RG = 4;
-    __device__ static F4 mfma(float a, float b, F4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
-};
-template <> struct GM<double> {
-    using V4 = D4;
-    using V2 = D2;
-    static constexpr int RS = 4, RG = 1;
-    __device__ static D4 mfma(double a, double b, D4 c) { return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0); }
-};
+// (GM<T>, the per-type MFMA pieces: msckf_common.h)
 __device__ __forceinline__ float gfma(float a, float b, float c) { return fmaf(a, b, c); }
 __device__ __forceinline__ double gfma(double a, double b, double c) { return fma(a, b, c); }
 

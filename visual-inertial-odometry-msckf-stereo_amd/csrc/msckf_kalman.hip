@@ -405,13 +405,14 @@ __global__ void __launch_bounds__(64) k_gchol_diag(DevState<T> st, UpdWs<T> ws, 
 // 2. panel rows i >= k + nb: A[i, k:k+nb] <- A[i, k:k+nb] L_kk^-T (one row per thread)
 template <int STAGE, typename T>
 __global__ void __launch_bounds__(256) k_gchol_trsm(DevState<T> st, UpdWs<T> ws, int k) {
-    const int b = blockIdx.y;
+    const Blk3 bk = xcd_blk3();
+    const int b = bk.y;
     KT* A;
     int nrow, ncol, nelim;
     if (!gdims<STAGE>(st, ws, b, A, nrow, ncol, nelim) || k >= nelim) return;
     const int ld = ncol, nb = nelim - k < GNB ? nelim - k : GNB;
-    const int i = k + nb + blockIdx.x * 256 + threadIdx.x;
-    if (k + nb + blockIdx.x * 256 >= nrow) return;
+    const int i = k + nb + bk.x * 256 + threadIdx.x;
+    if (k + nb + bk.x * 256 >= nrow) return;
     __shared__ double L[GNB][GNB + 1];
     for (int e = threadIdx.x; e < nb * nb; e += 256) {
         const int r = e / nb, c = e - r * nb;
@@ -436,7 +437,8 @@ __global__ void __launch_bounds__(256) k_gchol_trsm(DevState<T> st, UpdWs<T> ws,
 // stage A workspace in / out (grid-stride over the N x N lower part, blockIdx.y = filter)
 template <typename T>
 __global__ void __launch_bounds__(256) k_gchol_a_load(DevState<T> st, UpdWs<T> ws) {
-    const int b = blockIdx.y;
+    const Blk3 bk = xcd_blk3();
+    const int b = bk.y;
     KT* A;
     int N, ncol, nelim;
     if (!gdims<0>(st, ws, b, A, N, ncol, nelim)) return;
@@ -444,7 +446,7 @@ __global__ void __launch_bounds__(256) k_gchol_a_load(DevState<T> st, UpdWs<T> w
     const T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
     const int ld = st.Dmax;
     auto map = [&](int i) { return i < C ? 21 + i : i - C; };
-    for (int e = blockIdx.x * 256 + threadIdx.x; e < N * N; e += gridDim.x * 256) {
+    for (int e = bk.x * 256 + threadIdx.x; e < N * N; e += gridDim.x * 256) {
         const int i = e / N, j = e - i * N;
         if (j <= i) A[(size_t)i * N + j] = (KT)P[(size_t)map(i) * ld + map(j)];
     }
@@ -452,7 +454,8 @@ __global__ void __launch_bounds__(256) k_gchol_a_load(DevState<T> st, UpdWs<T> w
 
 template <typename T>
 __global__ void __launch_bounds__(256) k_gchol_a_store(DevState<T> st, UpdWs<T> ws) {
-    const int b = blockIdx.y;
+    const Blk3 bk = xcd_blk3();
+    const int b = bk.y;
     KT* A;
     int N, ncol, nelim;
     if (!gdims<0>(st, ws, b, A, N, ncol, nelim)) return;
@@ -460,7 +463,7 @@ __global__ void __launch_bounds__(256) k_gchol_a_store(DevState<T> st, UpdWs<T> 
     KT* Lc = ws.Lc + (size_t)b * Cpw * Cpw;
     KT* Vi = ws.Vi + (size_t)b * KW * Cpw;
     KT* Sii = ws.Sii + (size_t)b * KW * KW;
-    for (int e = blockIdx.x * 256 + threadIdx.x; e < N * N; e += gridDim.x * 256) {
+    for (int e = bk.x * 256 + threadIdx.x; e < N * N; e += gridDim.x * 256) {
         const int i = e / N, j = e - i * N;
         if (j > i) continue;
         const KT v = A[(size_t)i * N + j];
@@ -473,7 +476,8 @@ __global__ void __launch_bounds__(256) k_gchol_a_store(DevState<T> st, UpdWs<T> 
 // stage C workspace [C + E][C]: T (lower) then the extra rows [Vc_i (21); Lc (C); c^T]
 template <typename T>
 __global__ void __launch_bounds__(256) k_gchol_c_load(DevState<T> st, UpdWs<T> ws) {
-    const int b = blockIdx.y;
+    const Blk3 bk = xcd_blk3();
+    const int b = bk.y;
     KT* A;
     int nrow, C, nelim;
     if (!gdims<1>(st, ws, b, A, nrow, C, nelim)) return;
@@ -481,7 +485,7 @@ __global__ void __launch_bounds__(256) k_gchol_c_load(DevState<T> st, UpdWs<T> w
     const KT* Tm = ws.Tm + (size_t)b * ws.Cmax * ldt;
     const KT* Lc = ws.Lc + (size_t)b * Cpw * Cpw;
     const KT* Vi = ws.Vi + (size_t)b * KW * Cpw;
-    for (int e = blockIdx.x * 256 + threadIdx.x; e < nrow * C; e += gridDim.x * 256) {
+    for (int e = bk.x * 256 + threadIdx.x; e < nrow * C; e += gridDim.x * 256) {
         const int i = e / C, j = e - i * C;
         KT v = 0;
         if (i < C) v = j <= i ? Tm[(size_t)i * ldt + j] : KT(0);
@@ -497,13 +501,14 @@ __global__ void __launch_bounds__(256) k_gchol_c_load(DevState<T> st, UpdWs<T> w
 
 template <typename T>
 __global__ void __launch_bounds__(256) k_gchol_c_store(DevState<T> st, UpdWs<T> ws) {
-    const int b = blockIdx.y;
+    const Blk3 bk = xcd_blk3();
+    const int b = bk.y;
     KT* A;
     int nrow, C, nelim;
     if (!gdims<1>(st, ws, b, A, nrow, C, nelim)) return;
     const int E = nrow - C, Cpw = ws.Cp;
     KT* W = ws.W + (size_t)b * (st.Dmax + 1) * Cpw;
-    for (int e = blockIdx.x * 256 + threadIdx.x; e < E * C; e += gridDim.x * 256) {
+    for (int e = bk.x * 256 + threadIdx.x; e < E * C; e += gridDim.x * 256) {
         const int x = e / C, j = e - x * C;
         W[(size_t)x * Cpw + j] = A[(size_t)(C + x) * C + j];
     }
@@ -585,12 +590,13 @@ __device__ __forceinline__ void gemm64(int m, int n, int kb, int ke, int i0, int
 
 template <int STAGE, typename T>
 __global__ void __launch_bounds__(256) k_gchol_update(DevState<T> st, UpdWs<T> ws, int k) {
-    const int b = blockIdx.z;
+    const Blk3 bk = xcd_blk3();
+    const int b = bk.z;
     KT* A;
     int nrow, ncol, nelim;
     if (!gdims<STAGE>(st, ws, b, A, nrow, ncol, nelim) || k >= nelim) return;
     const int ld = ncol, k1 = k + (nelim - k < GNB ? nelim - k : GNB);
-    const int i0 = k1 + blockIdx.y * GT, j0 = k1 + blockIdx.x * GT;
+    const int i0 = k1 + bk.y * GT, j0 = k1 + bk.x * GT;
     if (i0 >= nrow || j0 >= ncol || i0 + GT - 1 < j0) return;   // outside, or entirely above the diagonal
     gemm64<true, true>(nrow, ncol, k, k1, i0, j0,
                        [&](int i, int p) { return A[(size_t)i * ld + p]; },
@@ -603,10 +609,11 @@ __global__ void __launch_bounds__(256) k_gchol_update(DevState<T> st, UpdWs<T> w
 // ---- stage B1: G = A Lc (C x C) ----
 template <typename T>
 __global__ void __launch_bounds__(256) k_kal_b1(DevState<T> st, UpdWs<T> ws) {
-    const int b = blockIdx.z;
+    const Blk3 bk = xcd_blk3();
+    const int b = bk.z;
     if (ws.info[4 * b] == 0) return;
     const int C = 6 * st.ncams[b];
-    const int i0 = blockIdx.y * GT, j0 = blockIdx.x * GT;
+    const int i0 = bk.y * GT, j0 = bk.x * GT;
     if (i0 >= C || j0 >= C) return;
     const int lda = ws.Cmax + 1, Cpw = ws.Cp;
     const KT* Am = ws.Hthin + (size_t)b * ws.Cmax * lda;
@@ -621,10 +628,11 @@ __global__ void __launch_bounds__(256) k_kal_b1(DevState<T> st, UpdWs<T> ws) {
 // ---- stage B2: [T | c] = s2 I + Lc^T [G | b] (lower triangle of T, and c) ----
 template <typename T>
 __global__ void __launch_bounds__(256) k_kal_b2(DevState<T> st, Params<T> prm, UpdWs<T> ws) {
-    const int b = blockIdx.z;
+    const Blk3 bk = xcd_blk3();
+    const int b = bk.z;
     if (ws.info[4 * b] == 0) return;
     const int C = 6 * st.ncams[b];
-    const int i0 = blockIdx.y * GT, j0 = blockIdx.x * GT;
+    const int i0 = bk.y * GT, j0 = bk.x * GT;
     if (i0 >= C || j0 > C) return;
     if (j0 > i0 + GT - 1 && !(C >= j0 && C < j0 + GT)) return;   // strictly upper and no c column
     const int ld = ws.Cmax + 1, Cpw = ws.Cp;
@@ -841,10 +849,11 @@ __global__ void __launch_bounds__(64 * NW) k_kal_b(DevState<T> st, Params<T> prm
 // ---- stage E: P+ = blockdiag(S_ii, 0) + s2 W W^T (lower tiles, mirrored), dx = W y ----
 template <typename T>
 __global__ void __launch_bounds__(256) k_kal_e(DevState<T> st, Params<T> prm, UpdWs<T> ws) {
-    const int b = blockIdx.z;
+    const Blk3 bk = xcd_blk3();
+    const int b = bk.z;
     if (ws.info[4 * b] == 0 || ws.info[4 * b + 3] < 0) return;
     const int C = 6 * st.ncams[b], D = 21 + C;
-    const int i0 = blockIdx.y * GT, j0 = blockIdx.x * GT;
+    const int i0 = bk.y * GT, j0 = bk.x * GT;
     if (i0 >= D || j0 > D) return;
     if (j0 > i0 + GT - 1 && !(D >= j0 && D < j0 + GT)) return;
     const int Cpw = ws.Cp, ld = st.Dmax;

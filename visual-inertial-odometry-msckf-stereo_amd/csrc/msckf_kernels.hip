@@ -604,47 +604,78 @@ __global__ void __launch_bounds__(64) k_propagate(DevState<T> st, Params<T> prm,
     }
     if (lane < IMU_STRIDE) imu[lane] = s_imu[lane];
     prop_sync();
-    // 64 columns x 21 of the new cross block: over both P11 and both cumulative-Phi
-    // buffers (free now; PH, after them, holds the cumulative Phi)
-    T* xb = reinterpret_cast<T*>(smem_raw);
-    static_assert(4 * MAT >= 64 * XBS, "cross-block staging");
+    // The IMU x cam cross block P[0:21, 21:D] <- Phi_cum P[0:21, 21:D] (and its
+    // transpose), 64 cam columns per chunk, on MFMA tiles (v_mfma_f32_16x16x4f32 /
+    // v_mfma_f64_16x16x4f64).  Phi_cum = Phi_n ... Phi_1 differs from I only in row
+    // blocks 0, 2, 4 (rows 0-2, 6-8, 12-14), whose non-zeros lie in columns 0..14
+    // (PM_PHI): the A operand is those nine rows (padded to 16) over K = 0..15, the
+    // B operand the chunk's rows 0..15 staged in LDS as [column][17], four 16-column
+    // tiles per chunk; the identity rows are copies.  The results go through the
+    // [column][XBS] staging rows (aliasing the B stage: every MFMA operand is read
+    // before the first staging write, one wave's LDS operations run in order) to
+    // row-major stores of both halves.
+    T* xb = reinterpret_cast<T*>(smem_raw);   // [64][XBS] staging rows; the B stage [64][17] first
+    static_assert(4 * MAT >= 64 * XBS && 4 * MAT >= 64 * 17, "cross-block staging");
+    using XV4 = typename GM<T>::V4;
+    constexpr int XRS = GM<T>::RS, XRG = GM<T>::RG;
+    const int l15 = lane & 15, lg = lane >> 4;
+    const int arow = l15 < 9 ? 6 * (l15 / 3) + l15 % 3 : 0;   // rows 0-2, 6-8, 12-14 of Phi_cum
+    T aop[4];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+        const int k = 4 * kk + lg;
+        const bool nz = l15 < 9 && k < 15 && ((PM_PHI >> (7 * (arow / 3) + k / 3)) & 1ull);
+        aop[kk] = nz ? PH[arow * RS + k] : T(0);
+    }
+    auto cross_chunk = [&](int j0, const T (&col)[21]) {
+        const bool in = j0 + lane < D;
+        T* S = xb;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) S[lane * 17 + k] = (in && k < 15) ? col[k] : T(0);
+        prop_sync();
+        // one 16-column tile at a time (four accumulator registers: the kernel sits at
+        // two waves per SIMD with ~240 VGPRs); the B operands of all four tiles are
+        // read before the first staging write
+        T bop[4][4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) bop[t][kk] = S[(16 * t + l15) * 17 + 4 * kk + lg];
+        prop_sync();
+#pragma unroll
+        for (int m = 0; m < 21; ++m)
+            if ((m / 3) & 1 || m >= 15) xb[lane * XBS + m] = col[m];   // identity rows
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            XV4 acc = XV4{0, 0, 0, 0};
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) acc = GM<T>::mfma(aop[kk], bop[t][kk], acc);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int r = XRG * lg + XRS * i;
+                if (r < 9) xb[(16 * t + l15) * XBS + 6 * (r / 3) + r % 3] = acc[i];
+            }
+        }
+        prop_sync();
+        if (in) {
+#pragma unroll
+            for (int i = 0; i < 21; ++i) P[i * ld + j0 + lane] = xb[lane * XBS + i];
+        }
+        xb_rows(P, ld, j0, min(64, D - j0), xb, lane);
+        prop_sync();
+    };
 #pragma unroll
     for (int pp = 0; pp < NPRE + 1; ++pp) {
         if (pp == NPRE) break;
-        const int j = 21 + 64 * pp + lane;
         if (21 + 64 * pp >= D) break;
-        if (j < D) {
-#pragma unroll
-            for (int i = 0; i < 21; ++i) {
-                const unsigned msk = (unsigned)(PM_PHI >> (7 * (i / 3))) & 0x7fu;
-                const T sacc = prop_dot(PH + i * RS, pre[pp], msk);
-                P[i * ld + j] = sacc;
-                xb[lane * XBS + i] = sacc;
-            }
-        }
-        prop_sync();
-        const int j0 = 21 + 64 * pp, nj = min(64, D - j0);
-        xb_rows(P, ld, j0, nj, xb, lane);
-        prop_sync();
+        cross_chunk(21 + 64 * pp, pre[pp]);
     }
     for (int j0 = 21 + 64 * NPRE; j0 < D; j0 += 64) {
         const int j = j0 + lane;
-        if (j < D) {
-            T col[21];
+        T col[21];
 #pragma unroll
-            for (int m = 0; m < 21; ++m) col[m] = P[m * ld + j];
-#pragma unroll
-            for (int i = 0; i < 21; ++i) {
-                const unsigned msk = (unsigned)(PM_PHI >> (7 * (i / 3))) & 0x7fu;
-                const T sacc = prop_dot(PH + i * RS, col, msk);
-                P[i * ld + j] = sacc;
-                xb[lane * XBS + i] = sacc;
-            }
-        }
-        prop_sync();
-        const int nj = min(64, D - j0);
-        xb_rows(P, ld, j0, nj, xb, lane);
-        prop_sync();
+        for (int m = 0; m < 21; ++m) col[m] = j < D ? P[m * ld + j] : T(0);
+        cross_chunk(j0, col);
     }
     PPROBE_T(t_end1);
     PPROBE_ADD(7, t_end1 - t_end0);
@@ -1663,9 +1694,14 @@ __host__ __device__ constexpr int info_slot_doubles(int Nmax) { return (Nmax * O
 
 template <typename T, int BPT, int NT>
 __global__ void __launch_bounds__(NT) k_info(DevState<T> st, FeatBatch<T> fb, UpdWs<T> ws, int fbn, int maxnf,
-                                             int maxobs) {
+                                             int maxobs, int rmp) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    const int b = blockIdx.x;
+    // grid (parts, B), parts >= 3 (80 cams: 4): a filter's parts get consecutive ids,
+    // remapped onto one XCD so that its records come from HBM once into that XCD's
+    // L2 (80x1000 compress 15.1 -> 14.1 ms); two parts (50 cams) measured slower
+    // that way (8.3 -> 8.9 ms) and keep the plain order, grid (B, parts)
+    const Blk3 bk = xcd_blk3();
+    const int b = rmp ? bk.y : blockIdx.x, part = rmp ? bk.x : blockIdx.y;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwave = NT >> 6;
     const int nc = st.ncams[b], C = 6 * nc, Cmax = ws.Cmax, Nmax = st.Nmax;
     int* info = ws.info + 4 * b;
@@ -1696,7 +1732,7 @@ __global__ void __launch_bounds__(NT) k_info(DevState<T> st, FeatBatch<T> fb, Up
         // a feature's contiguous cam range [s, e] activates the pairs s <= J <= I <= e,
         // a triangle that whole tiles cover far better than the row-major block order
         // (whose 64-block strips are mostly inactive for every feature)
-        const int tt = blockIdx.y * (NT >> 6) * BPT + (tid >> 6) + (NT >> 6) * m;
+        const int tt = part * (NT >> 6) * BPT + (tid >> 6) + (NT >> 6) * m;
         const int TS = (Nmax + 7) >> 3, ntl = TS * (TS + 1) / 2;
         int ti = (int)((sqrtf(8.0f * (float)tt + 1.0f) - 1.0f) * 0.5f);
         while (ti * (ti + 1) / 2 > tt) --ti;
@@ -1845,7 +1881,7 @@ __global__ void __launch_bounds__(NT) k_info(DevState<T> st, FeatBatch<T> fb, Up
 #pragma unroll
             for (int x = 0; x < 6; ++x) F[(size_t)(6 * I[m] + x) * ldf + Cmax] = bv[m][x];
     }
-    if (tid == 0 && blockIdx.y == 0) info[1] = C;
+    if (tid == 0 && part == 0) info[1] = C;
 }
 
 // ---------------------------------------------------------------------------
@@ -2765,8 +2801,9 @@ static void launch_info_cfg(hipStream_t s, const DevState<T>& st, const FeatBatc
     const int TS = (st.Nmax + 7) / 8, ntl = TS * (TS + 1) / 2;
     const int parts = (ntl + (NT / 64) - 1) / (NT / 64);
     lds_limit((const void*)k_info<T, 1, NT>, lds);
-    hipLaunchKernelGGL((k_info<T, 1, NT>), dim3(st.B, parts), dim3(NT), lds, s, st, fb, ws, fbn, pre ? maxnf : 0,
-                       pre ? maxobs : 0);
+    const int rmp = parts > 2;
+    hipLaunchKernelGGL((k_info<T, 1, NT>), rmp ? dim3(parts, st.B) : dim3(st.B, parts), dim3(NT), lds, s, st, fb, ws, fbn,
+                       pre ? maxnf : 0, pre ? maxobs : 0, rmp);
 }
 
 bool info_fused_fits(int Nmax, int maxnf) { return Nmax <= 32 && maxnf > 0 && info_fused_lds(maxnf) <= 160 * 1024; }
