@@ -539,7 +539,10 @@ constexpr int GT = 64, GK = 16, GPAD = 80;
 
 template <bool A_KFAST, bool B_KFAST, class FA, class FB, class FS>
 __device__ __forceinline__ void gemm64(int m, int n, int kb, int ke, int i0, int j0, FA A, FB B, FS store) {
-    __shared__ __attribute__((aligned(16))) double sa[GK][GPAD], sb[GK][GPAD];
+    // double-buffered K chunks: chunk c + 1's global loads are in flight (in
+    // registers) under chunk c's MFMAs, one barrier per chunk (round 6; the
+    // single-buffered loop exposed every chunk's load latency)
+    __shared__ __attribute__((aligned(16))) double sa[2][GK][GPAD], sb[2][GK][GPAD];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int wr = w >> 1, wc = w & 1, lc = lane & 15, lr = lane >> 4;
     v4d acc[2][2];
@@ -547,27 +550,48 @@ __device__ __forceinline__ void gemm64(int m, int n, int kb, int ke, int i0, int
     for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
         for (int ni = 0; ni < 2; ++ni) acc[mi][ni] = v4d{0.0, 0.0, 0.0, 0.0};
-    for (int k0 = kb; k0 < ke; k0 += GK) {
+    double ra[4], rb[4];
+    auto gload = [&](int k0) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int e = tid + 256 * q;
             int ii, kk, jj, k2;
             if (A_KFAST) { ii = e >> 4; kk = e & 15; } else { ii = e & 63; kk = e >> 6; }
             const int gi = i0 + ii, gk = k0 + kk;
-            sa[kk][ii] = (gi < m && gk < ke) ? A(gi, gk) : 0.0;
+            ra[q] = (gi < m && gk < ke) ? A(gi, gk) : 0.0;
             if (B_KFAST) { jj = e >> 4; k2 = e & 15; } else { jj = e & 63; k2 = e >> 6; }
             const int gj = j0 + jj, gk2 = k0 + k2;
-            sb[k2][jj] = (gj < n && gk2 < ke) ? B(gk2, gj) : 0.0;
+            rb[q] = (gj < n && gk2 < ke) ? B(gk2, gj) : 0.0;
         }
-        __syncthreads();
+    };
+    auto sstore = [&](int bf) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int e = tid + 256 * q;
+            int ii, kk, jj, k2;
+            if (A_KFAST) { ii = e >> 4; kk = e & 15; } else { ii = e & 63; kk = e >> 6; }
+            if (B_KFAST) { jj = e >> 4; k2 = e & 15; } else { jj = e & 63; k2 = e >> 6; }
+            sa[bf][kk][ii] = ra[q];
+            sb[bf][k2][jj] = rb[q];
+        }
+    };
+    if (kb < ke) {
+        gload(kb);
+        sstore(0);
+    }
+    __syncthreads();
+    for (int k0 = kb, it = 0; k0 < ke; k0 += GK, ++it) {
+        const int bf = it & 1;
+        const bool more = k0 + GK < ke;   // uniform
+        if (more) gload(k0 + GK);
 #pragma unroll
         for (int kc = 0; kc < GK / 4; ++kc) {
             const int kr = 4 * kc + lr;
             double av[2], bv[2];
 #pragma unroll
             for (int t = 0; t < 2; ++t) {
-                av[t] = sa[kr][32 * wr + 16 * t + lc];
-                bv[t] = sb[kr][32 * wc + 16 * t + lc];
+                av[t] = sa[bf][kr][32 * wr + 16 * t + lc];
+                bv[t] = sb[bf][kr][32 * wc + 16 * t + lc];
             }
 #pragma unroll
             for (int mi = 0; mi < 2; ++mi)
@@ -575,6 +599,7 @@ __device__ __forceinline__ void gemm64(int m, int n, int kb, int ke, int i0, int
                 for (int ni = 0; ni < 2; ++ni)
                     acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[mi], bv[ni], acc[mi][ni], 0, 0, 0);
         }
+        if (more) sstore(bf ^ 1);
         __syncthreads();
     }
 #pragma unroll
