@@ -331,14 +331,20 @@ __global__ void __launch_bounds__(64 * NW) k_kal_c2(DevState<T> st, UpdWs<T> ws)
 // ===========================================================================
 constexpr int GNB = 64;   // pivots per panel (50x400 / 80x1000 updates/s: 16: 24.1k / 4.98k, 32: 26.3k / 5.27k, 48: 26.8k / 5.21k, 64: 27.5k / 5.20k)
 
-// stage 0 = A: [P_cc P_ci; P_ic P_ii] (N = C + 21 square, C pivots);
-// stage 1 = C: T (C square) with the extra rows [Vc_i (21); Lc (C); c^T]
+// stage 0 = A: [P_cc P_ci; P_ic P_ii] (N = C + 21 square, C pivots), at the
+// start of the filter's workspace;
+// stage 1 = C: T (C square) with the extra rows [Vc_i (21); Lc (C); c^T], after
+// it (gchol_c_off): stage A's store writes the Vc_i / Lc rows and stage B2 the
+// T / c rows straight into it, and stage E reads the solved extra rows (W) from
+// it -- no copies in or out (round 6: k_gchol_c_load / c_store, 1.8 ms per
+// 50x400 step, removed)
+__host__ __device__ constexpr size_t gchol_c_off(int Cmax) { return (size_t)(Cmax + 21) * (Cmax + 21); }
 template <int STAGE, typename T>
 __device__ __forceinline__ bool gdims(const DevState<T>& st, const UpdWs<T>& ws, int b, KT*& A, int& nrow,
                                       int& ncol, int& nelim) {
     if (ws.info[4 * b] == 0 || ws.info[4 * b + 3] < 0) return false;
     const int C = 6 * st.ncams[b];
-    A = ws.Wk + (size_t)b * ws.wk_stride;
+    A = ws.Wk + (size_t)b * ws.wk_stride + (STAGE == 0 ? 0 : gchol_c_off(ws.Cmax));
     if (STAGE == 0) { nrow = C + 21; ncol = C + 21; }
     else { nrow = C + 22 + C; ncol = C; }
     nelim = C;
@@ -360,8 +366,8 @@ __global__ void __launch_bounds__(64) k_gchol_diag(DevState<T> st, UpdWs<T> ws, 
         d[i][j] = j <= i ? A[(size_t)(k + i) * ld + k + j] : 0.0;
     }
     // stage A: pivots floored as in k_kal_a (pcc_pivot_floor); stage C: at s2 down
-    // to -T_FLOOR_NEG x max diag(T), as k_kal_c1 / k_kal_mchol (T itself is still
-    // intact in ws.Tm: k_gchol_c_load factors a copy)
+    // to -T_FLOOR_NEG x max diag(T), as k_kal_c1 / k_kal_mchol (stage B2 keeps
+    // diag(T) in ws.Tm: the matrix itself is factored in place)
     double floor = STAGE == 0 ? 0.0 : ws.s2, lo;
     if (STAGE == 0) {
         const T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
@@ -463,54 +469,23 @@ __global__ void __launch_bounds__(256) k_gchol_a_store(DevState<T> st, UpdWs<T> 
     KT* Lc = ws.Lc + (size_t)b * Cpw * Cpw;
     KT* Vi = ws.Vi + (size_t)b * KW * Cpw;
     KT* Sii = ws.Sii + (size_t)b * KW * KW;
+    KT* Xc = ws.Wk + (size_t)b * ws.wk_stride + gchol_c_off(ws.Cmax) + (size_t)C * C;   // stage C's extra rows (ld C)
     for (int e = bk.x * 256 + threadIdx.x; e < N * N; e += gridDim.x * 256) {
         const int i = e / N, j = e - i * N;
-        if (j > i) continue;
-        const KT v = A[(size_t)i * N + j];
-        if (i < C) Lc[(size_t)i * Cpw + j] = v;
-        else if (j < C) Vi[(size_t)(i - C) * Cpw + j] = v;
-        else Sii[(i - C) * KW + (j - C)] = v;
-    }
-}
-
-// stage C workspace [C + E][C]: T (lower) then the extra rows [Vc_i (21); Lc (C); c^T]
-template <typename T>
-__global__ void __launch_bounds__(256) k_gchol_c_load(DevState<T> st, UpdWs<T> ws) {
-    const Blk3 bk = xcd_blk3();
-    const int b = bk.y;
-    KT* A;
-    int nrow, C, nelim;
-    if (!gdims<1>(st, ws, b, A, nrow, C, nelim)) return;
-    const int Cpw = ws.Cp, ldt = ws.Cmax + 1;
-    const KT* Tm = ws.Tm + (size_t)b * ws.Cmax * ldt;
-    const KT* Lc = ws.Lc + (size_t)b * Cpw * Cpw;
-    const KT* Vi = ws.Vi + (size_t)b * KW * Cpw;
-    for (int e = bk.x * 256 + threadIdx.x; e < nrow * C; e += gridDim.x * 256) {
-        const int i = e / C, j = e - i * C;
-        KT v = 0;
-        if (i < C) v = j <= i ? Tm[(size_t)i * ldt + j] : KT(0);
-        else {
-            const int x = i - C;
-            if (x < 21) v = Vi[(size_t)x * Cpw + j];
-            else if (x < 21 + C) v = j <= x - 21 ? Lc[(size_t)(x - 21) * Cpw + j] : KT(0);
-            else v = Tm[(size_t)j * ldt + C];
+        if (j > i) {   // the zeros above Lc's diagonal, in stage C's Lc rows
+            if (j < C) Xc[(size_t)(21 + i) * C + j] = 0.0;
+            continue;
         }
-        A[(size_t)i * C + j] = v;
-    }
-}
-
-template <typename T>
-__global__ void __launch_bounds__(256) k_gchol_c_store(DevState<T> st, UpdWs<T> ws) {
-    const Blk3 bk = xcd_blk3();
-    const int b = bk.y;
-    KT* A;
-    int nrow, C, nelim;
-    if (!gdims<1>(st, ws, b, A, nrow, C, nelim)) return;
-    const int E = nrow - C, Cpw = ws.Cp;
-    KT* W = ws.W + (size_t)b * (st.Dmax + 1) * Cpw;
-    for (int e = bk.x * 256 + threadIdx.x; e < E * C; e += gridDim.x * 256) {
-        const int x = e / C, j = e - x * C;
-        W[(size_t)x * Cpw + j] = A[(size_t)(C + x) * C + j];
+        const KT v = A[(size_t)i * N + j];
+        if (i < C) {
+            Lc[(size_t)i * Cpw + j] = v;
+            Xc[(size_t)(21 + i) * C + j] = v;
+        } else if (j < C) {
+            Vi[(size_t)(i - C) * Cpw + j] = v;
+            Xc[(size_t)(i - C) * C + j] = v;
+        } else {
+            Sii[(i - C) * KW + (j - C)] = v;
+        }
     }
 }
 
@@ -523,7 +498,7 @@ size_t kalman_global_ws_doubles(int Cmax) {   // per filter, 0 when the register
     if (kalman_chol_supported(Cmax)) return 0;
     const size_t C = Cmax, N = C + 21, E = 21 + C + 1;
     const size_t a = N * N, c = (C + E) * C;
-    return a > c ? a : c;
+    return a + c;   // stage A's matrix, then stage C's (gchol_c_off)
 }
 
 // ===========================================================================
@@ -664,14 +639,19 @@ __global__ void __launch_bounds__(256) k_kal_b2(DevState<T> st, Params<T> prm, U
     const KT* Lc = ws.Lc + (size_t)b * Cpw * Cpw;
     const KT* G = ws.G + (size_t)b * ws.Cmax * ld;
     const KT* Hb = ws.Hthin + (size_t)b * ws.Cmax * ld;   // b in column Cmax
-    KT* Tm = ws.Tm + (size_t)b * ws.Cmax * ld;
+    KT* Tm = ws.Tm + (size_t)b * ws.Cmax * ld;   // its diagonal only: stage C's pivot bound (k_gchol_diag<1>)
+    KT* Ac = ws.Wk + (size_t)b * ws.wk_stride + gchol_c_off(ws.Cmax);   // stage C's [T ; extra rows], ld C
     const double s2 = (double)prm.sigma2;
     gemm64<false, false>(C, C + 1, i0 & ~(GK - 1), C, i0, j0,
                          [&](int i, int k) { return k >= i ? Lc[(size_t)k * Cpw + i] : 0.0; },
                          [&](int k, int j) { return j < C ? G[(size_t)k * ld + j] : Hb[(size_t)k * ld + ws.Cmax]; },
                          [&](int i, int j, double v) {
-                             if (j < C && j <= i) Tm[(size_t)i * ld + j] = v + (i == j ? s2 : 0.0);
-                             if (j == C) Tm[(size_t)i * ld + C] = v;
+                             if (j < C && j <= i) {
+                                 const double t = v + (i == j ? s2 : 0.0);
+                                 Ac[(size_t)i * C + j] = t;
+                                 if (i == j) Tm[(size_t)i * ld + i] = t;
+                             }
+                             if (j == C) Ac[(size_t)(2 * C + 21) * C + i] = v;   // c^T: the last extra row
                          });
 }
 
@@ -881,14 +861,15 @@ __global__ void __launch_bounds__(256) k_kal_e(DevState<T> st, Params<T> prm, Up
     const int i0 = bk.y * GT, j0 = bk.x * GT;
     if (i0 >= D || j0 > D) return;
     if (j0 > i0 + GT - 1 && !(D >= j0 && D < j0 + GT)) return;
-    const int Cpw = ws.Cp, ld = st.Dmax;
-    const KT* W = ws.W + (size_t)b * (st.Dmax + 1) * Cpw;
+    const int ld = st.Dmax;
+    // W: stage C's solved extra rows [Vc_i ; Lc ; c^T] L_T^-T, in place after T (ld C)
+    const KT* W = ws.Wk + (size_t)b * ws.wk_stride + gchol_c_off(ws.Cmax) + (size_t)C * C;
     const KT* Sii = ws.Sii + (size_t)b * KW * KW;
     T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
     KT* dx = ws.dx + (size_t)b * (st.Dmax + ws.Cmax);
     const double s2 = (double)prm.sigma2;
-    gemm64<true, true>(D, D + 1, 0, C, i0, j0, [&](int i, int k) { return W[(size_t)i * Cpw + k]; },
-                       [&](int k, int j) { return W[(size_t)(j < D ? j : D) * Cpw + k]; },
+    gemm64<true, true>(D, D + 1, 0, C, i0, j0, [&](int i, int k) { return W[(size_t)i * C + k]; },
+                       [&](int k, int j) { return W[(size_t)(j < D ? j : D) * C + k]; },
                        [&](int i, int j, double v) {
                            if (j < D && j <= i) {
                                double p = s2 * v;
@@ -1270,7 +1251,6 @@ static void launch_gchol(hipStream_t s, const DevState<T>& st, const UpdWs<T>& w
     const int nrow = STAGE == 0 ? Cmax + 21 : 2 * Cmax + 22, ncol = STAGE == 0 ? Cmax + 21 : Cmax;
     const int ld_chunks = (nrow * ncol + 256 * 64 - 1) / (256 * 64);
     if (STAGE == 0) hipLaunchKernelGGL(k_gchol_a_load<T>, dim3(ld_chunks, st.B), dim3(256), 0, s, st, ws);
-    else hipLaunchKernelGGL(k_gchol_c_load<T>, dim3(ld_chunks, st.B), dim3(256), 0, s, st, ws);
     for (int k = 0; k < Cmax; k += GNB) {
         hipLaunchKernelGGL((k_gchol_diag<STAGE, T>), dim3(st.B), dim3(64), 0, s, st, ws, k);
         // grids for the rows / columns below / right of the panel: a filter's last panel
@@ -1284,7 +1264,6 @@ static void launch_gchol(hipStream_t s, const DevState<T>& st, const UpdWs<T>& w
             hipLaunchKernelGGL((k_gchol_update<STAGE, T>), dim3(tj, ti, st.B), dim3(256), 0, s, st, ws, k);
     }
     if (STAGE == 0) hipLaunchKernelGGL(k_gchol_a_store<T>, dim3(ld_chunks, st.B), dim3(256), 0, s, st, ws);
-    else hipLaunchKernelGGL(k_gchol_c_store<T>, dim3(ld_chunks, st.B), dim3(256), 0, s, st, ws);
 }
 
 // Register-tile stages A / C1 / C2 and E1 up to 32 cams (C <= 192); larger
