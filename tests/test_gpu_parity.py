@@ -342,8 +342,9 @@ def test_batched_fp64_vs_oracle(N, F, B, cap):
     34 (cap 36) -- the one-workgroup-per-tile-row k_info and the smallest
     global-memory Kalman window; 50 (cap 50: four staged features per k_info
     batch, cap 52: three) -- multi-workgroup assembly, global-memory Kalman stages A / C,
-    global-memory gating (fp64 LDS too small); 80 -- tracks longer
-    than 64 observations (two per lane in k_feature, cam masks beyond bit 63);
+    k_gate_mfma_wt on fp64 MFMA; 80 -- tracks longer than 64 observations (two
+    per lane in k_feature, cam masks beyond bit 63), the MFMA assembly over six
+    workgroups per filter (k_info_big);
     100 -- the longest tracks the reference chi2 table (dof <= 99,
     msckf.py:121-123) can gate."""
     problems = [synth.make_update_problem(N, F, seed=100 + b) for b in range(B)]

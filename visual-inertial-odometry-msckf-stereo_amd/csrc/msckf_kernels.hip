@@ -2110,6 +2110,257 @@ __global__ void __launch_bounds__(64 * IM_NW) k_info_mfma(DevState<T> st, FeatBa
 }
 
 // ---------------------------------------------------------------------------
+// Record-reading MFMA assembly for windows over 32 cams (round 6): the SYRK of
+// k_info_mfma, A = blockdiag_i(Hx_i^T Hx_i) - Gall^T Gall, on fp64 MFMA tiles
+// for up to 84 cams.  The lower 16 x 16 tiles of A are dealt over PARTS
+// workgroups per filter (IB_NW waves x IB_PPW tiles each, a filter's parts on
+// one XCD); every part stages the same chunks of IB_KF included features' G
+// rows from k_feature's Gram records (G and the cam of each record in one
+// fetch, issued under the previous chunk's MFMAs) and updates only its own
+// tiles, staging only the features that touch one of them.  The block-diagonal
+// terms are summed by the part that owns their tile, b by the part owning the
+// cam's diagonal tile.  A is stored as both triangles: stage B1 of the
+// global-memory Kalman path (k_kal_b1) reads whole rows of it.  (Replaces the
+// VALU 6 x 6 cam-pair assembly k_info there: 50x400 compress 8.3 ms.)
+// ---------------------------------------------------------------------------
+constexpr int IB_NW = 16, IB_PPW = 5, IB_KF = 8, IB_TPP = IB_NW * IB_PPW, IB_MAXN = 84;
+constexpr int IB_KMS = (3 * IB_KF / 4 + 1) & ~1;   // k-step masks (an even count: posc stays 8-byte aligned)
+// LDS row stride (doubles) of the staged Gall rows: >= 16 ceil(C / 16), = 16 mod 32 (as IM_GS)
+__host__ __device__ constexpr int ib_gs(int C) { return 32 * ((C + 15) / 32) + 16; }
+__host__ __device__ constexpr size_t info_big_lds(int Cmax, int maxnf) {
+    return (size_t)3 * IB_KF * ib_gs(Cmax) * sizeof(double) + IB_KMS * sizeof(unsigned) +
+           (size_t)(IB_MAXN * IB_KF + 4 * maxnf + 1) * sizeof(int);
+}
+int info_big_parts(int Cmax) {
+    const int TT = (Cmax + 15) / 16;
+    return (TT * (TT + 1) / 2 + IB_TPP - 1) / IB_TPP;
+}
+
+// NDO: (cam, element) pairs per thread, 27 Nmax <= NDO 64 IB_NW (2: up to 75 cams)
+template <typename T, int NDO>
+__global__ void __launch_bounds__(64 * IB_NW) k_info_big(DevState<T> st, FeatBatch<T> fb, UpdWs<T> ws, int maxnf) {
+    constexpr int NT = 64 * IB_NW, KF = IB_KF, KR = 3 * KF, NKS = KR / 4;
+    static_assert(KR % 4 == 0 && NKS <= IB_KMS && IB_MAXN * KF <= NT && 27 * IB_MAXN <= 3 * NT, "k_info_big shape");
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    const Blk3 bk = xcd_blk3();   // grid (parts, B): a filter's parts on one XCD
+    const int b = bk.y, part = bk.x;
+    const int tid = threadIdx.x, lane = tid & 63, lc = lane & 15, lr = lane >> 4;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    int* info = ws.info + 4 * b;
+    if (info[0] == 0) {   // nothing stacked: empty update
+        if (tid == 0 && part == 0) info[1] = 0;
+        return;
+    }
+    const int nc = st.ncams[b], C = 6 * nc, Cmax = ws.Cmax, GS = ib_gs(Cmax);
+    const int TT = (C + 15) >> 4, npair = TT * (TT + 1) / 2;
+    if (part * IB_TPP >= npair) {   // no tile of this window in this part (a smaller window)
+        if (tid == 0 && part == 0) info[1] = C;
+        return;
+    }
+    double* buf = reinterpret_cast<double*>(smem_raw);              // [KR][GS] dense rows of Gall
+    unsigned* kmask = reinterpret_cast<unsigned*>(buf + KR * GS);   // [NKS] tiles touched per k-step
+    int* posc = reinterpret_cast<int*>(kmask + IB_KMS);             // [KF][IB_MAXN] cam -> record (-1)
+    int* flist = posc + IB_MAXN * KF;                               // [maxnf] included features, in order
+    unsigned* ftm = reinterpret_cast<unsigned*>(flist + maxnf);     // [maxnf] their tile masks
+    int* fo0 = reinterpret_cast<int*>(ftm + maxnf);                 // [maxnf] first record
+    int* fM = fo0 + maxnf;                                          // [maxnf] records (0: not included)
+    int* s_n = fM + maxnf;
+    const int fbeg = fb.feat_off[b], fend = fb.feat_off[b + 1], nf = fend - fbeg;
+    // tile rows / columns of this part's tiles: a feature none of whose tile pairs
+    // falls in the part is not staged here at all
+    unsigned prow = 0, pcol = 0;
+    for (int p = part * IB_TPP; p < part * IB_TPP + IB_TPP && p < npair; ++p) {
+        int ti = 0;
+        while ((ti + 1) * (ti + 2) / 2 <= p) ++ti;
+        prow |= 1u << ti;
+        pcol |= 1u << (p - ti * (ti + 1) / 2);
+    }
+    unsigned* fmk = ftm;   // per feature first (index f), compacted to the list order below
+    for (int f = tid; f < nf; f += NT) {
+        const int a0 = fb.obs_off[fbeg + f], a1 = fb.obs_off[fbeg + f + 1];
+        const int M = fb.include[fbeg + f] ? a1 - a0 : 0;
+        unsigned m = 0;
+        for (int o = 0; o < M; ++o) {   // tile masks (<= 32 tile rows: C <= 512)
+            const int c = fb.obs_cam[a0 + o];
+            m |= (1u << ((6 * c) >> 4)) | (1u << ((6 * c + 5) >> 4));
+        }
+        fo0[f] = a0;
+        fM[f] = (m & prow) && (m & pcol) ? M : 0;
+        fmk[f] = m;
+    }
+    for (int e = tid; e < KR * GS; e += NT) buf[e] = 0.0;
+    for (int e = tid; e < IB_MAXN * KF; e += NT) posc[e] = -1;
+    __syncthreads();
+    if (wv == 0) {   // the included features of this part, in order
+        int base = 0;
+        for (int f0 = 0; f0 < nf; f0 += 64) {
+            const int f = f0 + lane;
+            const bool in = f < nf && fM[f] > 0;
+            const unsigned long long bal = __ballot(in);
+            if (in) flist[base + __popcll(bal & ((1ull << lane) - 1ull))] = f;
+            base += __popcll(bal);
+        }
+        if (lane == 0) *s_n = base;
+    }
+    __syncthreads();
+    const int nl = *s_n;
+    // ftm[i] (list order) overwrites fmk[f] (feature order) in place: i <= f, so read all first
+    unsigned mk[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int i = tid + NT * u;
+        mk[u] = i < nl ? fmk[flist[i]] : 0u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int i = tid + NT * u;
+        if (i < nl) ftm[i] = mk[u];
+    }
+    // (maxnf <= 4 NT: launch_compress)
+    // this wave's tiles: p = part IB_TPP + IB_PPW wv + q (lower, row-major order)
+    int pti[IB_PPW], ptj[IB_PPW];
+    bool pv[IB_PPW];
+    v4d acc[IB_PPW];
+#pragma unroll
+    for (int q = 0; q < IB_PPW; ++q) {
+        const int p = part * IB_TPP + IB_PPW * wv + q;
+        int ti = (int)((sqrtf(8.0f * (float)p + 1.0f) - 1.0f) * 0.5f);
+        while (ti * (ti + 1) / 2 > p) --ti;
+        while ((ti + 1) * (ti + 2) / 2 <= p) ++ti;
+        pti[q] = __builtin_amdgcn_readfirstlane(ti);
+        ptj[q] = __builtin_amdgcn_readfirstlane(p - ti * (ti + 1) / 2);
+        pv[q] = p < npair;
+        acc[q] = v4d{0.0, 0.0, 0.0, 0.0};
+    }
+    // (cam, element) pairs of the block diagonal (element < 21: packed lower DS) and
+    // b (21..26) this part sums: those whose element lies in one of its tiles
+    // (b: part 0)
+    int dco[NDO], drec[NDO];
+    double dsum[NDO];
+#pragma unroll
+    for (int u = 0; u < NDO; ++u) {
+        const int e = tid + NT * u, dc = e / 27, de = e - 27 * dc;
+        bool own = false;
+        if (e < 27 * nc) {
+            if (de < 21) {
+                int x = 0;
+                while ((x + 1) * (x + 2) / 2 <= de) ++x;
+                const int y = de - x * (x + 1) / 2, ti = (6 * dc + x) >> 4, tj = (6 * dc + y) >> 4;
+                own = (ti * (ti + 1) / 2 + tj) / IB_TPP == part;
+            } else {   // b of cam dc: the part of its diagonal tile (every feature seeing dc is staged there)
+                const int t = (6 * dc) >> 4;
+                own = (t * (t + 1) / 2 + t) / IB_TPP == part;
+            }
+        }
+        dco[u] = own ? dc : -1;
+        drec[u] = de < 21 ? OBG_DS + de : OBG_UB + (de - 21);
+        dsum[u] = 0.0;
+    }
+    // staging slot: chunk feature ss, its record so
+    const int ss = tid / IB_MAXN, so = tid - IB_MAXN * (tid / IB_MAXN);
+    double g[18];
+    int gcol = -1, gcam = 0;
+    auto fetch = [&](int l0) {
+        gcol = -1;
+        if (tid < IB_MAXN * KF && l0 + ss < nl) {
+            const int f = flist[l0 + ss];
+            if (so < fM[f]) {
+                const double* r = fb.obs_g + (size_t)(fo0[f] + so) * OBG_STRIDE;
+#pragma unroll
+                for (int k = 0; k < 18; ++k) g[k] = r[OBG_G + k];
+                gcam = (int)r[OBG_CAM];
+                gcol = 6 * gcam;
+            }
+        }
+    };
+    __syncthreads();   // ftm complete
+    fetch(0);
+    for (int l0 = 0; l0 < nl; l0 += KF) {
+        // ---- stage the chunk (buf is all zero, posc all -1 here) ----
+        const int mycol = gcol, mycam = gcam;
+        if (mycol >= 0) {
+#pragma unroll
+            for (int r = 0; r < 3; ++r)
+#pragma unroll
+                for (int u = 0; u < 6; ++u) buf[(3 * ss + r) * GS + mycol + u] = g[6 * r + u];
+            posc[IB_MAXN * ss + mycam] = so;
+        }
+        for (int k = tid; k < NKS; k += NT) {
+            unsigned m = 0;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = l0 + (4 * k + r) / 3;
+                if (i < nl) m |= ftm[i];
+            }
+            kmask[k] = m;
+        }
+        __syncthreads();
+        fetch(l0 + KF);   // the next chunk's G blocks, under this chunk's MFMAs
+        // ---- rank-KR update of this wave's tiles ----
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+            const unsigned km = kmask[ks];
+            const double* brow = buf + (4 * ks + lr) * GS + lc;
+#pragma unroll
+            for (int q = 0; q < IB_PPW; ++q)
+                if (pv[q] && ((km >> pti[q]) & (km >> ptj[q]) & 1u))
+                    acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(brow[16 * pti[q]], brow[16 * ptj[q]], acc[q], 0, 0, 0);
+        }
+        // block-diagonal / b terms of the chunk (after the MFMAs: no registers held across them)
+#pragma unroll
+        for (int u = 0; u < NDO; ++u)
+#pragma unroll
+            for (int s = 0; s < KF; ++s)
+                if (dco[u] >= 0 && l0 + s < nl) {
+                    const int o = posc[IB_MAXN * s + dco[u]];
+                    if (o >= 0) dsum[u] += fb.obs_g[(size_t)(fo0[flist[l0 + s]] + o) * OBG_STRIDE + drec[u]];
+                }
+        __syncthreads();
+        // ---- back to all-zero rows / empty table; a feature slot's 84 records span
+        // two waves, so the next chunk's scatter waits for every clear (barrier) ----
+        if (mycol >= 0) {
+#pragma unroll
+            for (int r = 0; r < 3; ++r)
+#pragma unroll
+                for (int u = 0; u < 6; ++u) buf[(3 * ss + r) * GS + mycol + u] = 0.0;
+            posc[IB_MAXN * ss + mycam] = -1;
+        }
+        __syncthreads();
+    }
+    KT* F = ws.Hthin + (size_t)b * Cmax * (Cmax + 1);
+    const int ldf = Cmax + 1;
+#pragma unroll
+    for (int q = 0; q < IB_PPW; ++q) {
+        if (!pv[q]) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int row = 16 * pti[q] + lr + 4 * r, col = 16 * ptj[q] + lc;
+            if (row < C && col < C) {   // both triangles (a diagonal tile holds both already)
+                F[(size_t)row * ldf + col] = -acc[q][r];
+                if (pti[q] != ptj[q]) F[(size_t)col * ldf + row] = -acc[q][r];
+            }
+        }
+    }
+    __syncthreads();   // the tiles' stores are visible to the block-diagonal owners
+#pragma unroll
+    for (int u = 0; u < NDO; ++u) {
+        if (dco[u] < 0) continue;
+        const int dc = dco[u], de = drec[u] < OBG_UB ? drec[u] - OBG_DS : 21 + drec[u] - OBG_UB;
+        if (de < 21) {
+            int x = 0;
+            while ((x + 1) * (x + 2) / 2 <= de) ++x;
+            const int y = de - x * (x + 1) / 2;
+            F[(size_t)(6 * dc + x) * ldf + 6 * dc + y] += dsum[u];
+            if (x != y) F[(size_t)(6 * dc + y) * ldf + 6 * dc + x] += dsum[u];
+        } else {
+            F[(size_t)(6 * dc + de - 21) * ldf + Cmax] = dsum[u];
+        }
+    }
+    if (tid == 0 && part == 0) info[1] = C;
+}
+
+// ---------------------------------------------------------------------------
 // Fused information assembly (windows up to 32 cams): k_info_mfma's SYRK
 // without the per-observation Gram records.  Each staged feature's G_i,
 // Hx_i^T Hx_i and UB_i are rebuilt in the workgroup from the inputs -- the
@@ -2823,6 +3074,22 @@ void launch_compress(hipStream_t s, const DevState<T>& st, const Params<T>& prm,
     if (st.Nmax <= 32 && maxobs > 0 && lds_m <= 160 * 1024) {
         lds_limit((const void*)k_info_mfma<T>, lds_m);
         hipLaunchKernelGGL((k_info_mfma<T>), dim3(st.B), dim3(64 * IM_NW), lds_m, s, st, fb, ws, maxnf, maxobs);
+        return;
+    }
+    // windows of four or more k_info_big parts (over ~58 cams, up to 84): fp64 MFMA
+    // tiles over several workgroups per filter.  (80x1000: compress 13.7 -> 12.1 ms;
+    // at 50 cams, three parts, it measured 9.0 ms against 8.3 for k_info and is not
+    // used there -- profiles/r06/info_big/)
+    const size_t lds_b = info_big_lds(ws.Cmax, maxnf);
+    if (info_big_parts(ws.Cmax) >= 4 && st.Nmax <= IB_MAXN && maxnf <= 4 * 64 * IB_NW && lds_b <= 160 * 1024) {
+        const dim3 grid(info_big_parts(ws.Cmax), st.B);
+        if (27 * st.Nmax <= 2 * 64 * IB_NW) {
+            lds_limit((const void*)k_info_big<T, 2>, lds_b);
+            hipLaunchKernelGGL((k_info_big<T, 2>), grid, dim3(64 * IB_NW), lds_b, s, st, fb, ws, maxnf);
+        } else {
+            lds_limit((const void*)k_info_big<T, 3>, lds_b);
+            hipLaunchKernelGGL((k_info_big<T, 3>), grid, dim3(64 * IB_NW), lds_b, s, st, fb, ws, maxnf);
+        }
         return;
     }
     // one wave per 8 x 8 tile of cam pairs
