@@ -512,40 +512,45 @@ size_t kalman_global_ws_doubles(int Cmax) {   // per filter, 0 when the register
 // ===========================================================================
 constexpr int GT = 64, GK = 16, GPAD = 80;
 
-template <bool A_KFAST, bool B_KFAST, class FA, class FB, class FS>
-__device__ __forceinline__ void gemm64(int m, int n, int kb, int ke, int i0, int j0, FA A, FB B, FS store) {
-    // double-buffered K chunks: chunk c + 1's global loads are in flight (in
-    // registers) under chunk c's MFMAs, one barrier per chunk (round 6; the
-    // single-buffered loop exposed every chunk's load latency)
-    __shared__ __attribute__((aligned(16))) double sa[2][GK][GPAD], sb[2][GK][GPAD];
+// TM x TM output tile per 256-thread workgroup (TM = 64 or 128): the four waves in
+// 2 x 2, each TM/2 square as (TM/32)^2 v_mfma_f64_16x16x4f64 blocks.
+// Double-buffered K chunks: chunk c + 1's global loads are in flight (in
+// registers) under chunk c's MFMAs, one barrier per chunk (round 6; the
+// single-buffered loop exposed every chunk's load latency).
+template <int TM, bool A_KFAST, bool B_KFAST, class FA, class FB, class FS>
+__device__ __forceinline__ void gemm_tile(int m, int n, int kb, int ke, int i0, int j0, FA A, FB B, FS store) {
+    constexpr int NBW = TM / 32, NLD = TM * GK / 256, PAD = TM + 16, HW = TM / 2;
+    __shared__ __attribute__((aligned(16))) double sa[2][GK][PAD], sb[2][GK][PAD];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int wr = w >> 1, wc = w & 1, lc = lane & 15, lr = lane >> 4;
-    v4d acc[2][2];
+    v4d acc[NBW][NBW];
 #pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
+    for (int mi = 0; mi < NBW; ++mi)
 #pragma unroll
-        for (int ni = 0; ni < 2; ++ni) acc[mi][ni] = v4d{0.0, 0.0, 0.0, 0.0};
-    double ra[4], rb[4];
+        for (int ni = 0; ni < NBW; ++ni) acc[mi][ni] = v4d{0.0, 0.0, 0.0, 0.0};
+    double ra[NLD], rb[NLD];
+    auto idx = [&](int q, bool kfast, int& r, int& kk) {
+        const int e = tid + 256 * q;
+        if (kfast) { r = e >> 4; kk = e & 15; } else { r = e % TM; kk = e / TM; }
+    };
     auto gload = [&](int k0) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int e = tid + 256 * q;
+        for (int q = 0; q < NLD; ++q) {
             int ii, kk, jj, k2;
-            if (A_KFAST) { ii = e >> 4; kk = e & 15; } else { ii = e & 63; kk = e >> 6; }
+            idx(q, A_KFAST, ii, kk);
+            idx(q, B_KFAST, jj, k2);
             const int gi = i0 + ii, gk = k0 + kk;
             ra[q] = (gi < m && gk < ke) ? A(gi, gk) : 0.0;
-            if (B_KFAST) { jj = e >> 4; k2 = e & 15; } else { jj = e & 63; k2 = e >> 6; }
             const int gj = j0 + jj, gk2 = k0 + k2;
             rb[q] = (gj < n && gk2 < ke) ? B(gk2, gj) : 0.0;
         }
     };
     auto sstore = [&](int bf) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int e = tid + 256 * q;
+        for (int q = 0; q < NLD; ++q) {
             int ii, kk, jj, k2;
-            if (A_KFAST) { ii = e >> 4; kk = e & 15; } else { ii = e & 63; kk = e >> 6; }
-            if (B_KFAST) { jj = e >> 4; k2 = e & 15; } else { jj = e & 63; k2 = e >> 6; }
+            idx(q, A_KFAST, ii, kk);
+            idx(q, B_KFAST, jj, k2);
             sa[bf][kk][ii] = ra[q];
             sb[bf][k2][jj] = rb[q];
         }
@@ -562,30 +567,34 @@ __device__ __forceinline__ void gemm64(int m, int n, int kb, int ke, int i0, int
 #pragma unroll
         for (int kc = 0; kc < GK / 4; ++kc) {
             const int kr = 4 * kc + lr;
-            double av[2], bv[2];
+            double av[NBW], bv[NBW];
 #pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                av[t] = sa[bf][kr][32 * wr + 16 * t + lc];
-                bv[t] = sb[bf][kr][32 * wc + 16 * t + lc];
+            for (int t = 0; t < NBW; ++t) {
+                av[t] = sa[bf][kr][HW * wr + 16 * t + lc];
+                bv[t] = sb[bf][kr][HW * wc + 16 * t + lc];
             }
 #pragma unroll
-            for (int mi = 0; mi < 2; ++mi)
+            for (int mi = 0; mi < NBW; ++mi)
 #pragma unroll
-                for (int ni = 0; ni < 2; ++ni)
+                for (int ni = 0; ni < NBW; ++ni)
                     acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[mi], bv[ni], acc[mi][ni], 0, 0, 0);
         }
         if (more) sstore(bf ^ 1);
         __syncthreads();
     }
 #pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
+    for (int mi = 0; mi < NBW; ++mi)
 #pragma unroll
-        for (int ni = 0; ni < 2; ++ni)
+        for (int ni = 0; ni < NBW; ++ni)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int i = i0 + 32 * wr + 16 * mi + lr + 4 * r, j = j0 + 32 * wc + 16 * ni + lc;
+                const int i = i0 + HW * wr + 16 * mi + lr + 4 * r, j = j0 + HW * wc + 16 * ni + lc;
                 if (i < m && j < n) store(i, j, acc[mi][ni][r]);
             }
+}
+template <bool A_KFAST, bool B_KFAST, class FA, class FB, class FS>
+__device__ __forceinline__ void gemm64(int m, int n, int kb, int ke, int i0, int j0, FA A, FB B, FS store) {
+    gemm_tile<64, A_KFAST, B_KFAST>(m, n, kb, ke, i0, j0, A, B, store);
 }
 
 template <int STAGE, typename T>
@@ -853,14 +862,15 @@ __global__ void __launch_bounds__(64 * NW) k_kal_b(DevState<T> st, Params<T> prm
 
 // ---- stage E: P+ = blockdiag(S_ii, 0) + s2 W W^T (lower tiles, mirrored), dx = W y ----
 template <typename T>
-__global__ void __launch_bounds__(256) k_kal_e(DevState<T> st, Params<T> prm, UpdWs<T> ws) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) k_kal_e(DevState<T> st, Params<T> prm, UpdWs<T> ws) {
+    constexpr int TE = 128;   // output tile (round 6: 64 -> 128, twice the operand reuse per chunk)
     const Blk3 bk = xcd_blk3();
     const int b = bk.z;
     if (ws.info[4 * b] == 0 || ws.info[4 * b + 3] < 0) return;
     const int C = 6 * st.ncams[b], D = 21 + C;
-    const int i0 = bk.y * GT, j0 = bk.x * GT;
+    const int i0 = bk.y * TE, j0 = bk.x * TE;
     if (i0 >= D || j0 > D) return;
-    if (j0 > i0 + GT - 1 && !(D >= j0 && D < j0 + GT)) return;
+    if (j0 > i0 + TE - 1 && !(D >= j0 && D < j0 + TE)) return;
     const int ld = st.Dmax;
     // W: stage C's solved extra rows [Vc_i ; Lc ; c^T] L_T^-T, in place after T (ld C)
     const KT* W = ws.Wk + (size_t)b * ws.wk_stride + gchol_c_off(ws.Cmax) + (size_t)C * C;
@@ -868,7 +878,7 @@ __global__ void __launch_bounds__(256) k_kal_e(DevState<T> st, Params<T> prm, Up
     T* P = st.P + (size_t)b * st.Dmax * st.Dmax;
     KT* dx = ws.dx + (size_t)b * (st.Dmax + ws.Cmax);
     const double s2 = (double)prm.sigma2;
-    gemm64<true, true>(D, D + 1, 0, C, i0, j0, [&](int i, int k) { return W[(size_t)i * C + k]; },
+    gemm_tile<TE, true, true>(D, D + 1, 0, C, i0, j0, [&](int i, int k) { return W[(size_t)i * C + k]; },
                        [&](int k, int j) { return W[(size_t)(j < D ? j : D) * C + k]; },
                        [&](int i, int j, double v) {
                            if (j < D && j <= i) {
@@ -1401,7 +1411,7 @@ void launch_kalman_chol(hipStream_t s, const DevState<T>& st, const Params<T>& p
     } else if (reg) {
         launch_e1<T, 8, 16>(s, st, prm, ws, ldsE);
     } else {   // large windows: one 64 x 64 tile per workgroup
-        const int dt = (st.Dmax + GT - 1) / GT, dt1 = (st.Dmax + 1 + GT - 1) / GT;
+        const int dt = (st.Dmax + 127) / 128, dt1 = (st.Dmax + 1 + 127) / 128;
         hipLaunchKernelGGL(k_kal_e<T>, dim3(dt1, dt, st.B), dim3(256), 0, s, st, prm, ws);
     }
     kt->end(s);
