@@ -510,7 +510,7 @@ size_t kalman_global_ws_doubles(int Cmax) {   // per filter, 0 when the register
 // memory for that operand (selects the coalesced load mapping).  store(i, j, v)
 // receives every in-range output element once.
 // ===========================================================================
-constexpr int GT = 64, GK = 16, GPAD = 80;
+constexpr int GT = 64, GK = 16;
 
 // TM x TM output tile per 256-thread workgroup (TM = 64 or 128): the four waves in
 // 2 x 2, each TM/2 square as (TM/32)^2 v_mfma_f64_16x16x4f64 blocks.
