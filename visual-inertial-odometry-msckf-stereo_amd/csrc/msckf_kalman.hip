@@ -351,7 +351,15 @@ __device__ __forceinline__ bool gdims(const DevState<T>& st, const UpdWs<T>& ws,
     return true;
 }
 
-// 1. factor the diagonal block A[k:k+nb, k:k+nb] in place (one wave per filter)
+// 1. factor the diagonal block A[k:k+nb, k:k+nb] in place (one wave per
+// filter).  Lane i holds row i in registers; per pivot j the pivot comes from
+// lane j (readlane), lane i scales its L[i][j] and publishes it to a 64-double
+// LDS column, and every lane updates its row right-looking, x[c] -= L[i][j]
+// L[c][j] (c > j, the column read as an LDS broadcast) -- the element-wise
+// right-looking order of the round-2 kernel (same operations, same results),
+// without its per-element LDS read-modify-writes and three barriers per pivot
+// (round 6).  The entries right of a
+// lane's diagonal collect garbage from those updates and are never stored.
 template <int STAGE, typename T>
 __global__ void __launch_bounds__(64) k_gchol_diag(DevState<T> st, UpdWs<T> ws, int k) {
     const int b = blockIdx.x;
@@ -359,11 +367,16 @@ __global__ void __launch_bounds__(64) k_gchol_diag(DevState<T> st, UpdWs<T> ws, 
     int nrow, ncol, nelim;
     if (!gdims<STAGE>(st, ws, b, A, nrow, ncol, nelim) || k >= nelim) return;
     const int ld = ncol, nb = nelim - k < GNB ? nelim - k : GNB;
-    __shared__ double d[GNB][GNB + 1];
+    __shared__ double colj[2][GNB];
+    __shared__ double lt[GNB * (GNB + 1) / 2];   // L_kk^T, packed by columns of L
     const int lane = threadIdx.x;
-    for (int e = lane; e < nb * nb; e += 64) {
-        const int i = e / nb, j = e - i * nb;
-        d[i][j] = j <= i ? A[(size_t)(k + i) * ld + k + j] : 0.0;
+    // row lane of the block's lower part (zeros right of the diagonal and past nb),
+    // every load in flight before the first use
+    double x[GNB];
+    {
+        const KT* src = A + (size_t)(k + lane) * ld + k;
+#pragma unroll
+        for (int j = 0; j < GNB; ++j) x[j] = (lane < nb && j <= lane) ? src[j] : (j == lane ? 1.0 : 0.0);
     }
     // stage A: pivots floored as in k_kal_a (pcc_pivot_floor); stage C: at s2 down
     // to -T_FLOOR_NEG x max diag(T), as k_kal_c1 / k_kal_mchol (stage B2 keeps
@@ -381,64 +394,71 @@ __global__ void __launch_bounds__(64) k_gchol_diag(DevState<T> st, UpdWs<T> ws, 
         for (int i = lane; i < nelim; i += 64) tmax = fmax(tmax, (double)Tm[(size_t)i * ldt + i]);
         lo = -T_FLOOR_NEG * wave_max(tmax);
     }
-    __syncthreads();
     bool bad = false;
-    for (int j = 0; j < nb; ++j) {   // right-looking, lane i owns row i
-        double piv = d[j][j];
-        piv = pivot_floored(piv, floor, lo);
-        if (!(piv > 0.0)) { bad = true; break; }
-        const double l = sqrt(piv), inv = 1.0 / l;
-        __syncthreads();
-        if (lane == j) d[j][j] = l;
-        if (lane > j && lane < nb) d[lane][j] *= inv;
-        __syncthreads();
-        if (lane > j && lane < nb) {
-            const double lij = d[lane][j];
-            for (int c = j + 1; c <= lane; ++c) d[lane][c] -= lij * d[c][j];
+#pragma unroll
+    for (int j = 0; j < GNB; ++j) {
+        if (j >= nb || bad) continue;   // uniform
+        const double piv = pivot_floored(lane_bcast(x[j], j), floor, lo);
+        if (!(piv > 0.0)) {
+            bad = true;
+            continue;
         }
-        __syncthreads();
+        const double l = sqrt(piv), inv = 1.0 / l;
+        const double lij = lane == j ? l : x[j] * inv;
+        x[j] = lij;
+        double* cj = colj[j & 1];
+        cj[lane] = lij;
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+#pragma unroll
+        for (int c = j + 1; c < GNB; ++c) x[c] -= lij * cj[c];
     }
     if (bad) {
         if (lane == 0) ws.info[4 * b + 3] = STAGE == 0 ? -2 : -1;
         return;
     }
-    for (int e = lane; e < nb * nb; e += 64) {
-        const int i = e / nb, j = e - i * nb;
-        if (j <= i) A[(size_t)(k + i) * ld + k + j] = d[i][j];
-    }
-}
-
-// 2. panel rows i >= k + nb: A[i, k:k+nb] <- A[i, k:k+nb] L_kk^-T (one row per thread)
-template <int STAGE, typename T>
-__global__ void __launch_bounds__(256) k_gchol_trsm(DevState<T> st, UpdWs<T> ws, int k) {
-    const Blk3 bk = xcd_blk3();
-    const int b = bk.y;
-    KT* A;
-    int nrow, ncol, nelim;
-    if (!gdims<STAGE>(st, ws, b, A, nrow, ncol, nelim) || k >= nelim) return;
-    const int ld = ncol, nb = nelim - k < GNB ? nelim - k : GNB;
-    const int i = k + nb + bk.x * 256 + threadIdx.x;
-    if (k + nb + bk.x * 256 >= nrow) return;
-    __shared__ double L[GNB][GNB + 1];
-    for (int e = threadIdx.x; e < nb * nb; e += 256) {
-        const int r = e / nb, c = e - r * nb;
-        L[r][c] = c <= r ? A[(size_t)(k + r) * ld + k + c] : 0.0;
-    }
-    __syncthreads();
-    if (i >= nrow) return;
-    KT* row = A + (size_t)i * ld + k;
-    double x[GNB];
+    if (lane < nb) {
+        KT* dst = A + (size_t)(k + lane) * ld + k;
 #pragma unroll
-    for (int j = 0; j < GNB; ++j) {
-        double v = j < nb ? row[j] : 0.0;
-#pragma unroll
-        for (int p = 0; p < j; ++p) v -= x[p] * L[j][p];
-        x[j] = j < nb ? v / L[j][j] : 0.0;
+        for (int j = 0; j < GNB; ++j)
+            if (j <= lane) dst[j] = x[j];
     }
+    // L_kk^-1 for k_gchol_trsm: L's columns to LDS (column j packed from its
+    // diagonal down, unit rows past nb), then lane j solves column j of L Y = I
+    // right-looking (each pivot's column read as an LDS broadcast run); Y goes
+    // row-major into the G workspace, which stage B1 fills only after stage A
+    // and stage B2 has consumed before stage C
+    auto lcol = [](int j) { return j * GNB - j * (j - 1) / 2; };   // offset of L[j][j]
 #pragma unroll
     for (int j = 0; j < GNB; ++j)
-        if (j < nb) row[j] = x[j];
+        if (j <= lane) lt[lcol(j) + lane - j] = x[j];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    double* rdg = colj[0];
+    rdg[lane] = 1.0 / lt[lcol(lane)];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+#pragma unroll
+    for (int i = 0; i < GNB; ++i) x[i] = i == lane ? 1.0 : 0.0;
+#pragma unroll
+    for (int i = 0; i < GNB; ++i) {
+        const double yi = x[i] * rdg[i];
+        x[i] = yi;
+#pragma unroll
+        for (int r = i + 1; r < GNB; ++r) x[r] -= yi * lt[lcol(i) + r - i];
+    }
+    KT* Li = ws.G + (size_t)b * ws.Cmax * (ws.Cmax + 1);
+#pragma unroll
+    for (int i = 0; i < GNB; ++i) Li[i * GNB + lane] = x[i];
 }
+
+// 2. panel rows i >= k + nb: A[i, k:k+nb] <- A[i, k:k+nb] L_kk^-T, one 64-row
+// tile per workgroup on the matrix cores (gemm64 below) against the inverse
+// k_gchol_diag left in the G workspace.  In place: a tile reads all of its rows'
+// panel columns before its store.  (The round-2 kernel solved one row per
+// thread from per-lane strided row reads: 0.66 ms per stage-C launch at 50x400.)
+template <int STAGE, typename T>
+__global__ void __launch_bounds__(256) k_gchol_trsm(DevState<T> st, UpdWs<T> ws, int k);
 
 // stage A workspace in / out (grid-stride over the N x N lower part, blockIdx.y = filter)
 template <typename T>
@@ -595,6 +615,23 @@ __device__ __forceinline__ void gemm_tile(int m, int n, int kb, int ke, int i0, 
 template <bool A_KFAST, bool B_KFAST, class FA, class FB, class FS>
 __device__ __forceinline__ void gemm64(int m, int n, int kb, int ke, int i0, int j0, FA A, FB B, FS store) {
     gemm_tile<64, A_KFAST, B_KFAST>(m, n, kb, ke, i0, j0, A, B, store);
+}
+
+template <int STAGE, typename T>
+__global__ void __launch_bounds__(256) k_gchol_trsm(DevState<T> st, UpdWs<T> ws, int k) {
+    const Blk3 bk = xcd_blk3();
+    const int b = bk.y;
+    KT* A;
+    int nrow, ncol, nelim;
+    if (!gdims<STAGE>(st, ws, b, A, nrow, ncol, nelim) || k >= nelim) return;
+    const int ld = ncol, nb = nelim - k < GNB ? nelim - k : GNB;
+    const int i0 = k + nb + bk.x * GT;
+    if (i0 >= nrow) return;
+    const KT* Li = ws.G + (size_t)b * ws.Cmax * (ws.Cmax + 1);   // L_kk^-1, row-major GNB x GNB
+    gemm64<true, true>(nrow, nb, 0, nb, i0, 0,
+                       [&](int i, int p) { return A[(size_t)i * ld + k + p]; },
+                       [&](int p, int j) { return Li[j * GNB + p]; },
+                       [&](int i, int j, double v) { A[(size_t)i * ld + k + j] = v; });
 }
 
 template <int STAGE, typename T>
@@ -1268,7 +1305,7 @@ static void launch_gchol(hipStream_t s, const DevState<T>& st, const UpdWs<T>& w
         // them for nb >= 1; blocks past a filter's matrix exit at once
         const int rows = nrow - k - 1;
         if (rows > 0)
-            hipLaunchKernelGGL((k_gchol_trsm<STAGE, T>), dim3((rows + 255) / 256, st.B), dim3(256), 0, s, st, ws, k);
+            hipLaunchKernelGGL((k_gchol_trsm<STAGE, T>), dim3((rows + GT - 1) / GT, st.B), dim3(256), 0, s, st, ws, k);
         const int ti = (rows + GT - 1) / GT, tj = (ncol - k - 1 + GT - 1) / GT;
         if (rows > 0 && tj > 0)
             hipLaunchKernelGGL((k_gchol_update<STAGE, T>), dim3(tj, ti, st.B), dim3(256), 0, s, st, ws, k);
