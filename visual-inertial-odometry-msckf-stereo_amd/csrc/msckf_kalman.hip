@@ -739,11 +739,16 @@ __global__ void __launch_bounds__(64 * NW) k_kal_b(DevState<T> st, Params<T> prm
     const KT* Lc = ws.Lc + (size_t)b * Cpw * Cpw;
     KT* G = ws.G + (size_t)b * ws.Cmax * ld;
     KT* Tm = ws.Tm + (size_t)b * ws.Cmax * ld;
-    // LDS images [2 buf][2 op][16][CqS], then [2][16] b chunk; the row stride
-    // CqS = Cq + 2 keeps the column-gathered writes of phase 1 conflict-free
-    const int CqS = Cq + 2;
+    // LDS images [2 buf][2 op][16][CqS], then [2][16] b chunk.  Row strides
+    // (ds_read_b64 banks are (a/4) % 64 per 32-lane half = two k rows of 16
+    // doubles): phase 1 uses CqS = 17 (mod 32) -- its column-gathered writes
+    // step 34 dwords across lanes (conflict-free on 32 write banks) and the two
+    // rows of a read half overlap on 2 banks only (Cq + 2 overlapped 28 of
+    // them for even nT); phase 2's writes are row-contiguous, so it takes
+    // CqS = 16 (mod 32) and its read halves are disjoint.
+    const int CqS1 = (Cq & ~31) + 17, CqS2 = (Cq & ~31) + 16;
     double* img = reinterpret_cast<double*>(smem_raw);
-    double* bb = img + 4 * 16 * CqS;
+    double* bb = img + 4 * 16 * CqS1;
     // operand 0 = rows of X (A in phase 1, Lc in phase 2), operand 1 = rows of Y (Lc, G).
     // load() issues the next chunk's global reads into registers before the
     // MFMAs of the current one; put() writes them to the other LDS buffer after.
@@ -768,7 +773,7 @@ __global__ void __launch_bounds__(64 * NW) k_kal_b(DevState<T> st, Params<T> prm
                 c = e - k * Cq;
             }
             const int gk = k0 + k;
-            pos[q] = k * CqS + c;
+            pos[q] = k * (ph == 0 ? CqS1 : CqS2) + c;
             const bool in = e < 16 * Cq && gk < C && c < C;
             const double lcv = (in && c <= gk) ? Lc[(size_t)gk * Cpw + c] : 0.0;
             double ov;
@@ -783,6 +788,7 @@ __global__ void __launch_bounds__(64 * NW) k_kal_b(DevState<T> st, Params<T> prm
         if (ph == 1 && tid < 16) rb = k0 + tid < C ? Am[(size_t)(k0 + tid) * ld + ws.Cmax] : 0.0;
     };
     auto put = [&](int ph, int buf) {
+        const int CqS = ph == 0 ? CqS1 : CqS2;
         double* i0 = img + (2 * buf) * 16 * CqS;
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
@@ -796,6 +802,7 @@ __global__ void __launch_bounds__(64 * NW) k_kal_b(DevState<T> st, Params<T> prm
     };
     // ---- phase 1: the lower tiles of G = A Lc ----
     {
+        const int CqS = CqS1;
         const int ntl = nT * (nT + 1) / 2;
         v4d acc[TP2];
         int gr[TP2], gc[TP2];
@@ -843,6 +850,7 @@ __global__ void __launch_bounds__(64 * NW) k_kal_b(DevState<T> st, Params<T> prm
     }
     // ---- phase 2: T = s2 I + Lc^T G (lower), c = Lc^T b ----
     {
+        const int CqS = CqS2;
         const int ntl = nT * (nT + 1) / 2;
         v4d acc[TP2];
         int ti[TP2], tj[TP2];
@@ -1412,9 +1420,9 @@ void launch_kalman_chol(hipStream_t s, const DevState<T>& st, const Params<T>& p
     }
     kt->begin(s, "kalman_b");
     if (Cq <= 16 * 8) {
-        launch_b<T, 8, 8>(s, st, prm, ws, (4 * 16 * (size_t)(Cq + 2) + 32) * sizeof(double));
+        launch_b<T, 8, 8>(s, st, prm, ws, (4 * 16 * (size_t)(Cq + 17) + 32) * sizeof(double));
     } else if (Cq <= 16 * 12) {
-        launch_b<T, 16, 12>(s, st, prm, ws, (4 * 16 * (size_t)(Cq + 2) + 32) * sizeof(double));
+        launch_b<T, 16, 12>(s, st, prm, ws, (4 * 16 * (size_t)(Cq + 17) + 32) * sizeof(double));
     } else {   // large windows: 64 x 64 output tiles, one workgroup each
         const int tiles = (Cmax + GT - 1) / GT;
         hipLaunchKernelGGL(k_kal_b1<T>, dim3(tiles, tiles, st.B), dim3(256), 0, s, st, ws);
