@@ -362,12 +362,16 @@ def test_batched_fp64_vs_oracle(N, F, B, cap):
 
 
 @pytest.mark.parametrize("kal", ["mfma", "tiles"])
-@pytest.mark.parametrize("N,F,B,cap", [(30, 200, 2, 30), (32, 80, 1, None), (20, 120, 3, None)])
+@pytest.mark.parametrize("N,F,B,cap", [(30, 200, 2, 30), (32, 80, 1, None), (20, 120, 3, None),
+                                       (13, 60, 2, None), (27, 100, 2, None)])
 def test_kalman_cholesky_paths_vs_oracle(kal, N, F, B, cap, monkeypatch):
     """Both implementations of the Kalman stages A / C1 on the same inputs
     (MSCKF_KALMAN_CHOL forces one; by default batches of >= 64 filters take
     the fp64 MFMA partial Cholesky k_kal_mchol, smaller ones the register
-    tiles of msckf_rchol.h): fp64 context against the oracle, P <= 1e-9."""
+    tiles of msckf_rchol.h): fp64 context against the oracle, P <= 1e-9.
+    N = 13 / 27 give odd 16-column tile counts (C = 78 / 162: 5 / 11 tiles) on
+    k_kal_b's two launch shapes (8 and 16 waves), whose LDS row strides depend
+    on that parity."""
     monkeypatch.setenv("MSCKF_KALMAN_CHOL", kal)
     problems = [synth.make_update_problem(N, F, seed=300 + b) for b in range(B)]
     ctx, ds, feat_off, acc, gam, pw, valid, rows = _batched(problems, np.float64, cap=cap)
